@@ -1,0 +1,83 @@
+"""ctypes binding of libfdhip.so (include/fd_hip.h). No fallback: a missing library raises."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libfdhip.so")
+CSRC = os.path.join(HERE, "csrc")
+
+FD_OK, FD_ERR_INVALID, FD_ERR_HIP, FD_ERR_CAPACITY = 0, 1, 2, 3
+FD_HARRIS, FD_SHI_TOMASI, FD_FAST = 0, 1, 2
+
+# Every symbol include/fd_hip.h declares (checked by tests/test_capi_symbols.py).
+EXPORTS = (
+    "fd_ctx_create", "fd_ctx_destroy", "fd_last_error", "fd_ctx_set_stream", "fd_ctx_use_own_stream",
+    "fd_ctx_get_stream",
+    "fd_ctx_synchronize", "fd_ctx_reserve", "fd_points_detect", "fd_points_candidates", "fd_points_response",
+    "fd_lsd_map",
+    "fd_build_info",
+)
+
+
+class FdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libfdhip error {code}: {msg}")
+        self.code = code
+
+
+class fd_point_opts(ctypes.Structure):
+    _fields_ = [("min_feature_distance", ctypes.c_int32), ("min_valid_response", ctypes.c_float)]
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libfdhip.so from the package's lib/ directory (built by __graft_entry__.build())."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                          f"or `make -C {CSRC}`; there is no CPU fallback")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (soname libamdhip64.so.7,
+    # the same as /opt/rocm's). Loading torch first makes libfdhip bind to that copy, so device
+    # pointers, streams and events are shared with torch; without torch, /opt/rocm's runtime is used.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    P, i32, i64, u32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32, ctypes.c_float
+    sig = {
+        "fd_ctx_create": (i32, [i32, ctypes.POINTER(P)]),
+        "fd_ctx_destroy": (None, [P]),
+        "fd_last_error": (ctypes.c_char_p, [P]),
+        "fd_ctx_set_stream": (i32, [P, P]),
+        "fd_ctx_use_own_stream": (i32, [P]),
+        "fd_ctx_get_stream": (P, [P]),
+        "fd_ctx_synchronize": (i32, [P]),
+        "fd_ctx_reserve": (i32, [P, i32, i32, i32, i32, i64]),
+        "fd_points_detect": (i32, [P, i32, P, i32, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, u32, P, i32,
+                                   P, i32]),
+        "fd_points_candidates": (i32, [P, i32, P, i32, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, P, P, P,
+                                       i64, P, P, i32]),
+        "fd_points_response": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, i64, P]),
+        "fd_lsd_map": (i32, [P, P, i32, i32, i32, i32, f32, P, P, P, P, i64, P, i32]),
+        "fd_build_info": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(ctx_ptr, rc: int) -> None:
+    if rc != FD_OK:
+        msg = load().fd_last_error(ctx_ptr)
+        raise FdError(rc, msg.decode() if msg else "")

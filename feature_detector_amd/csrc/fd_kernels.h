@@ -1,0 +1,106 @@
+// Kernel argument blocks and host-side launchers (defined in fd_points.hip / fd_lsd.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fdk {
+
+// Tile geometry of the per-pixel kernels: one wave owns kTileW output columns (lanes 1..62, 4 px
+// each; lanes 0 and 63 only supply halo data) and tile_h output rows, walked top to bottom.
+constexpr int kTileW = 248;
+constexpr int kSegCorner = kTileW / 2;  // strict 4-neighbour NMS: <= 1 candidate per 2 columns
+constexpr int kSegFast = kTileW;        // FAST has no NMS
+constexpr int kSelectChunk = 4096;      // candidates sorted per greedy chunk (LDS)
+constexpr int kGridLdsCells = 16384;    // occupancy grid kept in LDS up to this many cells
+constexpr int kMaxOffsetSegs = 48;
+
+struct Cand {
+    float resp;
+    uint32_t idx;  // row * cols + col
+};
+
+// FAST running offset o_k (feature_point_fast_detector.cpp:85,93) as a piecewise-arithmetic table:
+// o_k = o_start[s] + (k - k_start[s]) * inc[s], exact in double.
+struct FastOffsets {
+    int nseg;
+    int64_t k0;  // first k with o_k > threshold (score-0 pixels before it are never candidates)
+    int64_t k_start[kMaxOffsetSegs];
+    double o_start[kMaxOffsetSegs];
+    double inc[kMaxOffsetSegs];
+};
+
+struct PointsArgs {
+    const uint8_t *frames;
+    int batch, rows, cols;
+    int tiles_x, tiles_y, tile_h;
+    int aligned4;  // cols % 4 == 0 and 4-byte aligned frames: whole-dword loads are range-exact
+    float thr;
+    const uint32_t *mask;  // prior-feature bitmap [batch][rows][mask_wpr], bit = mask true; null = all ones
+    int mask_wpr;
+    // detect mode: unordered per-frame lists
+    Cand *list;
+    int64_t list_cap;
+    uint32_t *list_count;
+    // raster mode: per (frame, row, tile_x) segments
+    int32_t *seg_cnt;
+    Cand *seg;
+    float *resp_map;  // optional full response map (raster mode)
+    // masked FAST: k = row_base[f][r] + word_pref[f][r][w] + popcount within the word
+    const int32_t *row_base;
+    const int32_t *word_pref;
+};
+
+struct SelectArgs {
+    const Cand *list;
+    const uint32_t *list_count;
+    int64_t list_cap;
+    int rows, cols;
+    const uint32_t *mask;
+    int mask_wpr;
+    const int32_t *prior_counts;  // device, per frame (null = none)
+    uint32_t need;
+    int dist;
+    int grid_w, grid_h;
+    uint32_t *grid_global;  // [batch][grid_w * grid_h] when the grid does not fit LDS
+    float *out_xy;
+    int out_stride;
+    int32_t *out_counts;
+};
+
+struct CompactArgs {
+    const int32_t *seg_cnt;
+    const Cand *seg;
+    int rows, cols, tiles_x, seg_cap, row_lo, row_hi;  // segment rows [row_lo, row_hi)
+    float *out_resp;
+    int32_t *out_x, *out_y;
+    int64_t cap;
+    int64_t *out_counts;
+};
+
+struct LsdArgs {
+    const uint8_t *frames;
+    int batch, rows, cols;
+    int strips, chunks, chunk_h;
+    float min_norm;
+    float *norm, *angle;
+    uint8_t *valid;
+    int32_t *col_cnt;   // [batch][cols-1][chunks]
+    int32_t *col_base;  // same shape, exclusive scan in column-major order
+    int32_t *idx;
+    int64_t idx_cap;
+    int64_t *counts;
+};
+
+// Launchers (stream-ordered, no allocation, no synchronisation: graph-capturable).
+hipError_t launch_mask_boxes(const float *prior_xy, const int32_t *prior_frame, int n_prior, int dist, int rows,
+                             int cols, uint32_t *mask, int mask_wpr, hipStream_t s);
+hipError_t launch_fast_mask_scan(const uint32_t *mask, int mask_wpr, int batch, int rows, int cols, int32_t *row_base,
+                                 int32_t *word_pref, hipStream_t s);
+hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s);
+hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s);
+hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);
+hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
+hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
+
+}  // namespace fdk

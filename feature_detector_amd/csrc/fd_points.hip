@@ -1,0 +1,793 @@
+// Point-detection kernels for gfx950 (MI355X): Harris / Shi-Tomasi response + 4-neighbour NMS,
+// FAST-12 segment test, prior-feature mask, per-frame greedy min-distance selection.
+//
+// Reference (Horizon1026/Feature_Detector, paths relative to src/feature_point_detector/):
+//   gradient + 3x3 tensor ........ feature_point_harris_detector.cpp:17-64, :66-88, :108-116
+//   Harris response .............. feature_point_harris_detector.cpp:94-104
+//   Shi-Tomasi response .......... feature_point_shi_tomas_detector.cpp:94-103
+//   4-neighbour NMS .............. feature_point_harris_detector.cpp:120-137
+//   FAST ......................... feature_point_fast_detector.cpp:11-98
+//   mask / sort / greedy select .. feature_point_detector.cpp:7-25, :54-98
+// See DESIGN.md for the data layout, the roofline of each kernel and the bit-exactness argument.
+//
+// Build flags matter: -ffp-contract=off (the reference's x86-64 build has no FMA) and correctly
+// rounded f32 sqrt/div (hipcc default; never -ffast-math).
+#include "fd_device.h"
+#include "fd_kernels.h"
+
+namespace fdk {
+
+namespace {
+
+constexpr int kStage = 512;  // per-wave LDS staging of candidates (detect mode)
+constexpr float kInvCnt = 1.0f / 9.0f;                  // 1 / (3*3)  (:71)
+constexpr float kInvCnt2 = (1.0f / 9.0f) * (1.0f / 9.0f);  // harris :72
+constexpr float kHarrisAlpha = 0.04f;                  // feature_point_harris_detector.h:13
+
+__device__ __forceinline__ void decode_tile(const PointsArgs &a, int &f, int &ty, int &tx) {
+    int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    tx = w % a.tiles_x;
+    w /= a.tiles_x;
+    ty = w % a.tiles_y;
+    f = w / a.tiles_y;
+}
+
+// Dword of frame bytes [off, off+4). `aligned` (cols % 4 == 0) guarantees whole-dword range checks;
+// otherwise assemble from byte loads so that a dword straddling the frame end still returns its bytes.
+__device__ __forceinline__ uint32_t load_px4(__amdgpu_buffer_rsrc_t r, int32_t off, bool aligned) {
+    if (aligned) return buf_load_u32(r, off);
+    return buf_load_u8(r, off) | (buf_load_u8(r, off + 1) << 8) | (buf_load_u8(r, off + 2) << 16) |
+           (buf_load_u8(r, off + 3) << 24);
+}
+
+// Per-wave candidate sink. Detect mode: stage in LDS, append to the frame's list with one atomic per
+// flush. Raster mode: write the (row, tile) segment in column order.
+struct Sink {
+    Cand *stage;
+    int n;  // staged entries (wave-uniform)
+};
+
+__device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f) {
+    if (sk.n == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&a.list_count[f], static_cast<uint32_t>(sk.n));
+    base = __shfl(base, 0);
+    Cand *dst = a.list + static_cast<int64_t>(f) * a.list_cap;
+    for (int i = lane_id(); i < sk.n; i += kWave) {
+        const int64_t pos = static_cast<int64_t>(base) + i;
+        if (pos < a.list_cap) dst[pos] = sk.stage[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    sk.n = 0;
+}
+
+// Emit up to 4 candidates of this lane (columns c0..c0+3 of row `row`), preserving column order.
+template <bool RASTER, int SEGCAP>
+__device__ __forceinline__ void emit_row(Sink &sk, const PointsArgs &a, int f, int tx, int row, int c0,
+                                         const bool (&fl)[4], const float (&v)[4]) {
+    const uint64_t b0 = ballot(fl[0]), b1 = ballot(fl[1]), b2 = ballot(fl[2]), b3 = ballot(fl[3]);
+    const uint64_t lb = lanes_below();
+    int pos = popc64(b0 & lb) + popc64(b1 & lb) + popc64(b2 & lb) + popc64(b3 & lb);
+    const int tot = popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
+    const uint32_t rowbase = static_cast<uint32_t>(row) * static_cast<uint32_t>(a.cols);
+    if constexpr (RASTER) {
+        const int64_t seg = (static_cast<int64_t>(f) * a.rows + row) * a.tiles_x + tx;
+        if (lane_id() == 0) a.seg_cnt[seg] = tot;
+        Cand *dst = a.seg + seg * SEGCAP;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if (fl[m]) dst[pos++] = Cand{v[m], rowbase + static_cast<uint32_t>(c0 + m)};
+    } else {
+        if (tot == 0) return;
+        if (sk.n + tot > kStage) sink_flush(sk, a, f);
+        Cand *dst = sk.stage + sk.n;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if (fl[m]) dst[pos++] = Cand{v[m], rowbase + static_cast<uint32_t>(c0 + m)};
+        sk.n += tot;
+    }
+}
+
+__device__ __forceinline__ uint32_t mask_bits4(const PointsArgs &a, int f, int row, int c0) {
+    if (c0 < 0 || c0 >= a.cols) return 0u;
+    const uint32_t w = a.mask[(static_cast<int64_t>(f) * a.rows + row) * a.mask_wpr + (c0 >> 5)];
+    return (w >> (c0 & 31)) & 0xFu;
+}
+
+// Stored response of one pixel (responses_ semantics: 0 unless written).
+template <int KIND>
+__device__ __forceinline__ float corner_response(int sxx, int syy, int sxy, float thr) {
+    float res = 0.0f;
+    if constexpr (KIND == 0) {  // Harris, feature_point_harris_detector.cpp:95-103
+        const float fxx = static_cast<float>(sxx);
+        const float fyy = static_cast<float>(syy);
+        const float trace = fxx + fyy;
+        if (((trace * trace) * 0.21f) * kInvCnt2 > thr) {
+            const float fxy = static_cast<float>(sxy);
+            const float r = (((fxx * fyy) - (fxy * fxy)) - ((kHarrisAlpha * trace) * trace)) * kInvCnt2;
+            if (r > thr) res = r;
+        }
+    } else {  // Shi-Tomasi, feature_point_shi_tomas_detector.cpp:94-103
+        const float a = static_cast<float>(sxx) * kInvCnt;
+        const float c = static_cast<float>(syy) * kInvCnt;
+        const float ac = a + c;
+        if (ac > thr) {
+            const float b = static_cast<float>(sxy) * kInvCnt;
+            const float d = a - c;
+            const float common = __builtin_sqrtf((d * d) + ((4.0f * b) * b));
+            const float r = (ac + common) * 0.5f;
+            if (r > thr) res = r;
+        }
+    }
+    return res;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// K1: corner response + NMS. One wave per tile of kTileW columns x tile_h rows; lane l covers columns
+// c0 = tx*kTileW + 4(l-1) .. c0+3 and walks the rows keeping 3-row sliding windows in registers:
+// pixels (+ DPP halo dwords), horizontal tensor sums, responses.
+// ---------------------------------------------------------------------------------------------------
+template <int KIND, bool RASTER, bool MASKED>
+__global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
+    __shared__ Cand stage_all[RASTER ? 1 : 4][RASTER ? 1 : kStage];
+    int f, ty, tx;
+    decode_tile(a, f, ty, tx);
+    if (f >= a.batch) return;
+    const int lane = lane_id();
+    const int rows = a.rows, cols = a.cols;
+    const int c0 = tx * kTileW + 4 * (lane - 1);
+    const int y0 = 2 + ty * a.tile_h;
+    const int y1 = min(y0 + a.tile_h, rows - 2);  // output rows [y0, y1) within [2, rows-3]
+    const bool aligned = a.aligned4 != 0;
+    const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
+    Sink sk{stage_all[RASTER ? 0 : (threadIdx.x >> 6)], 0};
+
+    bool cval[4], colv[4];  // column inside [2, cols-3]; and owned by an interior lane (emitted)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        cval[m] = c0 + m >= 2 && c0 + m <= cols - 3;
+        colv[m] = cval[m] && lane >= 1 && lane <= 62;
+    }
+
+    uint32_t P[3] = {0, 0, 0}, L[3] = {0, 0, 0}, R[3] = {0, 0, 0};
+    int hxx[3][4], hyy[3][4], hxy[3][4];
+    float rsp[3][4];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) hxx[s][m] = hyy[s][m] = hxy[s][m] = 0, rsp[s][m] = 0.0f;
+
+    const int n_in = (y1 - y0) + 6;
+    for (int i0 = 0; i0 < n_in; i0 += 3) {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            const int su = (s + 1) % 3, sc = (s + 2) % 3;  // slots of rows ri-2 and ri-1
+            const int ri = y0 - 3 + i0 + s;                 // row loaded this step (slot s)
+            P[s] = load_px4(rs, ri * cols + c0, aligned);
+            L[s] = from_left(P[s]);
+            R[s] = from_right(P[s]);
+
+            // Gradient products of centre row ri-1 at columns c0-1..c0+4 (k = 0..5), then 3-wide
+            // horizontal sums for the lane's own columns (feature_point_harris_detector.cpp:35-62).
+            int qxx[6], qyy[6], qxy[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const int j = k - 1;
+                const int ix = win_byte(L[sc], P[sc], R[sc], j + 1) - win_byte(L[sc], P[sc], R[sc], j - 1);
+                const int iy = win_byte(L[s], P[s], R[s], j) - win_byte(L[su], P[su], R[su], j);
+                qxx[k] = ix * ix;
+                qyy[k] = iy * iy;
+                qxy[k] = ix * iy;
+            }
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                hxx[sc][m] = qxx[m] + qxx[m + 1] + qxx[m + 2];
+                hyy[sc][m] = qyy[m] + qyy[m + 1] + qyy[m + 2];
+                hxy[sc][m] = qxy[m] + qxy[m + 1] + qxy[m + 2];
+            }
+
+            // Response of row rr = ri-2: vertical 3-row sums are exact integers (< 2^24).
+            const int rr = ri - 2;
+            const bool rowv = rr >= 2 && rr <= rows - 3;
+            uint32_t mb = 0xFu;
+            if constexpr (MASKED) mb = rowv ? mask_bits4(a, f, rr, c0) : 0u;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int sxx = hxx[s][m] + hxx[su][m] + hxx[sc][m];
+                const int syy = hyy[s][m] + hyy[su][m] + hyy[sc][m];
+                const int sxy = hxy[s][m] + hxy[su][m] + hxy[sc][m];
+                const float r = corner_response<KIND>(sxx, syy, sxy, a.thr);
+                // Lane 0's columns 2-3 and lane 63's columns 0-1 are exact (their halo comes from
+                // lanes 1 / 62) and serve as the NMS neighbours of the tile's edge columns.
+                rsp[su][m] = (rowv && cval[m] && ((mb >> m) & 1u)) ? r : 0.0f;
+            }
+
+            // NMS of row nr = ri-3 (feature_point_harris_detector.cpp:120-137): strict, 4-neighbour.
+            const int nr = ri - 3;
+            if (nr >= y0 && nr < y1) {  // wave-uniform
+                const float lft = from_left_f(rsp[s][3]);
+                const float rgt = from_right_f(rsp[s][0]);
+                bool fl[4];
+                float v[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float x = rsp[s][m];
+                    const float xl = m == 0 ? lft : rsp[s][m - 1];
+                    const float xr = m == 3 ? rgt : rsp[s][m + 1];
+                    v[m] = x;
+                    fl[m] = colv[m] && x > a.thr && x > xl && x > xr && x > rsp[sc][m] && x > rsp[su][m];
+                }
+                emit_row<RASTER, kSegCorner>(sk, a, f, tx, nr, c0, fl, v);
+                if constexpr (RASTER) {
+                    if (a.resp_map != nullptr) {
+                        float *mrow = a.resp_map + (static_cast<int64_t>(f) * rows + nr) * cols;
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            if (colv[m]) mrow[c0 + m] = v[m];
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (!RASTER) sink_flush(sk, a, f);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// K3: FAST-12. Same tile walk with a 7-row register window (ring radius 3).
+// ---------------------------------------------------------------------------------------------------
+// Bresenham ring of radius 3 (kFastIndice, feature_point_fast_detector.cpp:7-8), as compile-time tables.
+__device__ constexpr int ring_dx(int k) {
+    constexpr int8_t t[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    return t[k];
+}
+__device__ constexpr int ring_dy(int k) {
+    constexpr int8_t t[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
+    return t[k];
+}
+
+// Longest circular run of set bits in a 16-bit ring mask (== the reference's two-pass count,
+// feature_point_fast_detector.cpp:55-78; 16 when the whole ring is set).
+__device__ __forceinline__ int circ_run16(uint32_t b) {
+    if (b == 0xFFFFu) return 16;
+    const uint32_t x = b | (b << 16);
+    const uint32_t r2 = x & (x >> 1), r4 = r2 & (r2 >> 2), r8 = r4 & (r4 >> 4);
+    uint32_t S = 0xFFFFFFFFu, T;
+    int r = 0;
+    T = S & r8;
+    if (T) { S = T; r = 8; }
+    T = S & (r4 >> r);
+    if (T) { S = T; r += 4; }
+    T = S & (r2 >> r);
+    if (T) { S = T; r += 2; }
+    T = S & (x >> r);
+    if (T) { r += 1; }
+    return r;
+}
+
+__device__ __forceinline__ float fast_offset(int nseg, const int64_t *ks, const double *os, const double *inc,
+                                             int64_t k) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {  // last segment with k_start <= k
+        const int mid = (lo + hi + 1) >> 1;
+        if (ks[mid] <= k) lo = mid; else hi = mid - 1;
+    }
+    return static_cast<float>(os[lo] + static_cast<double>(k - ks[lo]) * inc[lo]);
+}
+
+template <bool RASTER, bool MASKED>
+__global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
+    __shared__ Cand stage_all[RASTER ? 1 : 4][RASTER ? 1 : kStage];
+    __shared__ int64_t seg_k[kMaxOffsetSegs];
+    __shared__ double seg_o[kMaxOffsetSegs], seg_inc[kMaxOffsetSegs];
+    if (threadIdx.x == 0)
+        for (int i = 0; i < off.nseg; ++i) {
+            seg_k[i] = off.k_start[i];
+            seg_o[i] = off.o_start[i];
+            seg_inc[i] = off.inc[i];
+        }
+    __syncthreads();
+    int f, ty, tx;
+    decode_tile(a, f, ty, tx);
+    if (f >= a.batch) return;
+    const int lane = lane_id();
+    const int rows = a.rows, cols = a.cols;
+    const int c0 = tx * kTileW + 4 * (lane - 1);
+    const int y0 = 3 + ty * a.tile_h;
+    const int y1 = min(y0 + a.tile_h, rows - 3);  // output rows [y0, y1) within [3, rows-4]
+    const bool aligned = a.aligned4 != 0;
+    const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
+    Sink sk{stage_all[RASTER ? 0 : (threadIdx.x >> 6)], 0};
+    const int diff = 15;  // kMinPixelDiffValue (feature_point_fast_detector.h:14)
+
+    bool colv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) colv[m] = lane >= 1 && lane <= 62 && c0 + m >= 3 && c0 + m <= cols - 4;
+
+    uint32_t P[7], L[7], R[7];
+#pragma unroll
+    for (int s = 0; s < 7; ++s) P[s] = L[s] = R[s] = 0;
+
+    const int n_in = (y1 - y0) + 6;
+    for (int i0 = 0; i0 < n_in; i0 += 7) {
+#pragma unroll
+        for (int s = 0; s < 7; ++s) {
+            const int ri = y0 - 3 + i0 + s;
+            P[s] = load_px4(rs, ri * cols + c0, aligned);
+            L[s] = from_left(P[s]);
+            R[s] = from_right(P[s]);
+            const int orow = ri - 3;  // output row; its window rows orow-3..orow+3 are slots s+1..s (mod 7)
+            if (orow < y0 || orow >= y1) continue;  // wave-uniform
+#define PX(dy, j) win_byte(L[(s + 4 + (dy)) % 7], P[(s + 4 + (dy)) % 7], R[(s + 4 + (dy)) % 7], (j))
+            uint32_t mb = 0xFu;
+            if constexpr (MASKED) mb = mask_bits4(a, f, orow, c0);
+            bool pass[4];
+            int p[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                p[m] = PX(0, m);
+                const int hi = p[m] + diff, lo = p[m] - diff;
+                const int s4 = PX(0, m + 3), s8 = PX(3, m), s12 = PX(0, m - 3);
+                // Cardinal pre-check (:20-42): samples 4, 8, 12 all brighter or all darker.
+                pass[m] = colv[m] && ((mb >> m) & 1u) &&
+                          ((s4 > hi && s8 > hi && s12 > hi) || (s4 < lo && s8 < lo && s12 < lo));
+            }
+            int score[4] = {0, 0, 0, 0};
+            if (ballot(pass[0] || pass[1] || pass[2] || pass[3]) != 0ull) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int hi = p[m] + diff, lo = p[m] - diff;
+                    uint32_t B = 0, D = 0;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        const int v = PX(ring_dy(k), m + ring_dx(k));
+                        B |= static_cast<uint32_t>(v > hi) << k;
+                        D |= static_cast<uint32_t>(v < lo) << k;
+                    }
+                    const int sc = max(circ_run16(B), circ_run16(D));
+                    score[m] = pass[m] ? sc : 0;
+                }
+            }
+#undef PX
+            // Scan index k of each pixel among mask-true pixels (the offset counter of :85-93).
+            int64_t kbase;
+            uint32_t mword = 0;
+            if constexpr (MASKED) {
+                const int64_t rb = static_cast<int64_t>(f) * rows + orow;
+                kbase = a.row_base[rb];
+                if (c0 >= 0 && c0 < cols) {
+                    const int w = c0 >> 5;
+                    kbase += a.word_pref[rb * a.mask_wpr + w];
+                    mword = a.mask[rb * a.mask_wpr + w];
+                    if (w == 0) mword &= ~7u;
+                }
+            } else {
+                kbase = static_cast<int64_t>(orow - 3) * (cols - 6) + (c0 - 3);
+            }
+            bool fl[4];
+            float v[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                int64_t k;
+                if constexpr (MASKED) {
+                    k = kbase + __popc(mword & ((1u << ((c0 + m) & 31)) - 1u));  // earlier pixels in the word
+                } else {
+                    k = kbase + m;
+                }
+                const bool live = colv[m] && ((mb >> m) & 1u);
+                float resp = 0.0f;
+                bool cand = false;
+                if (live && (score[m] > 0 || k >= off.k0)) {
+                    const float o = fast_offset(off.nseg, seg_k, seg_o, seg_inc, k);
+                    resp = static_cast<float>(score[m]) + o;  // :88 ComputeResponseOfPixel(...) + offset
+                    cand = resp > a.thr;
+                }
+                fl[m] = cand;
+                v[m] = resp;
+            }
+            emit_row<RASTER, kSegFast>(sk, a, f, tx, orow, c0, fl, v);
+            if constexpr (RASTER) {
+                if (a.resp_map != nullptr) {
+                    float *mrow = a.resp_map + (static_cast<int64_t>(f) * rows + orow) * cols;
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        if (fl[m]) mrow[c0 + m] = v[m];
+                }
+            }
+        }
+    }
+    if constexpr (!RASTER) sink_flush(sk, a, f);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Prior-feature mask (feature_point_detector.cpp:90-98 + :76-88): one thread per (feature, box row)
+// clears the box's bits of that row. The bitmap is preset to all ones.
+// ---------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mask_boxes(const float *prior_xy, const int32_t *prior_frame, int n_prior,
+                                                    int dist, int rows, int cols, uint32_t *mask, int wpr) {
+    const int span = 2 * dist + 1;
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= static_cast<int64_t>(n_prior) * span) return;
+    const int p = static_cast<int>(t / span);
+    const int dr = static_cast<int>(t % span) - dist;
+    const int r0 = static_cast<int>(prior_xy[2 * p + 1]);  // static_cast<int32_t>(feature.y())
+    const int cc = static_cast<int>(prior_xy[2 * p + 0]);
+    const int r = r0 + dr;
+    if (r < 0 || r > rows - 1) return;
+    const int ca = max(cc - dist, 0), cb = min(cc + dist, cols - 1);
+    if (ca > cb) return;
+    uint32_t *row = mask + (static_cast<int64_t>(prior_frame[p]) * rows + r) * wpr;
+    for (int w = ca >> 5; w <= (cb >> 5); ++w) {
+        const int lo = max(ca - 32 * w, 0), hi = min(cb - 32 * w, 31);
+        const uint32_t bits = (hi == 31 ? 0xFFFFFFFFu : ((1u << (hi + 1)) - 1u)) & ~((1u << lo) - 1u);
+        atomicAnd(&row[w], ~bits);
+    }
+}
+
+// Masked FAST scan index: per frame, row_base[r] = mask-true pixels of rows [3, r) in cols [3, C-4];
+// word_pref[r][w] = mask-true pixels of row r in cols [3, min(32w, C-3)).
+__global__ __launch_bounds__(1024) void k_fast_mask_scan(const uint32_t *mask, int wpr, int rows, int cols,
+                                                         int32_t *row_base, int32_t *word_pref) {
+    __shared__ int32_t tot[4096];
+    const int f = blockIdx.x;
+    const uint32_t *fm = mask + static_cast<int64_t>(f) * rows * wpr;
+    for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+        int acc = 0;
+        const bool rv = r >= 3 && r <= rows - 4;
+        for (int w = 0; w < wpr; ++w) {
+            word_pref[(static_cast<int64_t>(f) * rows + r) * wpr + w] = acc;
+            uint32_t bits = rv ? fm[static_cast<int64_t>(r) * wpr + w] : 0u;
+            // keep columns in [3, cols-4]
+            const int lo = 3 - 32 * w, hi = (cols - 4) - 32 * w;
+            if (hi < 0) bits = 0;
+            else if (hi < 31) bits &= (1u << (hi + 1)) - 1u;
+            if (lo > 31) bits = 0;
+            else if (lo > 0) bits &= ~((1u << lo) - 1u);
+            acc += __popc(bits);
+        }
+        if (r < 4096) tot[r] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // rows <= 4096 (checked on host); sequential scan is tiny
+        int64_t acc = 0;
+        for (int r = 0; r < rows; ++r) {
+            row_base[static_cast<int64_t>(f) * rows + r] = static_cast<int32_t>(acc);
+            acc += tot[r];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// K4: per-frame greedy selection (SelectGoodFeatures, feature_point_detector.cpp:54-88).
+// Candidates are visited in (response desc, raster index asc) order without a full sort: a radix
+// descent over the 64-bit key sk = (orderable response bits << 32) | ~idx cuts the frame's list into
+// consecutive chunks of <= kSelectChunk keys, each gathered into LDS, bitonic-sorted and scanned by
+// one wave. Accepted features live in an occupancy grid of (d+1)-sized cells: at most one accepted
+// feature per cell, so a Chebyshev-distance test needs the 3x3 neighbouring cells only.
+// ---------------------------------------------------------------------------------------------------
+constexpr int kLevels = 8;
+__device__ __forceinline__ int lvl_width(int l) { return l == 0 ? 11 : (l == 7 ? 5 : 8); }
+__device__ __forceinline__ int lvl_top(int l) { return l == 7 ? 64 : 11 + 8 * l; }  // bits consumed through l
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint64_t sort_key(const Cand &c) {
+    return (static_cast<uint64_t>(float_key(c.resp)) << 32) | static_cast<uint64_t>(~c.idx);
+}
+
+__global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
+    __shared__ uint32_t suf0[2049];
+    __shared__ uint32_t sufl[kLevels - 1][257];
+    __shared__ uint64_t buf[kSelectChunk];
+    __shared__ uint32_t grid_lds[kGridLdsCells];
+    __shared__ uint64_t prefix[kLevels];
+    __shared__ int resume[kLevels];
+    __shared__ uint32_t gcount;
+    __shared__ int s_done, s_acc;
+
+    const int f = blockIdx.x;
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = lane_id();
+    const int rows = a.rows, cols = a.cols;
+    const int64_t n = min(static_cast<int64_t>(a.list_count[f]), a.list_cap);
+    const Cand *list = a.list + static_cast<int64_t>(f) * a.list_cap;
+    const int d = a.dist;
+    const bool use_grid = d >= 1;
+    const int cells = a.grid_w * a.grid_h;
+    const bool grid_in_lds = cells <= kGridLdsCells;
+    uint32_t *grid = grid_in_lds ? grid_lds : a.grid_global + static_cast<int64_t>(f) * cells;
+    const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
+    const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
+
+    if (use_grid)
+        for (int i = tid; i < cells; i += nthr) grid[i] = kEmpty;
+    if (tid == 0) {
+        s_done = 0;
+        s_acc = 0;
+        prefix[0] = 0;
+    }
+    __syncthreads();
+    if (n == 0) {  // RETURN_TRUE_IF(candidates_.empty()) (:55)
+        if (tid == 0) a.out_counts[f] = 0;
+        return;
+    }
+
+    // Histogram of digit `lvl` over keys in [klo, khi], then in-place suffix sums (wave 0).
+    auto build = [&](int lvl, uint64_t klo, uint64_t khi, uint32_t *S) {
+        const int nb = 1 << lvl_width(lvl);
+        const int rem = 64 - lvl_top(lvl);
+        for (int b = tid; b <= nb; b += nthr) S[b] = 0;
+        __syncthreads();
+        for (int64_t i = tid; i < n; i += nthr) {
+            const uint64_t sk = sort_key(list[i]);
+            if (sk >= klo && sk <= khi) atomicAdd(&S[(sk >> rem) & static_cast<uint64_t>(nb - 1)], 1u);
+        }
+        __syncthreads();
+        if (tid < kWave) {
+            const int ch = (nb + kWave - 1) / kWave;
+            const int b0 = min(lane * ch, nb), b1 = min(b0 + ch, nb);
+            uint32_t s = 0;
+            for (int b = b0; b < b1; ++b) s += S[b];
+            uint32_t incl = s;
+            for (int o = 1; o < kWave; o <<= 1) {
+                const uint32_t t = __shfl_down(incl, o);
+                if (lane + o < kWave) incl += t;
+            }
+            uint32_t run = incl - s;
+            for (int b = b1 - 1; b >= b0; --b) {
+                run += S[b];
+                S[b] = run;
+            }
+            if (lane == 0) S[nb] = 0;
+        }
+        __syncthreads();
+    };
+    auto suf = [&](int lvl) -> uint32_t * { return lvl == 0 ? suf0 : sufl[lvl - 1]; };
+
+    build(0, 0ull, ~0ull, suf0);
+    int level = 0;
+    int hi = (1 << lvl_width(0)) - 1;
+    while (true) {
+        if (s_done) break;
+        if (hi < 0) {
+            if (level == 0) break;
+            --level;
+            hi = resume[level];
+            continue;
+        }
+        const uint32_t *S = suf(level);
+        const uint32_t base = S[hi + 1];
+        // smallest lo in [0, hi] with S[lo] - base <= chunk (S is non-increasing in b)
+        int lo_b = 0, hi_b = hi + 1;
+        while (lo_b < hi_b) {
+            const int mid = (lo_b + hi_b) >> 1;
+            if (S[mid] - base <= static_cast<uint32_t>(kSelectChunk)) hi_b = mid; else lo_b = mid + 1;
+        }
+        const int lo = lo_b;
+        const int w = lvl_width(level);
+        const int rem = 64 - lvl_top(level);
+        const uint64_t pre = prefix[level];
+        if (lo > hi) {  // bin `hi` alone exceeds a chunk: descend into it
+            __syncthreads();
+            if (tid == 0) {
+                resume[level] = hi - 1;
+                prefix[level + 1] = (pre << w) | static_cast<uint64_t>(hi);
+            }
+            __syncthreads();
+            const uint64_t klo = ((pre << w) | static_cast<uint64_t>(hi)) << rem;
+            const uint64_t khi = klo | ((rem == 64) ? ~0ull : ((1ull << rem) - 1ull));
+            ++level;
+            build(level, klo, khi, suf(level));
+            hi = (1 << lvl_width(level)) - 1;
+            continue;
+        }
+        const uint32_t cnt = S[lo] - base;
+        if (cnt > 0) {
+            const uint64_t klo = ((pre << w) | static_cast<uint64_t>(lo)) << rem;
+            const uint64_t khi = (((pre << w) | static_cast<uint64_t>(hi)) << rem) | ((1ull << rem) - 1ull);
+            // gather
+            if (tid == 0) gcount = 0;
+            __syncthreads();
+            for (int64_t i = tid; i < n; i += nthr) {
+                const uint64_t sk = sort_key(list[i]);
+                if (sk >= klo && sk <= khi) buf[atomicAdd(&gcount, 1u)] = sk;
+            }
+            __syncthreads();
+            int np2 = 64;
+            while (np2 < static_cast<int>(cnt)) np2 <<= 1;
+            for (int i = static_cast<int>(cnt) + tid; i < np2; i += nthr) buf[i] = 0ull;
+            __syncthreads();
+            // bitonic sort, descending
+            for (int k = 2; k <= np2; k <<= 1) {
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < np2; i += nthr) {
+                        const int ij = i ^ j;
+                        if (ij > i) {
+                            const uint64_t x = buf[i], y = buf[ij];
+                            const bool desc = (i & k) == 0;
+                            if (desc ? (x < y) : (x > y)) {
+                                buf[i] = y;
+                                buf[ij] = x;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            // greedy scan by wave 0
+            if (tid < kWave) {
+                int acc = s_acc;
+                bool done = false;
+                for (int b0 = 0; b0 < static_cast<int>(cnt) && !done; b0 += kWave) {
+                    const int i = b0 + lane;
+                    const bool in = i < static_cast<int>(cnt);
+                    const uint64_t sk = in ? buf[i] : 0ull;
+                    const uint32_t idx = ~static_cast<uint32_t>(sk);
+                    const int y = in ? static_cast<int>(idx / static_cast<uint32_t>(cols)) : 0;
+                    const int x = in ? static_cast<int>(idx - static_cast<uint32_t>(y) * cols) : 0;
+                    bool ok = in;
+                    if (ok && fmask) ok = (fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u;
+                    if (ok && use_grid) {
+                        const int cx = x / (d + 1), cy = y / (d + 1);
+                        for (int gy = max(cy - 1, 0); gy <= min(cy + 1, a.grid_h - 1) && ok; ++gy)
+                            for (int gx = max(cx - 1, 0); gx <= min(cx + 1, a.grid_w - 1); ++gx) {
+                                const uint32_t e = grid_in_lds ? grid[gy * a.grid_w + gx]
+                                                               : __hip_atomic_load(&grid[gy * a.grid_w + gx],
+                                                                                   __ATOMIC_RELAXED,
+                                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                                if (e != kEmpty) {
+                                    const int ex = static_cast<int>(e & 0xFFFFu), ey = static_cast<int>(e >> 16);
+                                    if (abs(x - ex) <= d && abs(y - ey) <= d) { ok = false; break; }
+                                }
+                            }
+                    }
+                    uint64_t m = ballot(ok);
+                    while (m) {
+                        const int first = __ffsll(static_cast<unsigned long long>(m)) - 1;
+                        const int fx = __shfl(x, first), fy = __shfl(y, first);
+                        if (lane == 0) {
+                            if (acc < a.out_stride) {
+                                float *o = a.out_xy + (static_cast<int64_t>(f) * a.out_stride + acc) * 2;
+                                o[0] = static_cast<float>(fx);
+                                o[1] = static_cast<float>(fy);
+                            }
+                            if (use_grid) {
+                                const int gi = (fy / (d + 1)) * a.grid_w + fx / (d + 1);
+                                const uint32_t e = (static_cast<uint32_t>(fy) << 16) | static_cast<uint32_t>(fx);
+                                if (grid_in_lds) grid[gi] = e;
+                                else __hip_atomic_store(&grid[gi], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            }
+                        }
+                        ++acc;
+                        if (prior + static_cast<uint32_t>(acc) >= a.need) { done = true; break; }  // :67-69
+                        if (lane > first && ok && abs(x - fx) <= d && abs(y - fy) <= d) ok = false;
+                        m = ballot(ok) & ~((first == 63) ? ~0ull : ((2ull << first) - 1ull));
+                    }
+                    if (!grid_in_lds && use_grid) __builtin_amdgcn_s_waitcnt(0);
+                }
+                if (lane == 0) {
+                    s_acc = acc;
+                    if (done) s_done = 1;
+                }
+            }
+            __syncthreads();
+        }
+        hi = lo - 1;
+    }
+    if (tid == 0) a.out_counts[f] = s_acc;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// K2: raster compaction of the per-(row, tile) segments into the reference's push order.
+// ---------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_compact(CompactArgs a) {
+    __shared__ int64_t wsum[16];
+    __shared__ int64_t carry;
+    const int f = blockIdx.x;
+    const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+    const int nseg = (a.row_hi - a.row_lo) * a.tiles_x;
+    const int32_t *cnt = a.seg_cnt + (static_cast<int64_t>(f) * a.rows + a.row_lo) * a.tiles_x;
+    const Cand *seg = a.seg + (static_cast<int64_t>(f) * a.rows + a.row_lo) * a.tiles_x * a.seg_cap;
+    float *oresp = a.out_resp + static_cast<int64_t>(f) * a.cap;
+    int32_t *ox = a.out_x + static_cast<int64_t>(f) * a.cap;
+    int32_t *oy = a.out_y + static_cast<int64_t>(f) * a.cap;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int s0 = 0; s0 < nseg; s0 += 1024) {
+        const int s = s0 + tid;
+        const int c = s < nseg ? cnt[s] : 0;
+        // block exclusive scan of c
+        int64_t incl = c;
+        for (int o = 1; o < kWave; o <<= 1) {
+            const int64_t t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int64_t wpre = 0;
+        for (int q = 0; q < wv; ++q) wpre += wsum[q];
+        const int64_t start = carry + wpre + incl - c;
+        __syncthreads();
+        if (tid == 1023) carry = start + c;
+        for (int e = 0; e < c; ++e) {
+            const int64_t pos = start + e;
+            if (pos < a.cap) {
+                const Cand cd = seg[static_cast<int64_t>(s) * a.seg_cap + e];
+                const int y = static_cast<int>(cd.idx / static_cast<uint32_t>(a.cols));
+                oresp[pos] = cd.resp;
+                ox[pos] = static_cast<int32_t>(cd.idx - static_cast<uint32_t>(y) * a.cols);
+                oy[pos] = y;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) a.out_counts[f] = carry;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------------------------------
+static inline int blocks_for_waves(const PointsArgs &a) {
+    const int64_t waves = static_cast<int64_t>(a.batch) * a.tiles_y * a.tiles_x;
+    return static_cast<int>((waves + 3) / 4);
+}
+
+hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s) {
+    const dim3 grid(blocks_for_waves(a)), block(256);
+    const bool masked = a.mask != nullptr;
+#define FD_CORNER(K, RS, M) hipLaunchKernelGGL((k_corner<K, RS, M>), grid, block, 0, s, a)
+    if (kind == 0) {
+        if (raster) { if (masked) FD_CORNER(0, true, true); else FD_CORNER(0, true, false); }
+        else { if (masked) FD_CORNER(0, false, true); else FD_CORNER(0, false, false); }
+    } else {
+        if (raster) { if (masked) FD_CORNER(1, true, true); else FD_CORNER(1, true, false); }
+        else { if (masked) FD_CORNER(1, false, true); else FD_CORNER(1, false, false); }
+    }
+#undef FD_CORNER
+    return hipGetLastError();
+}
+
+hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s) {
+    const dim3 grid(blocks_for_waves(a)), block(256);
+    const bool masked = a.mask != nullptr;
+    if (raster) {
+        if (masked) hipLaunchKernelGGL((k_fast<true, true>), grid, block, 0, s, a, off);
+        else hipLaunchKernelGGL((k_fast<true, false>), grid, block, 0, s, a, off);
+    } else {
+        if (masked) hipLaunchKernelGGL((k_fast<false, true>), grid, block, 0, s, a, off);
+        else hipLaunchKernelGGL((k_fast<false, false>), grid, block, 0, s, a, off);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_mask_boxes(const float *prior_xy, const int32_t *prior_frame, int n_prior, int dist, int rows,
+                             int cols, uint32_t *mask, int mask_wpr, hipStream_t s) {
+    if (n_prior <= 0 || dist < 0) return hipSuccess;
+    const int64_t threads = static_cast<int64_t>(n_prior) * (2 * dist + 1);
+    hipLaunchKernelGGL(k_mask_boxes, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, s, prior_xy,
+                       prior_frame, n_prior, dist, rows, cols, mask, mask_wpr);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_mask_scan(const uint32_t *mask, int mask_wpr, int batch, int rows, int cols, int32_t *row_base,
+                                 int32_t *word_pref, hipStream_t s) {
+    hipLaunchKernelGGL(k_fast_mask_scan, dim3(batch), dim3(1024), 0, s, mask, mask_wpr, rows, cols, row_base,
+                       word_pref);
+    return hipGetLastError();
+}
+
+hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
+    hipLaunchKernelGGL(k_select, dim3(batch), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s) {
+    hipLaunchKernelGGL(k_compact, dim3(batch), dim3(1024), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace fdk

@@ -1,0 +1,658 @@
+// Host runtime of libfdhip.so: the C ABI declared in include/fd_hip.h.
+// Owns the per-context stream and grow-only device workspace, stages host buffers, builds the FAST
+// offset table and launches the kernels of fd_points.hip / fd_lsd.hip in stream order.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "fd_hip.h"
+#include "fd_kernels.h"
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+};
+
+}  // namespace
+
+struct fd_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // workspace
+    DevBuf frames, prior_xy, prior_frame, prior_counts, mask, row_base, word_pref;
+    DevBuf list, list_count, out_xy, out_counts, grid;
+    DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
+    DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts;
+    // FAST offset table cache
+    int64_t off_n = -1;
+    float off_thr = 0.0f;
+    fdk::FastOffsets off{};
+};
+
+namespace {
+
+int fail(fd_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define FD_HIP_TRY(ctx, expr)                                                                                    \
+    do {                                                                                                         \
+        hipError_t e_ = (expr);                                                                                  \
+        if (e_ != hipSuccess)                                                                                    \
+            return fail((ctx), FD_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+hipError_t ensure(DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.n >= bytes) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        if (e != hipSuccess) return e;
+        b.p = nullptr;
+        b.n = 0;
+    }
+    const size_t want = bytes + 256;  // slack: whole-dword loads near the end stay inside the allocation
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) return e;
+    b.n = want;
+    return hipSuccess;
+}
+
+void release(DevBuf &b) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+}
+
+template <typename T>
+T *as(DevBuf &b) {
+    return static_cast<T *>(b.p);
+}
+
+// Tile height: a multiple of `period` (3 for the corner walk, 7 for FAST) that still gives the launch
+// enough waves to fill 256 CUs, capped so halo rows stay a small overhead.
+int choose_tile_h(int64_t batch, int tiles_x, int out_rows, int period, int max_mult) {
+    const int64_t target_waves = 8192;
+    int64_t h = (batch * tiles_x * static_cast<int64_t>(out_rows)) / target_waves;
+    h = std::max<int64_t>(h, 2 * period);
+    h = ((h + period - 1) / period) * period;
+    h = std::min<int64_t>(h, static_cast<int64_t>(period) * max_mult);
+    return static_cast<int>(h);
+}
+
+// FAST running offset o_0 = 1e-5f, o_{k+1} = fl(o_k + 1e-5f) (feature_point_fast_detector.cpp:85,93)
+// as runs of constant increment; verified exact against the recurrence before use.
+int build_offsets(fd_ctx *c, int64_t n, float thr) {
+    if (c->off_n == n && c->off_thr == thr) return FD_OK;
+    fdk::FastOffsets o{};
+    o.nseg = 0;
+    o.k0 = std::numeric_limits<int64_t>::max();
+    std::vector<float> seq(static_cast<size_t>(std::max<int64_t>(n, 1)));
+    float v = 1e-5f;
+    double prev_inc = -1.0;
+    for (int64_t k = 0; k < n; ++k) {
+        seq[static_cast<size_t>(k)] = v;
+        const float next = v + 1e-5f;
+        const double inc = static_cast<double>(next) - static_cast<double>(v);
+        if (k == 0 || inc != prev_inc) {
+            if (o.nseg >= fdk::kMaxOffsetSegs) return fail(c, FD_ERR_INVALID, "FAST offset table too large");
+            o.k_start[o.nseg] = k;
+            o.o_start[o.nseg] = static_cast<double>(v);
+            o.inc[o.nseg] = inc;
+            ++o.nseg;
+            prev_inc = inc;
+        }
+        if (o.k0 == std::numeric_limits<int64_t>::max() && v > thr) o.k0 = k;
+        v = next;
+    }
+    if (o.nseg == 0) {
+        o.nseg = 1;
+        o.k_start[0] = 0;
+        o.o_start[0] = 1e-5;
+        o.inc[0] = 0.0;
+    }
+    int s = 0;
+    for (int64_t k = 0; k < n; ++k) {
+        while (s + 1 < o.nseg && o.k_start[s + 1] <= k) ++s;
+        const float r = static_cast<float>(o.o_start[s] + static_cast<double>(k - o.k_start[s]) * o.inc[s]);
+        if (r != seq[static_cast<size_t>(k)]) return fail(c, FD_ERR_INVALID, "FAST offset table not exact");
+    }
+    c->off = o;
+    c->off_n = n;
+    c->off_thr = thr;
+    return FD_OK;
+}
+
+struct PriorInfo {
+    int64_t total = 0;
+    const uint32_t *mask = nullptr;
+    const int32_t *counts_dev = nullptr;
+    int wpr = 0;
+};
+
+// Upload prior features and draw their boxes into the mask bitmap (feature_point_detector.cpp:90-98).
+int setup_priors(fd_ctx *c, int batch, int rows, int cols, int dist, const float *prior_xy,
+                 const int32_t *prior_counts, PriorInfo &pi) {
+    pi = PriorInfo{};
+    if (prior_counts == nullptr) return FD_OK;
+    std::vector<int32_t> frame_of;
+    for (int b = 0; b < batch; ++b) {
+        if (prior_counts[b] < 0) return fail(c, FD_ERR_INVALID, "negative prior count");
+        pi.total += prior_counts[b];
+    }
+    FD_HIP_TRY(c, ensure(c->prior_counts, sizeof(int32_t) * batch));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->prior_counts.p, prior_counts, sizeof(int32_t) * batch, hipMemcpyHostToDevice,
+                                 c->stream));
+    pi.counts_dev = as<int32_t>(c->prior_counts);
+    if (pi.total == 0) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // prior_counts is caller-owned host memory
+        return FD_OK;
+    }
+    if (prior_xy == nullptr) return fail(c, FD_ERR_INVALID, "prior_xy is NULL but prior_counts is not zero");
+    frame_of.reserve(static_cast<size_t>(pi.total));
+    for (int b = 0; b < batch; ++b)
+        for (int i = 0; i < prior_counts[b]; ++i) frame_of.push_back(b);
+    pi.wpr = (cols + 31) / 32;
+    const size_t mbytes = sizeof(uint32_t) * static_cast<size_t>(batch) * rows * pi.wpr;
+    FD_HIP_TRY(c, ensure(c->prior_xy, sizeof(float) * 2 * pi.total));
+    FD_HIP_TRY(c, ensure(c->prior_frame, sizeof(int32_t) * pi.total));
+    FD_HIP_TRY(c, ensure(c->mask, mbytes));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->prior_xy.p, prior_xy, sizeof(float) * 2 * pi.total, hipMemcpyHostToDevice,
+                                 c->stream));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->prior_frame.p, frame_of.data(), sizeof(int32_t) * pi.total,
+                                 hipMemcpyHostToDevice, c->stream));
+    FD_HIP_TRY(c, hipMemsetAsync(c->mask.p, 0xFF, mbytes, c->stream));
+    FD_HIP_TRY(c, fdk::launch_mask_boxes(as<float>(c->prior_xy), as<int32_t>(c->prior_frame),
+                                         static_cast<int>(pi.total), dist, rows, cols, as<uint32_t>(c->mask), pi.wpr,
+                                         c->stream));
+    // The synchronous copies above read host memory that the caller may free after return.
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    pi.mask = as<uint32_t>(c->mask);
+    return FD_OK;
+}
+
+int check_shape(fd_ctx *c, int kind, int batch, int rows, int cols, bool points = true) {
+    if (!c) return FD_ERR_INVALID;
+    if (kind < FD_HARRIS || kind > FD_FAST) return fail(c, FD_ERR_INVALID, "unknown detector kind");
+    if (batch < 1 || rows < 1 || cols < 1) return fail(c, FD_ERR_INVALID, "batch, rows and cols must be >= 1");
+    // the selection grid packs (x, y) into 16 bits each
+    if (points && (rows > 65535 || cols > 65535)) return fail(c, FD_ERR_INVALID, "rows and cols must be <= 65535");
+    if (static_cast<int64_t>(rows) * cols >= (int64_t(1) << 31)) return fail(c, FD_ERR_INVALID, "frame too large");
+    return FD_OK;
+}
+
+// Stage the frames on the device (or use the caller's device pointer).
+int stage_frames(fd_ctx *c, const uint8_t *frames, int on_device, int batch, int rows, int cols,
+                 const uint8_t *&dframes) {
+    if (frames == nullptr) return fail(c, FD_ERR_INVALID, "frames is NULL");  // feature_point_detector.cpp:9
+    const size_t bytes = static_cast<size_t>(batch) * rows * cols;
+    if (on_device) {
+        dframes = frames;
+        return FD_OK;
+    }
+    FD_HIP_TRY(c, ensure(c->frames, bytes));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->frames.p, frames, bytes, hipMemcpyHostToDevice, c->stream));
+    dframes = as<uint8_t>(c->frames);
+    return FD_OK;
+}
+
+// Geometry of the per-pixel launch for a detector kind.
+struct PointGeom {
+    int border;    // 2 for Harris/Shi-Tomasi, 3 for FAST
+    int out_rows;  // rows of the candidate region
+    int tiles_x, tiles_y, tile_h;
+    bool empty;
+};
+
+PointGeom point_geom(int kind, int batch, int rows, int cols) {
+    PointGeom g{};
+    g.border = kind == FD_FAST ? 3 : 2;
+    g.out_rows = rows - 2 * g.border;
+    const int out_cols = cols - 2 * g.border;
+    g.empty = g.out_rows <= 0 || out_cols <= 0;
+    g.tiles_x = std::max(1, (cols - g.border + fdk::kTileW - 1) / fdk::kTileW);
+    const int period = kind == FD_FAST ? 7 : 3;
+    g.tile_h = choose_tile_h(batch, g.tiles_x, std::max(g.out_rows, 1), period, kind == FD_FAST ? 9 : 20);
+    g.tiles_y = std::max(1, (std::max(g.out_rows, 1) + g.tile_h - 1) / g.tile_h);
+    return g;
+}
+
+int64_t detect_list_cap(int kind, int rows, int cols) {
+    const int64_t px = static_cast<int64_t>(rows) * cols;
+    return (kind == FD_FAST ? px : px / 2) + 64;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *fd_build_info(void) {
+    return "libfdhip gfx950 (MI355X); kernels: corner response+NMS, FAST-12, greedy select, LSD map; "
+           "flags: -O3 -ffp-contract=off";
+}
+
+int fd_ctx_create(int device, fd_ctx **out) {
+    if (!out) return FD_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return FD_ERR_HIP;
+    if (device < 0 || device >= n) return FD_ERR_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return FD_ERR_HIP;
+    fd_ctx *c = new fd_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return FD_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return FD_OK;
+}
+
+void fd_ctx_destroy(fd_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DevBuf *bufs[] = {&c->frames,   &c->prior_xy, &c->prior_frame, &c->prior_counts, &c->mask,    &c->row_base,
+                      &c->word_pref, &c->list,    &c->list_count,  &c->out_xy,       &c->out_counts, &c->grid,
+                      &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
+                      &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
+                      &c->l_idx,    &c->l_counts};
+    for (DevBuf *b : bufs) release(*b);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char *fd_last_error(const fd_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int fd_ctx_set_stream(fd_ctx *c, void *s) {
+    if (!c) return FD_ERR_INVALID;
+    c->stream = static_cast<hipStream_t>(s);
+    return FD_OK;
+}
+
+int fd_ctx_use_own_stream(fd_ctx *c) {
+    if (!c) return FD_ERR_INVALID;
+    c->stream = c->own_stream;
+    return FD_OK;
+}
+
+void *fd_ctx_get_stream(const fd_ctx *c) { return c ? static_cast<void *>(c->stream) : nullptr; }
+
+int fd_ctx_synchronize(fd_ctx *c) {
+    if (!c) return FD_ERR_INVALID;
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return FD_OK;
+}
+
+int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t max_prior_total) {
+    int rc = check_shape(c, kind, batch, rows, cols);
+    if (rc) return rc;
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    const int64_t cap = detect_list_cap(kind, rows, cols);
+    FD_HIP_TRY(c, ensure(c->list, sizeof(fdk::Cand) * cap * batch));
+    FD_HIP_TRY(c, ensure(c->list_count, sizeof(uint32_t) * batch));
+    FD_HIP_TRY(c, ensure(c->prior_counts, sizeof(int32_t) * batch));
+    if (max_prior_total > 0) {
+        FD_HIP_TRY(c, ensure(c->prior_xy, sizeof(float) * 2 * max_prior_total));
+        FD_HIP_TRY(c, ensure(c->prior_frame, sizeof(int32_t) * max_prior_total));
+        FD_HIP_TRY(c, ensure(c->mask, sizeof(uint32_t) * static_cast<size_t>(batch) * rows * ((cols + 31) / 32)));
+    }
+    if (kind == FD_FAST) {
+        rc = build_offsets(c, std::max<int64_t>(0, static_cast<int64_t>(rows - 6) * (cols - 6)), c->off_thr);
+        if (rc) return rc;
+    }
+    return FD_OK;
+}
+
+int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
+                     const fd_point_opts *opts, const float *prior_xy, const int32_t *prior_counts, uint32_t need,
+                     float *out_xy, int32_t out_stride, int32_t *out_counts, int outputs_on_device) {
+    int rc = check_shape(c, kind, batch, rows, cols);
+    if (rc) return rc;
+    if (!opts || !out_xy || !out_counts || out_stride < 1) return fail(c, FD_ERR_INVALID, "bad output arguments");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    const uint8_t *dframes = nullptr;
+    rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
+    if (rc) return rc;
+    PriorInfo pi;
+    rc = setup_priors(c, batch, rows, cols, opts->min_feature_distance, prior_xy, prior_counts, pi);
+    if (rc) return rc;
+
+    const PointGeom g = point_geom(kind, batch, rows, cols);
+    const int64_t cap = detect_list_cap(kind, rows, cols);
+    FD_HIP_TRY(c, ensure(c->list, sizeof(fdk::Cand) * cap * batch));
+    FD_HIP_TRY(c, ensure(c->list_count, sizeof(uint32_t) * batch));
+    FD_HIP_TRY(c, hipMemsetAsync(c->list_count.p, 0, sizeof(uint32_t) * batch, c->stream));
+
+    fdk::PointsArgs a{};
+    a.frames = dframes;
+    a.batch = batch;
+    a.rows = rows;
+    a.cols = cols;
+    a.tiles_x = g.tiles_x;
+    a.tiles_y = g.tiles_y;
+    a.tile_h = g.tile_h;
+    a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
+    a.thr = opts->min_valid_response;
+    a.mask = pi.mask;
+    a.mask_wpr = pi.wpr;
+    a.list = as<fdk::Cand>(c->list);
+    a.list_cap = cap;
+    a.list_count = as<uint32_t>(c->list_count);
+    if (!g.empty) {
+        if (kind == FD_FAST) {
+            rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
+            if (rc) return rc;
+            if (pi.mask) {
+                if (rows > 4096) return fail(c, FD_ERR_INVALID, "FAST with prior features supports rows <= 4096");
+                FD_HIP_TRY(c, ensure(c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
+                FD_HIP_TRY(c, ensure(c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * pi.wpr));
+                FD_HIP_TRY(c, fdk::launch_fast_mask_scan(pi.mask, pi.wpr, batch, rows, cols, as<int32_t>(c->row_base),
+                                                         as<int32_t>(c->word_pref), c->stream));
+                a.row_base = as<int32_t>(c->row_base);
+                a.word_pref = as<int32_t>(c->word_pref);
+            }
+            FD_HIP_TRY(c, fdk::launch_fast(false, a, c->off, c->stream));
+        } else {
+            FD_HIP_TRY(c, fdk::launch_corner(kind, false, a, c->stream));
+        }
+    }
+
+    fdk::SelectArgs s{};
+    s.list = a.list;
+    s.list_count = a.list_count;
+    s.list_cap = cap;
+    s.rows = rows;
+    s.cols = cols;
+    s.mask = pi.mask;
+    s.mask_wpr = pi.wpr;
+    s.prior_counts = pi.counts_dev;
+    s.need = need;
+    s.dist = opts->min_feature_distance;
+    if (s.dist >= 1) {
+        s.grid_w = (cols + s.dist) / (s.dist + 1);
+        s.grid_h = (rows + s.dist) / (s.dist + 1);
+        const int64_t cells = static_cast<int64_t>(s.grid_w) * s.grid_h;
+        if (cells > fdk::kGridLdsCells) {
+            FD_HIP_TRY(c, ensure(c->grid, sizeof(uint32_t) * cells * batch));
+            s.grid_global = as<uint32_t>(c->grid);
+        }
+    }
+    float *dxy = out_xy;
+    int32_t *dcnt = out_counts;
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, ensure(c->out_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch));
+        FD_HIP_TRY(c, ensure(c->out_counts, sizeof(int32_t) * batch));
+        dxy = as<float>(c->out_xy);
+        dcnt = as<int32_t>(c->out_counts);
+    }
+    s.out_xy = dxy;
+    s.out_stride = out_stride;
+    s.out_counts = dcnt;
+    FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, hipMemcpyAsync(out_xy, dxy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
+                                     hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dcnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int b = 0; b < batch; ++b)
+            if (out_counts[b] > out_stride) return fail(c, FD_ERR_CAPACITY, "out_stride smaller than the features found");
+    } else if (!frames_on_device) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host frames must stay valid until copied
+    }
+    return FD_OK;
+}
+
+int fd_points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,
+                       const fd_point_opts *opts, void *out_cands, int64_t cand_cap, uint32_t *out_counts) {
+    int rc = check_shape(c, kind, batch, rows, cols);
+    if (rc) return rc;
+    if (!opts || !frames || !out_cands || !out_counts || cand_cap < 1)
+        return fail(c, FD_ERR_INVALID, "bad arguments");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    const PointGeom g = point_geom(kind, batch, rows, cols);
+    FD_HIP_TRY(c, hipMemsetAsync(out_counts, 0, sizeof(uint32_t) * batch, c->stream));
+    if (g.empty) return FD_OK;
+    fdk::PointsArgs a{};
+    a.frames = frames;
+    a.batch = batch;
+    a.rows = rows;
+    a.cols = cols;
+    a.tiles_x = g.tiles_x;
+    a.tiles_y = g.tiles_y;
+    a.tile_h = g.tile_h;
+    a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(frames) % 4 == 0);
+    a.thr = opts->min_valid_response;
+    a.list = static_cast<fdk::Cand *>(out_cands);
+    a.list_cap = cand_cap;
+    a.list_count = out_counts;
+    if (kind == FD_FAST) {
+        rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
+        if (rc) return rc;
+        FD_HIP_TRY(c, fdk::launch_fast(false, a, c->off, c->stream));
+    } else {
+        FD_HIP_TRY(c, fdk::launch_corner(kind, false, a, c->stream));
+    }
+    return FD_OK;
+}
+
+int fd_points_candidates(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_device, int batch, int rows,
+                         int cols, const fd_point_opts *opts, const float *prior_xy, const int32_t *prior_counts,
+                         float *out_resp, int32_t *out_x, int32_t *out_y, int64_t cand_cap, int64_t *out_counts,
+                         float *out_response_map, int outputs_on_device) {
+    int rc = check_shape(c, kind, batch, rows, cols);
+    if (rc) return rc;
+    if (!opts || !out_resp || !out_x || !out_y || !out_counts || cand_cap < 0)
+        return fail(c, FD_ERR_INVALID, "bad output arguments");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    const uint8_t *dframes = nullptr;
+    rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
+    if (rc) return rc;
+    PriorInfo pi;
+    rc = setup_priors(c, batch, rows, cols, opts->min_feature_distance, prior_xy, prior_counts, pi);
+    if (rc) return rc;
+
+    const PointGeom g = point_geom(kind, batch, rows, cols);
+    const int segcap = kind == FD_FAST ? fdk::kSegFast : fdk::kSegCorner;
+    const size_t nseg = static_cast<size_t>(batch) * rows * g.tiles_x;
+    FD_HIP_TRY(c, ensure(c->seg_cnt, sizeof(int32_t) * nseg));
+    FD_HIP_TRY(c, ensure(c->seg, sizeof(fdk::Cand) * nseg * segcap));
+    const size_t npx = static_cast<size_t>(batch) * rows * cols;
+    float *dmap = nullptr;
+    if (out_response_map) {
+        if (outputs_on_device) {
+            dmap = out_response_map;
+        } else {
+            FD_HIP_TRY(c, ensure(c->resp_map, sizeof(float) * npx));
+            dmap = as<float>(c->resp_map);
+        }
+        FD_HIP_TRY(c, hipMemsetAsync(dmap, 0, sizeof(float) * npx, c->stream));
+    }
+    float *dr = out_resp;
+    int32_t *dx = out_x, *dy = out_y;
+    int64_t *dc = out_counts;
+    const size_t ncap = static_cast<size_t>(std::max<int64_t>(cand_cap, 1)) * batch;
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, ensure(c->c_resp, sizeof(float) * ncap));
+        FD_HIP_TRY(c, ensure(c->c_x, sizeof(int32_t) * ncap));
+        FD_HIP_TRY(c, ensure(c->c_y, sizeof(int32_t) * ncap));
+        FD_HIP_TRY(c, ensure(c->c_counts, sizeof(int64_t) * batch));
+        dr = as<float>(c->c_resp);
+        dx = as<int32_t>(c->c_x);
+        dy = as<int32_t>(c->c_y);
+        dc = as<int64_t>(c->c_counts);
+    }
+    if (g.empty) {
+        FD_HIP_TRY(c, hipMemsetAsync(dc, 0, sizeof(int64_t) * batch, c->stream));
+    } else {
+        fdk::PointsArgs a{};
+        a.frames = dframes;
+        a.batch = batch;
+        a.rows = rows;
+        a.cols = cols;
+        a.tiles_x = g.tiles_x;
+        a.tiles_y = g.tiles_y;
+        a.tile_h = g.tile_h;
+        a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
+        a.thr = opts->min_valid_response;
+        a.mask = pi.mask;
+        a.mask_wpr = pi.wpr;
+        a.seg_cnt = as<int32_t>(c->seg_cnt);
+        a.seg = as<fdk::Cand>(c->seg);
+        a.resp_map = dmap;
+        if (kind == FD_FAST) {
+            rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
+            if (rc) return rc;
+            if (pi.mask) {
+                if (rows > 4096) return fail(c, FD_ERR_INVALID, "FAST with prior features supports rows <= 4096");
+                FD_HIP_TRY(c, ensure(c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
+                FD_HIP_TRY(c, ensure(c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * pi.wpr));
+                FD_HIP_TRY(c, fdk::launch_fast_mask_scan(pi.mask, pi.wpr, batch, rows, cols, as<int32_t>(c->row_base),
+                                                         as<int32_t>(c->word_pref), c->stream));
+                a.row_base = as<int32_t>(c->row_base);
+                a.word_pref = as<int32_t>(c->word_pref);
+            }
+            FD_HIP_TRY(c, fdk::launch_fast(true, a, c->off, c->stream));
+        } else {
+            FD_HIP_TRY(c, fdk::launch_corner(kind, true, a, c->stream));
+        }
+        fdk::CompactArgs k{};
+        k.seg_cnt = a.seg_cnt;
+        k.seg = a.seg;
+        k.rows = rows;
+        k.cols = cols;
+        k.tiles_x = g.tiles_x;
+        k.seg_cap = segcap;
+        k.row_lo = g.border;
+        k.row_hi = rows - g.border;
+        k.out_resp = dr;
+        k.out_x = dx;
+        k.out_y = dy;
+        k.cap = cand_cap;
+        k.out_counts = dc;
+        FD_HIP_TRY(c, fdk::launch_compact(k, batch, c->stream));
+    }
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dc, sizeof(int64_t) * batch, hipMemcpyDeviceToHost, c->stream));
+        if (cand_cap > 0) {
+            FD_HIP_TRY(c, hipMemcpyAsync(out_resp, dr, sizeof(float) * cand_cap * batch, hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(out_x, dx, sizeof(int32_t) * cand_cap * batch, hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(out_y, dy, sizeof(int32_t) * cand_cap * batch, hipMemcpyDeviceToHost, c->stream));
+        }
+        if (out_response_map)
+            FD_HIP_TRY(c, hipMemcpyAsync(out_response_map, dmap, sizeof(float) * npx, hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int b = 0; b < batch; ++b)
+            if (out_counts[b] > cand_cap) return fail(c, FD_ERR_CAPACITY, "cand_cap smaller than the candidates found");
+    } else if (!frames_on_device) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    return FD_OK;
+}
+
+int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols, float min_norm,
+               float *norm, float *angle, uint8_t *valid, int32_t *valid_idx, int64_t idx_cap, int64_t *valid_counts,
+               int outputs_on_device) {
+    int rc = check_shape(c, FD_HARRIS, batch, rows, cols, false);
+    if (rc) return rc;
+    if (rows < 2 || cols < 2) return fail(c, FD_ERR_INVALID, "LSD needs rows >= 2 and cols >= 2");  // :14
+    if (!valid_counts || idx_cap < 0 || (idx_cap > 0 && !valid_idx))
+        return fail(c, FD_ERR_INVALID, "bad output arguments");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    const uint8_t *dframes = nullptr;
+    rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
+    if (rc) return rc;
+    const int mc = cols - 1;
+    const size_t nmap = static_cast<size_t>(batch) * (rows - 1) * mc;
+    float *dn = nullptr, *da = nullptr;
+    uint8_t *dv = nullptr;
+    if (outputs_on_device) {
+        dn = norm;
+        da = angle;
+        dv = valid;
+    } else {
+        if (norm) {
+            FD_HIP_TRY(c, ensure(c->l_norm, sizeof(float) * nmap));
+            dn = as<float>(c->l_norm);
+        }
+        if (angle) {
+            FD_HIP_TRY(c, ensure(c->l_angle, sizeof(float) * nmap));
+            da = as<float>(c->l_angle);
+        }
+    }
+    if (dv == nullptr) {  // the valid map is needed internally for the ordered scatter
+        FD_HIP_TRY(c, ensure(c->l_valid, nmap));
+        dv = as<uint8_t>(c->l_valid);
+    }
+    if (dn) FD_HIP_TRY(c, hipMemsetAsync(dn, 0, sizeof(float) * nmap, c->stream));
+    if (da) FD_HIP_TRY(c, hipMemsetAsync(da, 0, sizeof(float) * nmap, c->stream));
+    FD_HIP_TRY(c, hipMemsetAsync(dv, 0, nmap, c->stream));
+
+    int32_t *di = valid_idx;
+    int64_t *dc = valid_counts;
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, ensure(c->l_idx, sizeof(int32_t) * static_cast<size_t>(std::max<int64_t>(idx_cap, 1)) * batch));
+        FD_HIP_TRY(c, ensure(c->l_counts, sizeof(int64_t) * batch));
+        di = as<int32_t>(c->l_idx);
+        dc = as<int64_t>(c->l_counts);
+    }
+    const int work_rows = rows - 3;  // rows [1, rows-3]
+    const int work_cols = cols - 3;  // cols [1, cols-3]
+    if (work_rows <= 0 || work_cols <= 0) {
+        FD_HIP_TRY(c, hipMemsetAsync(dc, 0, sizeof(int64_t) * batch, c->stream));
+    } else {
+        fdk::LsdArgs a{};
+        a.frames = dframes;
+        a.batch = batch;
+        a.rows = rows;
+        a.cols = cols;
+        a.strips = (cols - 2 + 63) / 64;
+        const int64_t target = 8192;
+        int64_t ch = (static_cast<int64_t>(batch) * a.strips * work_rows) / target;
+        ch = std::max<int64_t>(16, std::min<int64_t>(ch, 256));
+        a.chunk_h = static_cast<int>(ch);
+        a.chunks = (work_rows + a.chunk_h - 1) / a.chunk_h;
+        a.min_norm = min_norm;
+        a.norm = dn;
+        a.angle = da;
+        a.valid = dv;
+        const size_t ncnt = static_cast<size_t>(batch) * mc * a.chunks;
+        FD_HIP_TRY(c, ensure(c->l_cnt, sizeof(int32_t) * ncnt));
+        FD_HIP_TRY(c, ensure(c->l_base, sizeof(int32_t) * ncnt));
+        a.col_cnt = as<int32_t>(c->l_cnt);
+        a.col_base = as<int32_t>(c->l_base);
+        a.idx = di;
+        a.idx_cap = idx_cap;
+        a.counts = dc;
+        FD_HIP_TRY(c, fdk::launch_lsd(a, c->stream));
+    }
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, hipMemcpyAsync(valid_counts, dc, sizeof(int64_t) * batch, hipMemcpyDeviceToHost, c->stream));
+        if (idx_cap > 0)
+            FD_HIP_TRY(c, hipMemcpyAsync(valid_idx, di, sizeof(int32_t) * idx_cap * batch, hipMemcpyDeviceToHost, c->stream));
+        if (norm) FD_HIP_TRY(c, hipMemcpyAsync(norm, dn, sizeof(float) * nmap, hipMemcpyDeviceToHost, c->stream));
+        if (angle) FD_HIP_TRY(c, hipMemcpyAsync(angle, da, sizeof(float) * nmap, hipMemcpyDeviceToHost, c->stream));
+        if (valid) FD_HIP_TRY(c, hipMemcpyAsync(valid, dv, nmap, hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int b = 0; b < batch; ++b)
+            if (valid_counts[b] > idx_cap) return fail(c, FD_ERR_CAPACITY, "idx_cap smaller than the valid pixels");
+    } else if (!frames_on_device) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    return FD_OK;
+}
+
+}  // extern "C"

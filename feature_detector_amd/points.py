@@ -1,0 +1,260 @@
+"""Batch host API over libfdhip.so: contexts, point detection, candidates, LSD map.
+
+Inputs are numpy arrays (host memory, staged by the library) or torch CUDA/ROCm tensors (device
+memory, used in place on the context's stream, which follows torch's current stream). Every call
+runs the HIP kernels; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import FD_FAST, FD_HARRIS, FD_SHI_TOMASI, fd_point_opts
+
+KINDS = {"harris": FD_HARRIS, "shi_tomasi": FD_SHI_TOMASI, "fast": FD_FAST}
+
+_ctx_lock = threading.Lock()
+_contexts: dict[int, "Context"] = {}
+
+
+class Context:
+    """One fd_ctx: a HIP stream and grow-only device workspace on one GPU (not thread-safe)."""
+
+    def __init__(self, device: int = 0):
+        L = _lib.load()
+        p = ctypes.c_void_p()
+        rc = L.fd_ctx_create(int(device), ctypes.byref(p))
+        if rc != _lib.FD_OK:
+            raise _lib.FdError(rc, f"fd_ctx_create(device={device}) failed (is a GPU visible?)")
+        self.ptr = p
+        self.device = int(device)
+
+    def close(self):
+        if self.ptr:
+            _lib.load().fd_ctx_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int | None):
+        """Run on the given hipStream_t (0 = the HIP null stream); None = the context's own stream."""
+        if stream_handle is None:
+            _lib.check(self.ptr, _lib.load().fd_ctx_use_own_stream(self.ptr))
+        else:
+            _lib.check(self.ptr, _lib.load().fd_ctx_set_stream(self.ptr, ctypes.c_void_p(int(stream_handle))))
+
+    def synchronize(self):
+        _lib.check(self.ptr, _lib.load().fd_ctx_synchronize(self.ptr))
+
+    def reserve(self, kind: int, batch: int, rows: int, cols: int, max_prior_total: int = 0):
+        _lib.check(self.ptr, _lib.load().fd_ctx_reserve(self.ptr, kind, batch, rows, cols, max_prior_total))
+
+
+def default_context(device: int = 0) -> Context:
+    with _ctx_lock:
+        c = _contexts.get(device)
+        if c is None:
+            c = Context(device)
+            _contexts[device] = c
+        return c
+
+
+def _is_torch_device_tensor(x) -> bool:
+    return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+def _frames(x):
+    """(pointer, on_device, batch, rows, cols, keepalive) for a u8 [B,]R,C array or tensor."""
+    if _is_torch_device_tensor(x):
+        import torch
+
+        if x.dtype != torch.uint8:
+            raise TypeError("frames must be uint8")
+        if not x.is_contiguous():
+            x = x.contiguous()
+        shape = tuple(x.shape)
+        ptr, on_dev = x.data_ptr(), 1
+    else:
+        x = np.ascontiguousarray(x)
+        if x.dtype != np.uint8:
+            raise TypeError("frames must be uint8")
+        shape = x.shape
+        ptr, on_dev = x.ctypes.data, 0
+    if len(shape) == 2:
+        b, r, c = 1, shape[0], shape[1]
+    elif len(shape) == 3:
+        b, r, c = shape
+    else:
+        raise ValueError("frames must be [rows, cols] or [batch, rows, cols]")
+    return ptr, on_dev, int(b), int(r), int(c), x
+
+
+def _bind_stream(ctx: Context, on_device: bool):
+    if on_device:
+        import torch
+
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    else:
+        ctx.set_stream(None)
+
+
+def _priors(prior, batch):
+    """prior: None, or a list (per frame) of (n_i, 2) float arrays of (x, y)."""
+    if prior is None:
+        return None, None, None
+    if len(prior) != batch:
+        raise ValueError("prior must have one entry per frame")
+    counts = np.array([len(p) for p in prior], np.int32)
+    flat = (np.concatenate([np.asarray(p, np.float32).reshape(-1, 2) for p in prior]) if counts.sum() > 0
+            else np.zeros((1, 2), np.float32))
+    flat = np.ascontiguousarray(flat, np.float32)
+    return flat, counts, (flat, counts)
+
+
+@dataclass
+class DetectResult:
+    xy: object  # [batch, stride, 2] float32 (numpy or torch)
+    counts: object  # [batch] int32
+
+    def features(self, b: int) -> np.ndarray:
+        xy = self.xy if isinstance(self.xy, np.ndarray) else self.xy.cpu().numpy()
+        n = int(self.counts[b]) if isinstance(self.counts, np.ndarray) else int(self.counts[b].item())
+        return xy[b, :n].copy()
+
+
+def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_valid_response: float = 0.1,
+                  prior=None, ctx: Context | None = None, out=None) -> DetectResult:
+    """FeaturePointDetector::DetectGoodFeatures on a batch (include/fd_hip.h fd_points_detect).
+
+    Returns the NEW features per frame (x, y), in selection order. With torch device frames the
+    outputs are device tensors (asynchronous on the current stream); `out` may pass preallocated
+    (xy, counts) tensors so that repeated calls allocate nothing (graph capture).
+    """
+    kind = KINDS[kind] if isinstance(kind, str) else int(kind)
+    ptr, on_dev, b, r, c, keep = _frames(frames)
+    ctx = ctx or default_context()
+    _bind_stream(ctx, bool(on_dev))
+    opts = fd_point_opts(int(min_feature_distance), float(min_valid_response))
+    pxy, pcnt, _keep2 = _priors(prior, b)
+    stride = max(int(need), 1) + 1
+    if on_dev:
+        import torch
+
+        if out is None:
+            xy = torch.empty((b, stride, 2), dtype=torch.float32, device=frames.device)
+            cnt = torch.empty((b,), dtype=torch.int32, device=frames.device)
+        else:
+            xy, cnt = out
+            stride = xy.shape[1]
+        xy_ptr, cnt_ptr = xy.data_ptr(), cnt.data_ptr()
+    else:
+        xy = np.zeros((b, stride, 2), np.float32)
+        cnt = np.zeros((b,), np.int32)
+        xy_ptr, cnt_ptr = xy.ctypes.data, cnt.ctypes.data
+    rc = _lib.load().fd_points_detect(
+        ctx.ptr, kind, ctypes.c_void_p(ptr), on_dev, b, r, c, ctypes.byref(opts),
+        ctypes.c_void_p(pxy.ctypes.data) if pxy is not None else None,
+        ctypes.c_void_p(pcnt.ctypes.data) if pcnt is not None else None,
+        int(need), ctypes.c_void_p(xy_ptr), stride, ctypes.c_void_p(cnt_ptr), on_dev)
+    _lib.check(ctx.ptr, rc)
+    del keep
+    return DetectResult(xy, cnt)
+
+
+def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx: Context | None = None):
+    """The per-pixel stage alone (fd_points_response) on torch device frames [B, R, C].
+
+    Returns (cands, counts): cands int64 [B, cap] holding (float response, uint32 raster index)
+    pairs in unspecified order, counts int32 [B]. Asynchronous on torch's current stream.
+    """
+    import torch
+
+    kind = KINDS[kind] if isinstance(kind, str) else int(kind)
+    ptr, on_dev, b, r, c, keep = _frames(frames)
+    if not on_dev:
+        raise TypeError("point_response takes device frames")
+    ctx = ctx or default_context()
+    _bind_stream(ctx, True)
+    cap = r * c if kind == FD_FAST else r * c // 2 + 64
+    if out is None:
+        cands = torch.empty((b, cap), dtype=torch.int64, device=frames.device)
+        counts = torch.empty((b,), dtype=torch.int32, device=frames.device)
+    else:
+        cands, counts = out
+        cap = cands.shape[1]
+    opts = fd_point_opts(15, float(min_valid_response))
+    rc = _lib.load().fd_points_response(ctx.ptr, kind, ctypes.c_void_p(ptr), b, r, c, ctypes.byref(opts),
+                                        ctypes.c_void_p(cands.data_ptr()), int(cap),
+                                        ctypes.c_void_p(counts.data_ptr()))
+    _lib.check(ctx.ptr, rc)
+    del keep
+    return cands, counts
+
+
+def point_candidates(kind, frames, min_feature_distance: int = 15, min_valid_response: float = 0.1, prior=None,
+                     cap: int | None = None, response_map: bool = False, ctx: Context | None = None):
+    """The ComputeCandidates seam (fd_points_candidates): raster-ordered candidates per frame.
+
+    Host (numpy) frames only. Returns a list of (resp, x, y) arrays per frame, and the response map
+    [batch, rows, cols] if requested.
+    """
+    kind = KINDS[kind] if isinstance(kind, str) else int(kind)
+    ptr, on_dev, b, r, c, keep = _frames(frames)
+    if on_dev:
+        raise TypeError("point_candidates takes host frames")
+    ctx = ctx or default_context()
+    _bind_stream(ctx, False)
+    opts = fd_point_opts(int(min_feature_distance), float(min_valid_response))
+    pxy, pcnt, _keep2 = _priors(prior, b)
+    if cap is None:
+        cap = r * c if kind == FD_FAST else r * c // 2 + 16
+    resp = np.zeros((b, max(cap, 1)), np.float32)
+    xs = np.zeros((b, max(cap, 1)), np.int32)
+    ys = np.zeros((b, max(cap, 1)), np.int32)
+    counts = np.zeros((b,), np.int64)
+    rmap = np.zeros((b, r, c), np.float32) if response_map else None
+    rc = _lib.load().fd_points_candidates(
+        ctx.ptr, kind, ctypes.c_void_p(ptr), 0, b, r, c, ctypes.byref(opts),
+        ctypes.c_void_p(pxy.ctypes.data) if pxy is not None else None,
+        ctypes.c_void_p(pcnt.ctypes.data) if pcnt is not None else None,
+        ctypes.c_void_p(resp.ctypes.data), ctypes.c_void_p(xs.ctypes.data), ctypes.c_void_p(ys.ctypes.data),
+        int(cap), ctypes.c_void_p(counts.ctypes.data),
+        ctypes.c_void_p(rmap.ctypes.data) if rmap is not None else None, 0)
+    _lib.check(ctx.ptr, rc)
+    del keep
+    out = [(resp[i, :counts[i]].copy(), xs[i, :counts[i]].copy(), ys[i, :counts[i]].copy()) for i in range(b)]
+    return (out, rmap) if response_map else out
+
+
+def lsd_map(frames, min_norm: float = 20.0, cap: int | None = None, ctx: Context | None = None):
+    """ComputeLineLevelAngleMap (fd_lsd_map) on host frames.
+
+    Returns per frame (norm, angle, valid, valid_idx_colmajor); maps are (rows-1, cols-1).
+    """
+    ptr, on_dev, b, r, c, keep = _frames(frames)
+    if on_dev:
+        raise TypeError("lsd_map takes host frames")
+    ctx = ctx or default_context()
+    _bind_stream(ctx, False)
+    mr, mc = r - 1, c - 1
+    cap = mr * mc if cap is None else cap
+    norm = np.zeros((b, mr, mc), np.float32)
+    ang = np.zeros((b, mr, mc), np.float32)
+    val = np.zeros((b, mr, mc), np.uint8)
+    idx = np.zeros((b, max(cap, 1)), np.int32)
+    cnt = np.zeros((b,), np.int64)
+    rc = _lib.load().fd_lsd_map(ctx.ptr, ctypes.c_void_p(ptr), 0, b, r, c, float(min_norm),
+                                ctypes.c_void_p(norm.ctypes.data), ctypes.c_void_p(ang.ctypes.data),
+                                ctypes.c_void_p(val.ctypes.data), ctypes.c_void_p(idx.ctypes.data), int(cap),
+                                ctypes.c_void_p(cnt.ctypes.data), 0)
+    _lib.check(ctx.ptr, rc)
+    del keep
+    return [(norm[i], ang[i], val[i], idx[i, :cnt[i]].copy()) for i in range(b)]

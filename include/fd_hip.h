@@ -1,0 +1,133 @@
+/*
+ * fd_hip.h -- C ABI of the MI355X feature-detection hot path (libfdhip.so).
+ *
+ * Plain C, no HIP/torch types: pointers, sizes and status codes only. A context owns one HIP stream
+ * (or borrows the caller's) and all device workspace; calls on different contexts may run
+ * concurrently from different host threads (one context per GPU is the multi-GPU model).
+ *
+ * Each entry point names the reference interface it replaces (paths relative to
+ * Horizon1026/Feature_Detector/src/). The reference has no FFI of its own: its seams are the C++
+ * virtual FeaturePointDetector::ComputeCandidates (feature_point_detector.h:44, called at
+ * feature_point_detector.cpp:20), the whole DetectGoodFeatures (feature_point_detector.h:29), and the
+ * private FeatureLineDetector::ComputeLineLevelAngleMap (feature_line_detector.h:66, called at
+ * feature_line_detector.cpp:22). The C++ drop-in classes in include/feature_detector/ call these.
+ *
+ * Conventions: every function returns FD_OK (0) or an FD_ERR_* code; fd_last_error() describes the
+ * last failure on that context. Pointers flagged "*_on_device" are HIP device pointers on the
+ * context's device, otherwise host pointers. Device-pointer calls are asynchronous on the context
+ * stream; host-pointer outputs are complete when the call returns.
+ */
+#ifndef FD_HIP_H_
+#define FD_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FD_OK 0
+#define FD_ERR_INVALID 1  /* bad argument */
+#define FD_ERR_HIP 2      /* HIP runtime error (allocation, launch, copy) */
+#define FD_ERR_CAPACITY 3 /* an output capacity was too small; counts still report true sizes */
+
+typedef struct fd_ctx fd_ctx;
+
+/* Detector kinds: FeaturePointHarrisDetector (feature_point_harris_detector.h:9),
+ * FeaturePointShiTomasDetector (feature_point_shi_tomas_detector.h:9),
+ * FeaturePointFastDetector (feature_point_fast_detector.h:9). */
+enum fd_point_kind { FD_HARRIS = 0, FD_SHI_TOMASI = 1, FD_FAST = 2 };
+
+/* FeaturePointDetector::Options (feature_point_detector.h:15-20) fields used on the hot path.
+ * The SubOptions of the reference are private constants and fixed here: Harris kAlpha = 0.04 and
+ * kHalfPatchSize = 1 (feature_point_harris_detector.h:12-15), Shi-Tomasi kHalfPatchSize = 1
+ * (feature_point_shi_tomas_detector.h:12-14), FAST kN = 12 and kMinPixelDiffValue = 15
+ * (feature_point_fast_detector.h:12-15). */
+typedef struct fd_point_opts {
+    int32_t min_feature_distance; /* kMinFeatureDistance, default 15 */
+    float min_valid_response;     /* kMinValidResponse,  default 0.1 */
+} fd_point_opts;
+
+/* ---- context ---------------------------------------------------------------------------------- */
+int fd_ctx_create(int device, fd_ctx **out);
+void fd_ctx_destroy(fd_ctx *ctx);
+const char *fd_last_error(const fd_ctx *ctx);
+/* Run on the caller's hipStream_t from now on (NULL = the HIP null stream, e.g. PyTorch's default
+ * stream). A new context runs on a non-blocking stream of its own; fd_ctx_use_own_stream restores it. */
+int fd_ctx_set_stream(fd_ctx *ctx, void *hip_stream);
+int fd_ctx_use_own_stream(fd_ctx *ctx);
+void *fd_ctx_get_stream(const fd_ctx *ctx);
+int fd_ctx_synchronize(fd_ctx *ctx);
+/* Pre-size device workspace for a (kind, batch, rows, cols) shape so that later calls of that shape
+ * allocate nothing (required before hipGraph capture of fd_points_detect). */
+int fd_ctx_reserve(fd_ctx *ctx, int kind, int batch, int rows, int cols, int64_t max_prior_total);
+
+/* ---- corner / FAST points ----------------------------------------------------------------------- */
+/*
+ * fd_points_detect -- FeaturePointDetector::DetectGoodFeatures (feature_point_detector.cpp:7-25) on a
+ * batch of independent frames: mask from prior features (:12-16, :90-98), candidates
+ * (ComputeCandidates: Harris feature_point_harris_detector.cpp:5-137, Shi-Tomasi
+ * feature_point_shi_tomas_detector.cpp:5-137, FAST feature_point_fast_detector.cpp:11-98), sort by
+ * response and greedy min-distance selection (SelectGoodFeatures :54-88).
+ *
+ *   frames        batch * rows * cols u8, row-major, frame-contiguous (GrayImage layout)
+ *   prior_xy      all frames' incoming `features` (x, y float pairs) concatenated, or NULL
+ *   prior_counts  batch entries (number of prior features of each frame), or NULL
+ *   need          needed_feature_num (counts the prior features, checked after each append, :67-69)
+ *   out_xy        batch * out_stride (x, y) float pairs: the NEW features of each frame, in order
+ *   out_counts    batch int32: number of new features per frame
+ * Candidate order: response descending, ties by raster index ascending (the reference's std::sort
+ * is unstable; see DESIGN.md "Tie order"). out_stride must be >= min(need, candidates) + 1.
+ */
+int fd_points_detect(fd_ctx *ctx, int kind, const uint8_t *frames, int frames_on_device, int batch, int rows,
+                     int cols, const fd_point_opts *opts, const float *prior_xy, const int32_t *prior_counts,
+                     uint32_t need, float *out_xy, int32_t out_stride, int32_t *out_counts, int outputs_on_device);
+
+/*
+ * fd_points_candidates -- the ComputeCandidates seam (feature_point_detector.h:44): per frame, the
+ * candidates in the order the reference pushes them (raster order), as (response, x, y). Mask rules
+ * as above. Writes at most cand_cap per frame at [b * cand_cap]; out_counts (int64) gets the true
+ * count (FD_ERR_CAPACITY if any exceeds cand_cap). Optionally also returns the response map
+ * (batch * rows * cols float, 0 where not stored; NULL to skip) -- Harris/Shi-Tomasi responses_
+ * (feature_point_harris_detector.cpp:74-75,100-102); for FAST the map holds score + offset of every
+ * candidate pixel and 0 elsewhere.
+ */
+int fd_points_candidates(fd_ctx *ctx, int kind, const uint8_t *frames, int frames_on_device, int batch, int rows,
+                         int cols, const fd_point_opts *opts, const float *prior_xy, const int32_t *prior_counts,
+                         float *out_resp, int32_t *out_x, int32_t *out_y, int64_t cand_cap, int64_t *out_counts,
+                         float *out_response_map, int outputs_on_device);
+
+/*
+ * fd_points_response -- the per-pixel stage alone (response + NMS for Harris/Shi-Tomasi, segment test
+ * + offset for FAST), i.e. ComputeCandidates without ordering: per frame, the candidates as
+ * (response float, raster index uint32) pairs in unspecified order at out_cands[b * cand_cap], and
+ * their count in out_counts[b] (uint32). Device pointers only (frames and outputs). Used to time the
+ * hot kernel alone and by callers that select features themselves.
+ */
+int fd_points_response(fd_ctx *ctx, int kind, const uint8_t *frames, int batch, int rows, int cols,
+                       const fd_point_opts *opts, void *out_cands, int64_t cand_cap, uint32_t *out_counts);
+
+/* ---- LSD level-line map ------------------------------------------------------------------------ */
+/*
+ * fd_lsd_map -- FeatureLineDetector::ComputeLineLevelAngleMap (feature_line_detector.cpp:56-97).
+ * Maps are (rows-1) x (cols-1) per frame, row-major, computed for row in [1, rows-3] and col in
+ * [1, cols-3] and 0 elsewhere:
+ *   norm   gradient_norm (:82)          (float, NULL to skip)
+ *   angle  line_level_angle (:85)       (float, 0 where not valid; NULL to skip)
+ *   valid  is_valid = norm > min_norm   (u8, NULL to skip)
+ * valid_idx receives, per frame at [b * idx_cap], the row-major map index (row * (cols-1) + col) of
+ * every valid pixel in the reference's scan order (column outer, row inner, :71-72, :86), i.e.
+ * sorted_pixels_ before its std::sort (:92). valid_counts (int64) gets the true counts.
+ */
+int fd_lsd_map(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols, float min_norm,
+               float *norm, float *angle, uint8_t *valid, int32_t *valid_idx, int64_t idx_cap, int64_t *valid_counts,
+               int outputs_on_device);
+
+/* ---- build info --------------------------------------------------------------------------------- */
+const char *fd_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FD_HIP_H_ */

@@ -1,0 +1,168 @@
+"""ctypes binding of the CPU oracle (oracle/fd_oracle.cpp). TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, and only
+as the checker / the timed CPU baseline. The product path (feature_detector_amd) never imports it.
+Each wrapper names the reference function it restates (paths relative to /root/reference/src/).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "liborc.so")
+SRC = os.path.join(HERE, "fd_oracle.cpp")
+
+HARRIS, SHI_TOMASI, FAST = 0, 1, 2
+_P = ctypes.c_void_p
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with the reference build's float semantics (no -march => no FMA)."""
+    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(SRC):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        i32, i64, f32, u32, u8 = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint32, ctypes.c_uint8
+        sig = {
+            "orc_tensor_sums": (None, [_P, i32, i32, _P, _P, _P]),
+            "orc_response_map": (None, [_P, i32, i32, i32, f32, _P, _P]),
+            "orc_nms": (i64, [_P, i32, i32, f32, _P, _P, _P, i64]),
+            "orc_fast_score": (i32, [_P, i32, i32, i32, i32, i32]),
+            "orc_fast_candidates": (i64, [_P, i32, i32, f32, _P, _P, _P, _P, i64]),
+            "orc_fast_offsets": (None, [i64, _P]),
+            "orc_detect": (i64, [i32, _P, i32, i32, i32, f32, u32, _P, i32, i32, _P, i32, _P, _P, _P, _P, i64]),
+            "orc_prefix_has_ties": (i32, [_P, i64]),
+            "orc_sparsify": (None, [_P, i32, i32, i32, i32, i32, u8, u8, _P, _P]),
+            "orc_lsd_map": (i64, [_P, i32, i32, f32, _P, _P, _P, _P, i64]),
+            "orc_lsd_sort": (None, [_P, _P, i64, i32]),
+            "orc_lsd_min_region_size": (u32, [i32, i32, f32]),
+            "orc_make_frame": (None, [i32, u32, i32, i32, i32, _P]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def make_frame(pattern: str, seed: int, rows: int, cols: int, period: int = 16) -> np.ndarray:
+    """Seeded synthetic frame: 'noise' (uniform u8) or 'checker' (period-px 60/180 + U[-10,10])."""
+    out = np.empty((rows, cols), np.uint8)
+    lib().orc_make_frame(0 if pattern == "noise" else 1, seed, rows, cols, period, _ptr(out))
+    return out
+
+
+def response_map(img, kind, thr, mask=None):
+    img = np.ascontiguousarray(img, np.uint8)
+    R, C = img.shape
+    out = np.zeros((R, C), np.float32)
+    m = None if mask is None else np.ascontiguousarray(mask, np.int32)
+    lib().orc_response_map(_ptr(img), R, C, kind, thr, _ptr(m), _ptr(out))
+    return out
+
+
+def tensor_sums(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    R, C = img.shape
+    a, b, c = (np.zeros((R, C), np.int32) for _ in range(3))
+    lib().orc_tensor_sums(_ptr(img), R, C, _ptr(a), _ptr(b), _ptr(c))
+    return a, b, c
+
+
+def nms(resp, thr):
+    resp = np.ascontiguousarray(resp, np.float32)
+    R, C = resp.shape
+    cap = R * C // 2 + 16
+    r, x, y = np.zeros(cap, np.float32), np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+    n = lib().orc_nms(_ptr(resp), R, C, thr, _ptr(r), _ptr(x), _ptr(y), cap)
+    return r[:n], x[:n], y[:n]
+
+
+def fast_candidates(img, thr, mask=None):
+    img = np.ascontiguousarray(img, np.uint8)
+    R, C = img.shape
+    cap = R * C
+    r, x, y = np.zeros(cap, np.float32), np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+    m = None if mask is None else np.ascontiguousarray(mask, np.int32)
+    n = lib().orc_fast_candidates(_ptr(img), R, C, thr, _ptr(m), _ptr(r), _ptr(x), _ptr(y), cap)
+    return r[:n], x[:n], y[:n]
+
+
+def fast_offsets(n):
+    out = np.zeros(n, np.float32)
+    lib().orc_fast_offsets(n, _ptr(out))
+    return out
+
+
+def detect(kind, img, dist, thr, need, prior=None, sort_mode=0):
+    """FeaturePointDetector::DetectGoodFeatures (feature_point_detector.cpp:7-25) for one frame.
+
+    Returns (new_features[n,2] float32 (x, y), sorted candidates (resp, x, y)).
+    sort_mode 0 = reference std::sort order, 1 = stable (response desc, raster asc).
+    """
+    img = np.ascontiguousarray(img, np.uint8)
+    R, C = img.shape
+    pr = np.zeros((1, 2), np.float32) if prior is None or len(prior) == 0 else np.ascontiguousarray(prior, np.float32)
+    n_prior = 0 if prior is None else len(prior)
+    out_cap = max(int(need) + 1, 1)
+    out = np.zeros((out_cap, 2), np.float32)
+    nout = ctypes.c_int(0)
+    cap = R * C
+    cr, cx, cy = np.zeros(cap, np.float32), np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+    n = lib().orc_detect(kind, _ptr(img), R, C, dist, thr, need, _ptr(pr), n_prior, sort_mode, _ptr(out), out_cap,
+                         ctypes.byref(nout), _ptr(cr), _ptr(cx), _ptr(cy), cap)
+    return out[: nout.value].copy(), (cr[:n].copy(), cx[:n].copy(), cy[:n].copy())
+
+
+def prefix_has_ties(sorted_resp, n_scanned):
+    a = np.ascontiguousarray(sorted_resp, np.float32)
+    return bool(lib().orc_prefix_has_ties(_ptr(a), int(n_scanned)))
+
+
+def sparsify(xy, rows, cols, grid_rows=12, grid_cols=12, need_filter=1, after_filter=0, status=None):
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    n = len(xy)
+    st = np.ones(n, np.uint8) if status is None or len(status) != n else np.array(status, np.uint8)
+    gm = np.zeros((grid_rows, grid_cols), np.int32)
+    lib().orc_sparsify(_ptr(xy), n, rows, cols, grid_rows, grid_cols, need_filter, after_filter, _ptr(st), _ptr(gm))
+    return st, gm
+
+
+def lsd_map(img, min_norm=20.0):
+    img = np.ascontiguousarray(img, np.uint8)
+    R, C = img.shape
+    norm = np.zeros((R - 1, C - 1), np.float32)
+    ang = np.zeros((R - 1, C - 1), np.float32)
+    val = np.zeros((R - 1, C - 1), np.uint8)
+    cap = (R - 1) * (C - 1)
+    idx = np.zeros(cap, np.int32)
+    n = lib().orc_lsd_map(_ptr(img), R, C, min_norm, _ptr(norm), _ptr(ang), _ptr(val), _ptr(idx), cap)
+    return norm, ang, val, idx[:n].copy()
+
+
+def lsd_sort(norm, idx, sort_mode=0):
+    norm = np.ascontiguousarray(norm, np.float32)
+    idx = np.array(idx, np.int32)
+    lib().orc_lsd_sort(_ptr(norm), _ptr(idx), len(idx), sort_mode)
+    return idx
+
+
+def lsd_min_region_size(rows, cols, tol_rad=22.5 * 3.14159265358979323846 / 180.0):
+    return int(lib().orc_lsd_min_region_size(rows, cols, np.float32(tol_rad)))

@@ -1,0 +1,81 @@
+"""GPU parity of the LSD level-line map (fd_lsd_map) against the oracle: bit-exact norm, valid flag
+and angle (the kernel restates glibc's fdlibm atan2f), and the column-major valid list in the
+reference's scan order (sorted_pixels_ before its std::sort, feature_line_detector.cpp:71-92)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fd():
+    import feature_detector_amd as fd
+
+    fd.load()
+    return fd
+
+
+def check_lsd(fd, oracle, img, min_norm=20.0):
+    (n, a, v, idx), = fd.lsd_map(img, min_norm)
+    en, ea, ev, eidx = oracle.lsd_map(img, min_norm)
+    assert np.array_equal(n.view(np.uint32), en.view(np.uint32))
+    assert np.array_equal(v, ev)
+    assert np.array_equal(a.view(np.uint32), ea.view(np.uint32))
+    assert np.array_equal(idx, eidx)
+    # host std::sort of the GPU list reproduces the reference's sorted_pixels_ exactly
+    assert np.array_equal(oracle.lsd_sort(n, idx, 0), oracle.lsd_sort(en, eidx, 0))
+    return idx
+
+
+def test_image_png(fd, oracle, image_png, ref_counts):
+    idx = check_lsd(fd, oracle, image_png)
+    assert len(idx) == ref_counts["image_png"]["lsd_valid"]
+
+
+@pytest.mark.parametrize("rec_i", [0, 1, 2])
+def test_synthetic_counts(fd, oracle, ref_counts, rec_i):
+    rec = ref_counts["synthetic_lsd_valid"][rec_i]
+    img = oracle.make_frame(rec["pattern"], 1234, rec["rows"], rec["cols"], rec["period"])
+    idx = check_lsd(fd, oracle, img)
+    assert len(idx) == rec["valid"]
+
+
+@pytest.mark.parametrize("shape", [(2, 2), (3, 3), (4, 4), (5, 67), (67, 5), (100, 129), (257, 63)])
+def test_ragged(fd, oracle, shape):
+    img = np.random.default_rng(shape[0] * 1000 + shape[1]).integers(0, 256, shape, dtype=np.uint8)
+    check_lsd(fd, oracle, img, 20.0)
+
+
+@pytest.mark.parametrize("min_norm", [0.0, 5.0, 100.0, 400.0])
+def test_thresholds(fd, oracle, min_norm):
+    img = np.random.default_rng(3).integers(0, 256, (120, 200), dtype=np.uint8)
+    check_lsd(fd, oracle, img, min_norm)
+
+
+def test_angle_domain_exhaustive(fd, oracle):
+    """Every (ad, bc) gradient pair -> every half-integer (gx, gy): built as 2x2 blocks."""
+    vals = []
+    for ad in range(-255, 256):
+        for bc in range(-255, 256):
+            # I(r,c)=p, I(r+1,c+1)=p+ad, I(r,c+1)=q, I(r+1,c)=q-bc with values in [0,255]
+            p = max(0, -ad)
+            q = max(0, bc)
+            if p + ad > 255 or q - bc > 255 or q > 255:
+                continue
+            vals.append((p, q, q - bc, p + ad))
+    n = len(vals)
+    img = np.zeros((3, 2 * n + 2), np.uint8)
+    for i, (a, b, c, d) in enumerate(vals):
+        img[1, 1 + 2 * i], img[1, 2 + 2 * i] = a, b
+        img[2, 1 + 2 * i], img[2, 2 + 2 * i] = c, d
+    img = np.concatenate([img, np.zeros((2, img.shape[1]), np.uint8)])
+    check_lsd(fd, oracle, img, 0.0)
+
+
+def test_batch(fd, oracle):
+    frames = np.stack([oracle.make_frame("checker", s, 240, 320, 32) for s in range(5)])
+    res = fd.lsd_map(frames)
+    for b in range(5):
+        en, ea, ev, eidx = oracle.lsd_map(frames[b])
+        assert np.array_equal(res[b][3], eidx)
+        assert np.array_equal(res[b][1].view(np.uint32), ea.view(np.uint32))
