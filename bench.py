@@ -101,15 +101,16 @@ def kernel_time_ms(torch, fd, frames_pool, kind, thr, reps=50):
     stream it is launched on (torch's current stream, which the library context follows)."""
     b, r, c = frames_pool[0].shape
     cap = r * c if kind == "fast" else r * c // 2 + 64
-    cands = torch.empty((b, cap), dtype=torch.int64, device=frames_pool[0].device)
-    counts = torch.empty((b,), dtype=torch.int32, device=frames_pool[0].device)
+    dev = frames_pool[0].device
+    out = (torch.empty((b, cap), dtype=torch.float32, device=dev), torch.empty((b, cap), dtype=torch.int32, device=dev),
+           torch.empty((b,), dtype=torch.int32, device=dev))
     for i in range(3):
-        fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=(cands, counts))
+        fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=out)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for i in range(reps):
-        fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=(cands, counts))
+        fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=out)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps

@@ -65,7 +65,7 @@ def load() -> ctypes.CDLL:
                                    P, i32]),
         "fd_points_candidates": (i32, [P, i32, P, i32, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, P, P, P,
                                        i64, P, P, i32]),
-        "fd_points_response": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, i64, P]),
+        "fd_points_response": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
         "fd_lsd_map": (i32, [P, P, i32, i32, i32, i32, f32, P, P, P, P, i64, P, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
     }

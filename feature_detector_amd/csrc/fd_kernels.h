@@ -11,10 +11,12 @@ namespace fdk {
 constexpr int kTileW = 248;
 constexpr int kSegCorner = kTileW / 2;  // strict 4-neighbour NMS: <= 1 candidate per 2 columns
 constexpr int kSegFast = kTileW;        // FAST has no NMS
-constexpr int kSelectChunk = 4096;      // candidates sorted per greedy chunk (LDS)
+constexpr int kSelectChunk = 2048;      // candidates sorted per greedy chunk (LDS)
 constexpr int kGridLdsCells = 16384;    // occupancy grid kept in LDS up to this many cells
 constexpr int kMaxOffsetSegs = 48;
+constexpr int kHistBins = 4096;         // level-0 digit of the selection key: top 12 bits of the response
 
+// A raster-mode segment entry (fd_points_candidates only).
 struct Cand {
     float resp;
     uint32_t idx;  // row * cols + col
@@ -34,14 +36,17 @@ struct PointsArgs {
     const uint8_t *frames;
     int batch, rows, cols;
     int tiles_x, tiles_y, tile_h;
+    int blocks_per_frame;  // workgroups of 4 waves per frame (a workgroup never straddles frames)
     int aligned4;  // cols % 4 == 0 and 4-byte aligned frames: whole-dword loads are range-exact
     float thr;
     const uint32_t *mask;  // prior-feature bitmap [batch][rows][mask_wpr], bit = mask true; null = all ones
     int mask_wpr;
-    // detect mode: unordered per-frame lists
-    Cand *list;
+    // detect mode: unordered per-frame lists (SoA) + level-0 key histogram
+    float *list_resp;
+    uint32_t *list_idx;
     int64_t list_cap;
     uint32_t *list_count;
+    uint32_t *hist0;  // [batch][kHistBins] or null
     // raster mode: per (frame, row, tile_x) segments
     int32_t *seg_cnt;
     Cand *seg;
@@ -52,8 +57,10 @@ struct PointsArgs {
 };
 
 struct SelectArgs {
-    const Cand *list;
+    const float *list_resp;
+    const uint32_t *list_idx;
     const uint32_t *list_count;
+    const uint32_t *hist0;
     int64_t list_cap;
     int rows, cols;
     const uint32_t *mask;
@@ -66,6 +73,7 @@ struct SelectArgs {
     float *out_xy;
     int out_stride;
     int32_t *out_counts;
+    uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 
 struct CompactArgs {

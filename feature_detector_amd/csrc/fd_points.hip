@@ -24,12 +24,14 @@ constexpr float kInvCnt = 1.0f / 9.0f;                  // 1 / (3*3)  (:71)
 constexpr float kInvCnt2 = (1.0f / 9.0f) * (1.0f / 9.0f);  // harris :72
 constexpr float kHarrisAlpha = 0.04f;                  // feature_point_harris_detector.h:13
 
-__device__ __forceinline__ void decode_tile(const PointsArgs &a, int &f, int &ty, int &tx) {
-    int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-    tx = w % a.tiles_x;
-    w /= a.tiles_x;
-    ty = w % a.tiles_y;
-    f = w / a.tiles_y;
+// Workgroup -> (frame, 4 consecutive tiles of that frame); returns false for the idle waves of a
+// frame's last workgroup (they still take part in the workgroup barriers).
+__device__ __forceinline__ bool decode_tile(const PointsArgs &a, int &f, int &ty, int &tx) {
+    f = blockIdx.x / a.blocks_per_frame;
+    const int t = (blockIdx.x % a.blocks_per_frame) * 4 + (threadIdx.x >> 6);
+    tx = t % a.tiles_x;
+    ty = t / a.tiles_x;
+    return t < a.tiles_x * a.tiles_y;
 }
 
 // Dword of frame bytes [off, off+4). `aligned` (cols % 4 == 0) guarantees whole-dword range checks;
@@ -43,8 +45,10 @@ __device__ __forceinline__ uint32_t load_px4(__amdgpu_buffer_rsrc_t r, int32_t o
 // Per-wave candidate sink. Detect mode: stage in LDS, append to the frame's list with one atomic per
 // flush. Raster mode: write the (row, tile) segment in column order.
 struct Sink {
-    Cand *stage;
-    int n;  // staged entries (wave-uniform)
+    float *resp;     // LDS staging (detect mode)
+    uint32_t *idx;
+    uint32_t *hist;  // LDS level-0 histogram of the workgroup's frame, or null
+    int n;           // staged entries (wave-uniform)
 };
 
 __device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f) {
@@ -54,11 +58,15 @@ __device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t base = 0;
     if (lane_id() == 0) base = atomicAdd(&a.list_count[f], static_cast<uint32_t>(sk.n));
-    base = __shfl(base, 0);
-    Cand *dst = a.list + static_cast<int64_t>(f) * a.list_cap;
+    base = __builtin_amdgcn_readfirstlane(base);
+    float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
     for (int i = lane_id(); i < sk.n; i += kWave) {
         const int64_t pos = static_cast<int64_t>(base) + i;
-        if (pos < a.list_cap) dst[pos] = sk.stage[i];
+        if (pos < a.list_cap) {
+            dr[pos] = sk.resp[i];
+            di[pos] = sk.idx[i];
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -85,10 +93,15 @@ __device__ __forceinline__ void emit_row(Sink &sk, const PointsArgs &a, int f, i
     } else {
         if (tot == 0) return;
         if (sk.n + tot > kStage) sink_flush(sk, a, f);
-        Cand *dst = sk.stage + sk.n;
+        pos += sk.n;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
-            if (fl[m]) dst[pos++] = Cand{v[m], rowbase + static_cast<uint32_t>(c0 + m)};
+            if (fl[m]) {
+                sk.resp[pos] = v[m];
+                sk.idx[pos] = rowbase + static_cast<uint32_t>(c0 + m);
+                if (sk.hist) atomicAdd(&sk.hist[float_key(v[m]) >> 20], 1u);
+                ++pos;
+            }
         sk.n += tot;
     }
 }
@@ -97,6 +110,25 @@ __device__ __forceinline__ uint32_t mask_bits4(const PointsArgs &a, int f, int r
     if (c0 < 0 || c0 >= a.cols) return 0u;
     const uint32_t w = a.mask[(static_cast<int64_t>(f) * a.rows + row) * a.mask_wpr + (c0 >> 5)];
     return (w >> (c0 & 31)) & 0xFu;
+}
+
+// Workgroup-shared staging + level-0 histogram (detect mode).
+struct DetectLds {
+    float resp[4][kStage];
+    uint32_t idx[4][kStage];
+    uint32_t hist[kHistBins];
+};
+
+__device__ __forceinline__ void hist_clear(uint32_t *h) {
+    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+}
+__device__ __forceinline__ void hist_flush(const uint32_t *h, uint32_t *g) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
+        const uint32_t v = h[b];
+        if (v) atomicAdd(&g[b], v);
+    }
 }
 
 // Stored response of one pixel (responses_ semantics: 0 unless written).
@@ -127,6 +159,9 @@ __device__ __forceinline__ float corner_response(int sxx, int syy, int sxy, floa
     return res;
 }
 
+template <int KIND, bool RASTER, bool MASKED>
+__device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, int tx, Sink &sk);
+
 // ---------------------------------------------------------------------------------------------------
 // K1: corner response + NMS. One wave per tile of kTileW columns x tile_h rows; lane l covers columns
 // c0 = tx*kTileW + 4(l-1) .. c0+3 and walks the rows keeping 3-row sliding windows in registers:
@@ -134,10 +169,24 @@ __device__ __forceinline__ float corner_response(int sxx, int syy, int sxy, floa
 // ---------------------------------------------------------------------------------------------------
 template <int KIND, bool RASTER, bool MASKED>
 __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
-    __shared__ Cand stage_all[RASTER ? 1 : 4][RASTER ? 1 : kStage];
+    __shared__ DetectLds lds_all[1];
     int f, ty, tx;
-    decode_tile(a, f, ty, tx);
-    if (f >= a.batch) return;
+    const bool active = decode_tile(a, f, ty, tx);
+    Sink sk{nullptr, nullptr, nullptr, 0};
+    if constexpr (!RASTER) {
+        const int wv = threadIdx.x >> 6;
+        sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0};
+        if (a.hist0) hist_clear(lds_all[0].hist);
+    }
+    if (active) corner_tile<KIND, RASTER, MASKED>(a, f, ty, tx, sk);
+    if constexpr (!RASTER) {
+        if (active) sink_flush(sk, a, f);
+        if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+    }
+}
+
+template <int KIND, bool RASTER, bool MASKED>
+__device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, int tx, Sink &sk) {
     const int lane = lane_id();
     const int rows = a.rows, cols = a.cols;
     const int c0 = tx * kTileW + 4 * (lane - 1);
@@ -145,7 +194,6 @@ __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
     const int y1 = min(y0 + a.tile_h, rows - 2);  // output rows [y0, y1) within [2, rows-3]
     const bool aligned = a.aligned4 != 0;
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
-    Sink sk{stage_all[RASTER ? 0 : (threadIdx.x >> 6)], 0};
 
     bool cval[4], colv[4];  // column inside [2, cols-3]; and owned by an interior lane (emitted)
 #pragma unroll
@@ -234,7 +282,6 @@ __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
             }
         }
     }
-    if constexpr (!RASTER) sink_flush(sk, a, f);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -280,8 +327,12 @@ __device__ __forceinline__ float fast_offset(int nseg, const int64_t *ks, const 
 }
 
 template <bool RASTER, bool MASKED>
+__device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int64_t *seg_k,
+                                          const double *seg_o, const double *seg_inc, int f, int ty, int tx, Sink &sk);
+
+template <bool RASTER, bool MASKED>
 __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
-    __shared__ Cand stage_all[RASTER ? 1 : 4][RASTER ? 1 : kStage];
+    __shared__ DetectLds lds_all[1];
     __shared__ int64_t seg_k[kMaxOffsetSegs];
     __shared__ double seg_o[kMaxOffsetSegs], seg_inc[kMaxOffsetSegs];
     if (threadIdx.x == 0)
@@ -292,8 +343,23 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
         }
     __syncthreads();
     int f, ty, tx;
-    decode_tile(a, f, ty, tx);
-    if (f >= a.batch) return;
+    const bool active = decode_tile(a, f, ty, tx);
+    Sink sk{nullptr, nullptr, nullptr, 0};
+    if constexpr (!RASTER) {
+        const int wv = threadIdx.x >> 6;
+        sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0};
+        if (a.hist0) hist_clear(lds_all[0].hist);
+    }
+    if (active) fast_tile<RASTER, MASKED>(a, off, seg_k, seg_o, seg_inc, f, ty, tx, sk);
+    if constexpr (!RASTER) {
+        if (active) sink_flush(sk, a, f);
+        if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+    }
+}
+
+template <bool RASTER, bool MASKED>
+__device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int64_t *seg_k,
+                                          const double *seg_o, const double *seg_inc, int f, int ty, int tx, Sink &sk) {
     const int lane = lane_id();
     const int rows = a.rows, cols = a.cols;
     const int c0 = tx * kTileW + 4 * (lane - 1);
@@ -301,7 +367,6 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
     const int y1 = min(y0 + a.tile_h, rows - 3);  // output rows [y0, y1) within [3, rows-4]
     const bool aligned = a.aligned4 != 0;
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
-    Sink sk{stage_all[RASTER ? 0 : (threadIdx.x >> 6)], 0};
     const int diff = 15;  // kMinPixelDiffValue (feature_point_fast_detector.h:14)
 
     bool colv[4];
@@ -400,7 +465,6 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
             }
         }
     }
-    if constexpr (!RASTER) sink_flush(sk, a, f);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -470,18 +534,122 @@ __global__ __launch_bounds__(1024) void k_fast_mask_scan(const uint32_t *mask, i
 // feature per cell, so a Chebyshev-distance test needs the 3x3 neighbouring cells only.
 // ---------------------------------------------------------------------------------------------------
 constexpr int kLevels = 8;
-__device__ __forceinline__ int lvl_width(int l) { return l == 0 ? 11 : (l == 7 ? 5 : 8); }
-__device__ __forceinline__ int lvl_top(int l) { return l == 7 ? 64 : 11 + 8 * l; }  // bits consumed through l
+// digit widths per level: 12 (sign, exponent, 3 mantissa bits of the response), then 8 x 6, then 4
+__device__ __forceinline__ int lvl_width(int l) { return l == 0 ? 12 : (l == 7 ? 4 : 8); }
+__device__ __forceinline__ int lvl_top(int l) { return l == 7 ? 64 : 12 + 8 * l; }  // bits consumed through l
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint64_t sort_key(const Cand &c) {
-    return (static_cast<uint64_t>(float_key(c.resp)) << 32) | static_cast<uint64_t>(~c.idx);
+// Diagnostic phase clocks (only when a.stamps is set): slot 15 keeps the last clock; FD_STAMP(k)
+// adds the time since then to slot k.
+#define FD_STAMP(slot)                                                                  \
+    do {                                                                                \
+        if (a.stamps && threadIdx.x == 0) {                                             \
+            const uint64_t now_ = __builtin_readcyclecounter();                         \
+            uint64_t *st_ = a.stamps + blockIdx.x * 16;                                 \
+            if ((slot) > 0) st_[(slot)] += now_ - st_[15];                              \
+            st_[15] = now_;                                                             \
+        }                                                                               \
+    } while (0)
+
+__device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx) {
+    return (static_cast<uint64_t>(float_key(resp)) << 32) | static_cast<uint64_t>(~idx);
+}
+
+constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
+constexpr int kSubChunk = 512;  // keys sorted per greedy sub-chunk
+
+// One wave scans a sorted chunk in order (SelectGoodFeatures, feature_point_detector.cpp:62-72), a
+// batch of 64 candidates at a time: occupancy-grid test against earlier batches, then the batch is
+// resolved at once from cmask (per candidate: earlier candidates of its batch within distance d,
+// computed beforehand by the whole workgroup).
+// GRID: 0 = no distance test (d <= 0), 1 = occupancy grid in LDS, 2 = grid in global memory.
+template <int GRID>
+__device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
+                                             const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
+                                             uint32_t prior, int &s_acc, int &s_done) {
+    const int lane = lane_id();
+    const int d = a.dist;
+    int acc = s_acc;
+    bool done = false;
+    for (int b0 = 0; b0 < cnt && !done; b0 += kWave) {
+        const int i = b0 + lane;
+        const bool in = i < cnt;
+        const uint32_t e = in ? pxy[i] : kEmpty;
+        bool ok = e != kEmpty;
+        const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+        int cell = gw2 + 1;
+        uint64_t C = 0;
+        if constexpr (GRID != 0) {
+            cell = in ? static_cast<int>(pcell[i]) : gw2 + 1;
+            C = in ? cmask[i] : 0ull;
+            uint32_t g[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
+                if constexpr (GRID == 1) g[q] = grid[o];
+                else g[q] = __hip_atomic_load(&grid[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const int gx = static_cast<int>(g[q] & 0xFFFFu), gy = static_cast<int>(g[q] >> 16);
+                if (g[q] != kEmpty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
+            }
+        }
+        const uint64_t m = ballot(ok);
+        C &= m;
+        // Fixed point: a lane is decided once all of C is; accepted iff none of C was accepted.
+        uint64_t acc_m = 0, dec_m = ~m;
+        bool mine = !ok;
+        while (dec_m != ~0ull) {
+            const bool can = !mine && (C & ~dec_m) == 0;
+            const bool take = can && (C & acc_m) == 0;
+            dec_m |= ballot(can);
+            acc_m |= ballot(take);
+            mine = mine || can;
+        }
+        // need cutoff (:67-69): features.size() >= need is checked after every append
+        const uint32_t have = prior + static_cast<uint32_t>(acc);
+        const int allow = have < a.need ? static_cast<int>(a.need - have) : 1;
+        if (popc64(acc_m) >= allow) {
+            uint64_t keep = 0, t = acc_m;
+            for (int k = 0; k < allow; ++k) {
+                keep |= t & (~t + 1ull);
+                t &= t - 1ull;
+            }
+            acc_m = keep;
+            done = true;
+        }
+        if ((acc_m >> lane) & 1ull) {
+            const int pos = acc + popc64(acc_m & lanes_below());
+            if (pos < a.out_stride) {
+                float2 *o = reinterpret_cast<float2 *>(a.out_xy) + static_cast<int64_t>(f) * a.out_stride + pos;
+                *o = make_float2(static_cast<float>(x), static_cast<float>(y));
+            }
+            if constexpr (GRID != 0) {
+                const uint32_t ev = (static_cast<uint32_t>(y) << 16) | static_cast<uint32_t>(x);
+                if constexpr (GRID == 1) grid[cell] = ev;
+                else __hip_atomic_store(&grid[cell], ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        acc += popc64(acc_m);
+        if constexpr (GRID == 2) __builtin_amdgcn_s_waitcnt(0);
+    }
+    if (lane == 0) {
+        s_acc = acc;
+        if (done) s_done = 1;
+    }
 }
 
 __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
-    __shared__ uint32_t suf0[2049];
+    __shared__ uint32_t suf0[kHistBins + 1];
     __shared__ uint32_t sufl[kLevels - 1][257];
-    __shared__ uint64_t buf[kSelectChunk];
+    __shared__ __attribute__((aligned(16))) uint64_t sup[kSelectChunk];  // superchunk keys (unsorted)
+    // sub-chunk keys (merge-sorted between buf and tmp; buf later holds the conflict masks)
+    __shared__ __attribute__((aligned(16))) uint64_t buf[kSelectChunk];
+    __shared__ __attribute__((aligned(16))) uint64_t tmp[kSelectChunk];
+    // sorted chunk, decoded: (y << 16) | x (kEmpty when a prior masks it) and occupancy-grid cell
+    __shared__ __attribute__((aligned(16))) uint32_t pxy[kSelectChunk];
+    __shared__ uint32_t pcell[kSelectChunk];
     __shared__ uint32_t grid_lds[kGridLdsCells];
     __shared__ uint64_t prefix[kLevels];
     __shared__ int resume[kLevels];
@@ -489,64 +657,100 @@ __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
     __shared__ int s_done, s_acc;
 
     const int f = blockIdx.x;
-    const int tid = threadIdx.x, nthr = blockDim.x, lane = lane_id();
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = lane_id(), wave = tid >> 6;
     const int rows = a.rows, cols = a.cols;
     const int64_t n = min(static_cast<int64_t>(a.list_count[f]), a.list_cap);
-    const Cand *list = a.list + static_cast<int64_t>(f) * a.list_cap;
+    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
     const int d = a.dist;
     const bool use_grid = d >= 1;
-    const int cells = a.grid_w * a.grid_h;
+    // Occupancy grid of (d+1)-sized cells with a one-cell border (no bounds checks in the scan).
+    const int gw2 = a.grid_w + 2;
+    const int cells = gw2 * (a.grid_h + 2);
     const bool grid_in_lds = cells <= kGridLdsCells;
-    uint32_t *grid = grid_in_lds ? grid_lds : a.grid_global + static_cast<int64_t>(f) * cells;
+    uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
     const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
     const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
+    FD_STAMP(0);
 
-    if (use_grid)
-        for (int i = tid; i < cells; i += nthr) grid[i] = kEmpty;
+    if (use_grid) {
+        if (grid_in_lds)
+            for (int i = tid; i < cells; i += nthr) grid_lds[i] = kEmpty;
+        else
+            for (int i = tid; i < cells; i += nthr) grid_g[i] = kEmpty;
+    }
     if (tid == 0) {
         s_done = 0;
         s_acc = 0;
         prefix[0] = 0;
     }
-    __syncthreads();
     if (n == 0) {  // RETURN_TRUE_IF(candidates_.empty()) (:55)
         if (tid == 0) a.out_counts[f] = 0;
         return;
     }
 
-    // Histogram of digit `lvl` over keys in [klo, khi], then in-place suffix sums (wave 0).
+    // In-place suffix sums of S[0..nb) by the whole block; S[nb] = 0.
+    __shared__ uint32_t wtot[16];
+    auto suffix = [&](uint32_t *S, int nb) {
+        const int ch = (nb + nthr - 1) / nthr;  // contiguous bins per thread (<= 4)
+        const int b0 = min(tid * ch, nb), b1 = min(b0 + ch, nb);
+        uint32_t v[4] = {0, 0, 0, 0};
+        uint32_t sacc = 0;
+        for (int b = b0; b < b1; ++b) {
+            v[b - b0] = S[b];
+            sacc += v[b - b0];
+        }
+        // suffix over threads: wave-level, then across the 16 waves
+        uint32_t incl = sacc;
+        for (int o = 1; o < kWave; o <<= 1) {
+            const uint32_t t = __shfl_down(incl, o);
+            if (lane + o < kWave) incl += t;
+        }
+        if (lane == 0) wtot[wave] = incl;
+        __syncthreads();
+        uint32_t after = 0;
+        for (int q = wave + 1; q < nthr / kWave; ++q) after += wtot[q];
+        uint32_t run = incl - sacc + after;
+        for (int b = b1 - 1; b >= b0; --b) {
+            run += v[b - b0];
+            S[b] = run;
+        }
+        if (tid == 0) S[nb] = 0;
+        __syncthreads();
+    };
+    // Histogram of digit `lvl` (>= 1) over keys in [klo, khi] (one pass over the list).
     auto build = [&](int lvl, uint64_t klo, uint64_t khi, uint32_t *S) {
         const int nb = 1 << lvl_width(lvl);
         const int rem = 64 - lvl_top(lvl);
         for (int b = tid; b <= nb; b += nthr) S[b] = 0;
         __syncthreads();
-        for (int64_t i = tid; i < n; i += nthr) {
-            const uint64_t sk = sort_key(list[i]);
-            if (sk >= klo && sk <= khi) atomicAdd(&S[(sk >> rem) & static_cast<uint64_t>(nb - 1)], 1u);
+        for (int64_t b0 = tid; b0 < n; b0 += static_cast<int64_t>(kPassUnroll) * nthr) {
+            float r[kPassUnroll];
+            uint32_t ix[kPassUnroll];
+#pragma unroll
+            for (int u = 0; u < kPassUnroll; ++u) {
+                const int64_t i = min(b0 + static_cast<int64_t>(u) * nthr, n - 1);
+                r[u] = lresp[i];
+                ix[u] = lidx[i];
+            }
+#pragma unroll
+            for (int u = 0; u < kPassUnroll; ++u) {
+                const int64_t i = b0 + static_cast<int64_t>(u) * nthr;
+                const uint64_t sk = make_key(r[u], ix[u]);
+                if (i < n && sk >= klo && sk <= khi) atomicAdd(&S[(sk >> rem) & static_cast<uint64_t>(nb - 1)], 1u);
+            }
         }
         __syncthreads();
-        if (tid < kWave) {
-            const int ch = (nb + kWave - 1) / kWave;
-            const int b0 = min(lane * ch, nb), b1 = min(b0 + ch, nb);
-            uint32_t s = 0;
-            for (int b = b0; b < b1; ++b) s += S[b];
-            uint32_t incl = s;
-            for (int o = 1; o < kWave; o <<= 1) {
-                const uint32_t t = __shfl_down(incl, o);
-                if (lane + o < kWave) incl += t;
-            }
-            uint32_t run = incl - s;
-            for (int b = b1 - 1; b >= b0; --b) {
-                run += S[b];
-                S[b] = run;
-            }
-            if (lane == 0) S[nb] = 0;
-        }
-        __syncthreads();
+        suffix(S, nb);
     };
     auto suf = [&](int lvl) -> uint32_t * { return lvl == 0 ? suf0 : sufl[lvl - 1]; };
 
-    build(0, 0ull, ~0ull, suf0);
+    // Level-0 histogram: accumulated by the per-pixel kernel while it emitted the candidates.
+    for (int b = tid; b < kHistBins; b += nthr) suf0[b] = a.hist0[static_cast<int64_t>(f) * kHistBins + b];
+    __syncthreads();
+    FD_STAMP(1);
+    suffix(suf0, kHistBins);
+    FD_STAMP(2);
     int level = 0;
     int hi = (1 << lvl_width(0)) - 1;
     while (true) {
@@ -559,13 +763,14 @@ __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
         }
         const uint32_t *S = suf(level);
         const uint32_t base = S[hi + 1];
-        // smallest lo in [0, hi] with S[lo] - base <= chunk (S is non-increasing in b)
+        const uint32_t lim = static_cast<uint32_t>(kSelectChunk);
+        // smallest lo in [0, hi] with S[lo] - base <= lim (S is non-increasing in b)
         int lo_b = 0, hi_b = hi + 1;
         while (lo_b < hi_b) {
             const int mid = (lo_b + hi_b) >> 1;
-            if (S[mid] - base <= static_cast<uint32_t>(kSelectChunk)) hi_b = mid; else lo_b = mid + 1;
+            if (S[mid] - base <= lim) hi_b = mid; else lo_b = mid + 1;
         }
-        const int lo = lo_b;
+        int lo = lo_b;
         const int w = lvl_width(level);
         const int rem = 64 - lvl_top(level);
         const uint64_t pre = prefix[level];
@@ -577,106 +782,187 @@ __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
             }
             __syncthreads();
             const uint64_t klo = ((pre << w) | static_cast<uint64_t>(hi)) << rem;
-            const uint64_t khi = klo | ((rem == 64) ? ~0ull : ((1ull << rem) - 1ull));
+            const uint64_t khi = klo | ((1ull << rem) - 1ull);
             ++level;
+            if (a.stamps && tid == 0) a.stamps[blockIdx.x * 16 + 9] += 1;
+            FD_STAMP(7);
             build(level, klo, khi, suf(level));
+            FD_STAMP(6);  // descent pass
             hi = (1 << lvl_width(level)) - 1;
             continue;
         }
         const uint32_t cnt = S[lo] - base;
+        FD_STAMP(7);  // loop control
         if (cnt > 0) {
             const uint64_t klo = ((pre << w) | static_cast<uint64_t>(lo)) << rem;
             const uint64_t khi = (((pre << w) | static_cast<uint64_t>(hi)) << rem) | ((1ull << rem) - 1ull);
-            // gather
+            const uint32_t k32lo = static_cast<uint32_t>(klo >> 32), k32hi = static_cast<uint32_t>(khi >> 32);
+            // gather the chunk: wave-uniform loop bounds, one LDS atomic per wave per round
             if (tid == 0) gcount = 0;
             __syncthreads();
-            for (int64_t i = tid; i < n; i += nthr) {
-                const uint64_t sk = sort_key(list[i]);
-                if (sk >= klo && sk <= khi) buf[atomicAdd(&gcount, 1u)] = sk;
+            for (int64_t b0 = static_cast<int64_t>(wave) * kWave; b0 < n;
+                 b0 += static_cast<int64_t>(kPassUnroll) * nthr) {
+                float r[kPassUnroll];
+                uint32_t ix[kPassUnroll];
+#pragma unroll
+                for (int u = 0; u < kPassUnroll; ++u) {  // unconditional (clamped) loads: all in flight
+                    const int64_t i = min(b0 + static_cast<int64_t>(u) * nthr + lane, n - 1);
+                    r[u] = lresp[i];
+                    ix[u] = lidx[i];
+                }
+#pragma unroll
+                for (int u = 0; u < kPassUnroll; ++u) {
+                    const int64_t i = b0 + static_cast<int64_t>(u) * nthr + lane;
+                    const uint32_t k32 = float_key(r[u]);
+                    const bool near = i < n && k32 >= k32lo && k32 <= k32hi;  // cheap 32-bit prefilter
+                    if (ballot(near) == 0ull) continue;
+                    const uint64_t sk = make_key(r[u], ix[u]);
+                    const bool hit = near && sk >= klo && sk <= khi;
+                    const uint64_t m = ballot(hit);
+                    if (m) {
+                        uint32_t off = 0;
+                        if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
+                        off = __builtin_amdgcn_readfirstlane(off);
+                        if (hit) sup[off + popc64(m & lanes_below())] = sk;
+                    }
+                }
             }
             __syncthreads();
-            int np2 = 64;
-            while (np2 < static_cast<int>(cnt)) np2 <<= 1;
-            for (int i = static_cast<int>(cnt) + tid; i < np2; i += nthr) buf[i] = 0ull;
-            __syncthreads();
-            // bitonic sort, descending
-            for (int k = 2; k <= np2; k <<= 1) {
-                for (int j = k >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < np2; i += nthr) {
-                        const int ij = i ^ j;
-                        if (ij > i) {
-                            const uint64_t x = buf[i], y = buf[ij];
-                            const bool desc = (i & k) == 0;
-                            if (desc ? (x < y) : (x > y)) {
-                                buf[i] = y;
-                                buf[ij] = x;
-                            }
+            FD_STAMP(3);  // gather
+            const uint32_t s1 = static_cast<uint32_t>(d + 1);
+            auto place = [&](int pos, uint64_t sk) {  // decode position, prior mask, grid cell
+                const uint32_t idx = ~static_cast<uint32_t>(sk);
+                const uint32_t y = idx / static_cast<uint32_t>(cols);
+                const uint32_t x = idx - y * static_cast<uint32_t>(cols);
+                bool ok = true;
+                if (fmask) ok = (fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u;
+                pxy[pos] = ok ? ((y << 16) | x) : kEmpty;
+                if (use_grid) pcell[pos] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
+            };
+            // Sub-chunks of <= kSubChunk keys from the top bins of the superchunk (already in LDS):
+            // the greedy usually stops within the first few hundred keys.
+            int shi = hi;
+            while (shi >= lo && !s_done) {
+                const uint32_t sbase = S[shi + 1];
+                int q0 = lo, q1 = shi + 1;
+                while (q0 < q1) {
+                    const int mid = (q0 + q1) >> 1;
+                    if (S[mid] - sbase <= static_cast<uint32_t>(kSubChunk)) q1 = mid; else q0 = mid + 1;
+                }
+                const int slo = min(q0, shi);  // one bin larger than a sub-chunk is taken whole
+                const uint32_t sc = S[slo] - sbase;
+                if (sc > 0) {
+                    const uint64_t sklo = ((pre << w) | static_cast<uint64_t>(slo)) << rem;
+                    const uint64_t skhi = (((pre << w) | static_cast<uint64_t>(shi)) << rem) | ((1ull << rem) - 1ull);
+                    if (tid == 0) gcount = 0;
+                    __syncthreads();
+                    for (int b0 = wave * kWave; b0 < static_cast<int>(cnt); b0 += nthr) {
+                        const int i = b0 + lane;
+                        const uint64_t sk = i < static_cast<int>(cnt) ? sup[i] : 0ull;
+                        const bool hit = i < static_cast<int>(cnt) && sk >= sklo && sk <= skhi;
+                        const uint64_t m = ballot(hit);
+                        if (m) {
+                            uint32_t off = 0;
+                            if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
+                            off = __builtin_amdgcn_readfirstlane(off);
+                            if (hit) buf[off + popc64(m & lanes_below())] = sk;
                         }
                     }
                     __syncthreads();
-                }
-            }
-            // greedy scan by wave 0
-            if (tid < kWave) {
-                int acc = s_acc;
-                bool done = false;
-                for (int b0 = 0; b0 < static_cast<int>(cnt) && !done; b0 += kWave) {
-                    const int i = b0 + lane;
-                    const bool in = i < static_cast<int>(cnt);
-                    const uint64_t sk = in ? buf[i] : 0ull;
-                    const uint32_t idx = ~static_cast<uint32_t>(sk);
-                    const int y = in ? static_cast<int>(idx / static_cast<uint32_t>(cols)) : 0;
-                    const int x = in ? static_cast<int>(idx - static_cast<uint32_t>(y) * cols) : 0;
-                    bool ok = in;
-                    if (ok && fmask) ok = (fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u;
-                    if (ok && use_grid) {
-                        const int cx = x / (d + 1), cy = y / (d + 1);
-                        for (int gy = max(cy - 1, 0); gy <= min(cy + 1, a.grid_h - 1) && ok; ++gy)
-                            for (int gx = max(cx - 1, 0); gx <= min(cx + 1, a.grid_w - 1); ++gx) {
-                                const uint32_t e = grid_in_lds ? grid[gy * a.grid_w + gx]
-                                                               : __hip_atomic_load(&grid[gy * a.grid_w + gx],
-                                                                                   __ATOMIC_RELAXED,
-                                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                                if (e != kEmpty) {
-                                    const int ex = static_cast<int>(e & 0xFFFFu), ey = static_cast<int>(e >> 16);
-                                    if (abs(x - ex) <= d && abs(y - ey) <= d) { ok = false; break; }
-                                }
-                            }
-                    }
-                    uint64_t m = ballot(ok);
-                    while (m) {
-                        const int first = __ffsll(static_cast<unsigned long long>(m)) - 1;
-                        const int fx = __shfl(x, first), fy = __shfl(y, first);
-                        if (lane == 0) {
-                            if (acc < a.out_stride) {
-                                float *o = a.out_xy + (static_cast<int64_t>(f) * a.out_stride + acc) * 2;
-                                o[0] = static_cast<float>(fx);
-                                o[1] = static_cast<float>(fy);
-                            }
-                            if (use_grid) {
-                                const int gi = (fy / (d + 1)) * a.grid_w + fx / (d + 1);
-                                const uint32_t e = (static_cast<uint32_t>(fy) << 16) | static_cast<uint32_t>(fx);
-                                if (grid_in_lds) grid[gi] = e;
-                                else __hip_atomic_store(&grid[gi], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            }
+                    FD_STAMP(10);  // sub-chunk extract
+                {
+                    // Merge sort of unique keys, descending: rank inside runs of 64 by counting larger
+                    // keys (broadcast LDS reads), then log2 merge levels where each key moves to
+                    // (its offset in its run) + (number of larger keys in the sibling run, by binary search).
+                    const int c = static_cast<int>(sc);
+                    const int c64 = (c + 63) & ~63;
+                    for (int i = c + tid; i < c64; i += nthr) buf[i] = 0ull;
+                    __syncthreads();
+                    for (int p = tid; p < c; p += nthr) {
+                        const uint64_t me = buf[p];
+                        const ulonglong2 *b2 = reinterpret_cast<const ulonglong2 *>(buf + (p & ~63));
+                        int lr = 0;
+    #pragma unroll 8
+                        for (int j = 0; j < 32; ++j) {
+                            const ulonglong2 q = b2[j];
+                            lr += (q.x > me) + (q.y > me);
                         }
-                        ++acc;
-                        if (prior + static_cast<uint32_t>(acc) >= a.need) { done = true; break; }  // :67-69
-                        if (lane > first && ok && abs(x - fx) <= d && abs(y - fy) <= d) ok = false;
-                        m = ballot(ok) & ~((first == 63) ? ~0ull : ((2ull << first) - 1ull));
+                        tmp[(p & ~63) + lr] = me;
                     }
-                    if (!grid_in_lds && use_grid) __builtin_amdgcn_s_waitcnt(0);
+                    __syncthreads();
+                    FD_STAMP(11);  // run sort
+                    uint64_t *src = tmp, *dst = buf;
+                    for (int w = 64; w < c; w <<= 1) {
+                        for (int p = tid; p < c; p += nthr) {
+                            const uint64_t me = src[p];
+                            const int run = p / w;
+                            const int pair = (run & ~1) * w;
+                            const int sib = (run ^ 1) * w;
+                            int lo2 = 0, hi2 = max(0, min(w, c - sib));  // larger keys in the sibling run
+                            while (lo2 < hi2) {
+                                const int mid = (lo2 + hi2) >> 1;
+                                if (src[sib + mid] > me) lo2 = mid + 1; else hi2 = mid;
+                            }
+                            dst[pair + (p - run * w) + lo2] = me;
+                        }
+                        __syncthreads();
+                        uint64_t *t2 = src;
+                        src = dst;
+                        dst = t2;
+                    }
+                    FD_STAMP(12);  // merges
+                    for (int i = tid; i < c; i += nthr) place(i, src[i]);
+                    __syncthreads();
+                    FD_STAMP(13);  // place
+                    // conflict masks: earlier candidates of the same 64-batch within distance d
+                    if (use_grid) {
+                        for (int p = tid; p < c; p += nthr) {
+                            const uint32_t e = pxy[p];
+                            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+                            uint64_t C = 0;
+                            const int bb = p & ~63, me = p - bb;
+                            const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb);  // broadcast reads
+                            const int n4 = (me + 3) >> 2;  // only earlier entries matter
+#pragma unroll 2
+                            for (int j4 = 0; j4 < n4; ++j4) {
+                                const uint4 e4 = q4[j4];
+                                const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
+                                uint32_t bits = 0;
+#pragma unroll
+                                for (int t = 0; t < 4; ++t) {
+                                    const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
+                                    const bool nb = j4 * 4 + t < me && ev[t] != kEmpty && abs(x - ex) <= d && abs(y - ey) <= d;
+                                    bits |= static_cast<uint32_t>(nb) << t;
+                                }
+                                C |= static_cast<uint64_t>(bits) << (j4 * 4);
+                            }
+                            buf[p] = e == kEmpty ? 0ull : C;
+                        }
+                    }
                 }
-                if (lane == 0) {
-                    s_acc = acc;
-                    if (done) s_done = 1;
+                __syncthreads();
+                FD_STAMP(14);  // conflict masks
+                // greedy scan in order by wave 0 (SelectGoodFeatures :62-72)
+                if (tid < kWave) {
+                    const int c = static_cast<int>(sc);
+                    if (!use_grid)
+                        greedy_chunk<0>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done);
+                    else if (grid_in_lds)
+                        greedy_chunk<1>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done);
+                    else
+                        greedy_chunk<2>(a, f, c, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done);
                 }
+                __syncthreads();
+                FD_STAMP(5);  // greedy
+                }
+                shi = slo - 1;
             }
-            __syncthreads();
+            if (a.stamps && tid == 0) a.stamps[blockIdx.x * 16 + 8] += 1;
         }
         hi = lo - 1;
     }
     if (tid == 0) a.out_counts[f] = s_acc;
+    FD_STAMP(7);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -732,8 +1018,7 @@ __global__ __launch_bounds__(1024) void k_compact(CompactArgs a) {
 // Launchers
 // ---------------------------------------------------------------------------------------------------
 static inline int blocks_for_waves(const PointsArgs &a) {
-    const int64_t waves = static_cast<int64_t>(a.batch) * a.tiles_y * a.tiles_x;
-    return static_cast<int>((waves + 3) / 4);
+    return a.batch * a.blocks_per_frame;
 }
 
 hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s) {

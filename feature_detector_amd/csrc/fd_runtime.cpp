@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -30,9 +32,10 @@ struct fd_ctx {
     std::string err;
     // workspace
     DevBuf frames, prior_xy, prior_frame, prior_counts, mask, row_base, word_pref;
-    DevBuf list, list_count, out_xy, out_counts, grid;
+    DevBuf list_resp, list_idx, list_count, hist0, out_xy, out_counts, grid;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts;
+    DevBuf dbg;
     // FAST offset table cache
     int64_t off_n = -1;
     float off_thr = 0.0f;
@@ -212,6 +215,7 @@ struct PointGeom {
     int border;    // 2 for Harris/Shi-Tomasi, 3 for FAST
     int out_rows;  // rows of the candidate region
     int tiles_x, tiles_y, tile_h;
+    int blocks_per_frame;
     bool empty;
 };
 
@@ -225,6 +229,7 @@ PointGeom point_geom(int kind, int batch, int rows, int cols) {
     const int period = kind == FD_FAST ? 7 : 3;
     g.tile_h = choose_tile_h(batch, g.tiles_x, std::max(g.out_rows, 1), period, kind == FD_FAST ? 9 : 20);
     g.tiles_y = std::max(1, (std::max(g.out_rows, 1) + g.tile_h - 1) / g.tile_h);
+    g.blocks_per_frame = (g.tiles_x * g.tiles_y + 3) / 4;
     return g;
 }
 
@@ -264,8 +269,9 @@ void fd_ctx_destroy(fd_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf *bufs[] = {&c->frames,   &c->prior_xy, &c->prior_frame, &c->prior_counts, &c->mask,    &c->row_base,
-                      &c->word_pref, &c->list,    &c->list_count,  &c->out_xy,       &c->out_counts, &c->grid,
+    DevBuf *bufs[] = {&c->frames,    &c->prior_xy,  &c->prior_frame, &c->prior_counts, &c->mask,       &c->row_base,
+                      &c->word_pref, &c->list_resp, &c->list_idx,  &c->list_count,   &c->hist0,      &c->out_xy,
+                      &c->out_counts, &c->grid,     &c->dbg,
                       &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
                       &c->l_idx,    &c->l_counts};
@@ -302,8 +308,10 @@ int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t m
     if (rc) return rc;
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const int64_t cap = detect_list_cap(kind, rows, cols);
-    FD_HIP_TRY(c, ensure(c->list, sizeof(fdk::Cand) * cap * batch));
+    FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
+    FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
     FD_HIP_TRY(c, ensure(c->list_count, sizeof(uint32_t) * batch));
+    FD_HIP_TRY(c, ensure(c->hist0, sizeof(uint32_t) * fdk::kHistBins * batch));
     FD_HIP_TRY(c, ensure(c->prior_counts, sizeof(int32_t) * batch));
     if (max_prior_total > 0) {
         FD_HIP_TRY(c, ensure(c->prior_xy, sizeof(float) * 2 * max_prior_total));
@@ -333,9 +341,12 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
 
     const PointGeom g = point_geom(kind, batch, rows, cols);
     const int64_t cap = detect_list_cap(kind, rows, cols);
-    FD_HIP_TRY(c, ensure(c->list, sizeof(fdk::Cand) * cap * batch));
+    FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
+    FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
     FD_HIP_TRY(c, ensure(c->list_count, sizeof(uint32_t) * batch));
+    FD_HIP_TRY(c, ensure(c->hist0, sizeof(uint32_t) * fdk::kHistBins * batch));
     FD_HIP_TRY(c, hipMemsetAsync(c->list_count.p, 0, sizeof(uint32_t) * batch, c->stream));
+    FD_HIP_TRY(c, hipMemsetAsync(c->hist0.p, 0, sizeof(uint32_t) * fdk::kHistBins * batch, c->stream));
 
     fdk::PointsArgs a{};
     a.frames = dframes;
@@ -347,11 +358,14 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     a.tile_h = g.tile_h;
     a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
     a.thr = opts->min_valid_response;
+    a.blocks_per_frame = g.blocks_per_frame;
     a.mask = pi.mask;
     a.mask_wpr = pi.wpr;
-    a.list = as<fdk::Cand>(c->list);
+    a.list_resp = as<float>(c->list_resp);
+    a.list_idx = as<uint32_t>(c->list_idx);
     a.list_cap = cap;
     a.list_count = as<uint32_t>(c->list_count);
+    a.hist0 = as<uint32_t>(c->hist0);
     if (!g.empty) {
         if (kind == FD_FAST) {
             rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
@@ -372,8 +386,10 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     }
 
     fdk::SelectArgs s{};
-    s.list = a.list;
+    s.list_resp = a.list_resp;
+    s.list_idx = a.list_idx;
     s.list_count = a.list_count;
+    s.hist0 = a.hist0;
     s.list_cap = cap;
     s.rows = rows;
     s.cols = cols;
@@ -385,7 +401,7 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     if (s.dist >= 1) {
         s.grid_w = (cols + s.dist) / (s.dist + 1);
         s.grid_h = (rows + s.dist) / (s.dist + 1);
-        const int64_t cells = static_cast<int64_t>(s.grid_w) * s.grid_h;
+        const int64_t cells = static_cast<int64_t>(s.grid_w + 2) * (s.grid_h + 2);  // bordered grid
         if (cells > fdk::kGridLdsCells) {
             FD_HIP_TRY(c, ensure(c->grid, sizeof(uint32_t) * cells * batch));
             s.grid_global = as<uint32_t>(c->grid);
@@ -402,7 +418,25 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     s.out_xy = dxy;
     s.out_stride = out_stride;
     s.out_counts = dcnt;
+    static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
+    if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
+        FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 16 * batch));
+        FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 16 * batch, c->stream));
+        s.stamps = as<uint64_t>(c->dbg);
+    }
     FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
+    if (stamps) {
+        uint64_t h[16];
+        FD_HIP_TRY(c, hipMemcpyAsync(h, c->dbg.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        std::fprintf(stderr, "k_select cycles: init %llu hist0 %llu gather %llu sort %llu greedy %llu descent %llu "
+                             "control %llu | chunks %llu descents %llu | extract %llu runsort %llu merges %llu place %llu cmask %llu\n",
+                     (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
+                     (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
+                     (unsigned long long)h[7], (unsigned long long)h[8], (unsigned long long)h[9],
+                     (unsigned long long)h[10], (unsigned long long)h[11], (unsigned long long)h[12],
+                     (unsigned long long)h[13], (unsigned long long)h[14]);
+    }
     if (!outputs_on_device) {
         FD_HIP_TRY(c, hipMemcpyAsync(out_xy, dxy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
                                      hipMemcpyDeviceToHost, c->stream));
@@ -417,10 +451,11 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
 }
 
 int fd_points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,
-                       const fd_point_opts *opts, void *out_cands, int64_t cand_cap, uint32_t *out_counts) {
+                       const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
+                       uint32_t *out_counts) {
     int rc = check_shape(c, kind, batch, rows, cols);
     if (rc) return rc;
-    if (!opts || !frames || !out_cands || !out_counts || cand_cap < 1)
+    if (!opts || !frames || !out_resp || !out_idx || !out_counts || cand_cap < 1)
         return fail(c, FD_ERR_INVALID, "bad arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const PointGeom g = point_geom(kind, batch, rows, cols);
@@ -434,9 +469,11 @@ int fd_points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, in
     a.tiles_x = g.tiles_x;
     a.tiles_y = g.tiles_y;
     a.tile_h = g.tile_h;
+    a.blocks_per_frame = g.blocks_per_frame;
     a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(frames) % 4 == 0);
     a.thr = opts->min_valid_response;
-    a.list = static_cast<fdk::Cand *>(out_cands);
+    a.list_resp = out_resp;
+    a.list_idx = out_idx;
     a.list_cap = cand_cap;
     a.list_count = out_counts;
     if (kind == FD_FAST) {
@@ -506,6 +543,7 @@ int fd_points_candidates(fd_ctx *c, int kind, const uint8_t *frames, int frames_
         a.tiles_x = g.tiles_x;
         a.tiles_y = g.tiles_y;
         a.tile_h = g.tile_h;
+        a.blocks_per_frame = g.blocks_per_frame;
         a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
         a.thr = opts->min_valid_response;
         a.mask = pi.mask;

@@ -172,8 +172,8 @@ def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_v
 def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx: Context | None = None):
     """The per-pixel stage alone (fd_points_response) on torch device frames [B, R, C].
 
-    Returns (cands, counts): cands int64 [B, cap] holding (float response, uint32 raster index)
-    pairs in unspecified order, counts int32 [B]. Asynchronous on torch's current stream.
+    Returns (resp, idx, counts): resp float32 [B, cap], idx int32 [B, cap] (raster index), in
+    unspecified order, counts int32 [B]. Asynchronous on torch's current stream.
     """
     import torch
 
@@ -185,18 +185,19 @@ def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx:
     _bind_stream(ctx, True)
     cap = r * c if kind == FD_FAST else r * c // 2 + 64
     if out is None:
-        cands = torch.empty((b, cap), dtype=torch.int64, device=frames.device)
+        resp = torch.empty((b, cap), dtype=torch.float32, device=frames.device)
+        idx = torch.empty((b, cap), dtype=torch.int32, device=frames.device)
         counts = torch.empty((b,), dtype=torch.int32, device=frames.device)
     else:
-        cands, counts = out
-        cap = cands.shape[1]
+        resp, idx, counts = out
+        cap = resp.shape[1]
     opts = fd_point_opts(15, float(min_valid_response))
     rc = _lib.load().fd_points_response(ctx.ptr, kind, ctypes.c_void_p(ptr), b, r, c, ctypes.byref(opts),
-                                        ctypes.c_void_p(cands.data_ptr()), int(cap),
+                                        ctypes.c_void_p(resp.data_ptr()), ctypes.c_void_p(idx.data_ptr()), int(cap),
                                         ctypes.c_void_p(counts.data_ptr()))
     _lib.check(ctx.ptr, rc)
     del keep
-    return cands, counts
+    return resp, idx, counts
 
 
 def point_candidates(kind, frames, min_feature_distance: int = 15, min_valid_response: float = 0.1, prior=None,

@@ -99,13 +99,14 @@ int fd_points_candidates(fd_ctx *ctx, int kind, const uint8_t *frames, int frame
 
 /*
  * fd_points_response -- the per-pixel stage alone (response + NMS for Harris/Shi-Tomasi, segment test
- * + offset for FAST), i.e. ComputeCandidates without ordering: per frame, the candidates as
- * (response float, raster index uint32) pairs in unspecified order at out_cands[b * cand_cap], and
- * their count in out_counts[b] (uint32). Device pointers only (frames and outputs). Used to time the
- * hot kernel alone and by callers that select features themselves.
+ * + offset for FAST), i.e. ComputeCandidates without ordering: per frame, the candidates' responses
+ * at out_resp[b * cand_cap] and raster indices (row * cols + col) at out_idx[b * cand_cap], in
+ * unspecified order, and their count in out_counts[b]. Device pointers only (frames and outputs).
+ * Used to time the hot kernel alone and by callers that select features themselves.
  */
 int fd_points_response(fd_ctx *ctx, int kind, const uint8_t *frames, int batch, int rows, int cols,
-                       const fd_point_opts *opts, void *out_cands, int64_t cand_cap, uint32_t *out_counts);
+                       const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
+                       uint32_t *out_counts);
 
 /* ---- LSD level-line map ------------------------------------------------------------------------ */
 /*
