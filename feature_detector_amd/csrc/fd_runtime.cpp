@@ -303,6 +303,16 @@ int fd_ctx_synchronize(fd_ctx *c) {
     return FD_OK;
 }
 
+int fd_ctx_stage(fd_ctx *c, const void *host, int64_t bytes, const uint8_t **device_out) {
+    if (!c || !host || bytes < 0 || !device_out) return fail(c, FD_ERR_INVALID, "bad arguments");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    FD_HIP_TRY(c, ensure(c->frames, static_cast<size_t>(bytes)));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->frames.p, host, static_cast<size_t>(bytes), hipMemcpyHostToDevice, c->stream));
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *device_out = as<uint8_t>(c->frames);
+    return FD_OK;
+}
+
 int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t max_prior_total) {
     int rc = check_shape(c, kind, batch, rows, cols);
     if (rc) return rc;

@@ -61,6 +61,10 @@ int fd_ctx_synchronize(fd_ctx *ctx);
 /* Pre-size device workspace for a (kind, batch, rows, cols) shape so that later calls of that shape
  * allocate nothing (required before hipGraph capture of fd_points_detect). */
 int fd_ctx_reserve(fd_ctx *ctx, int kind, int batch, int rows, int cols, int64_t max_prior_total);
+/* Copy `bytes` of host memory into the context's frame staging buffer; *device_out receives its device
+ * address, valid until the next call that stages frames on this context. Lets a caller run several
+ * entry points on one upload (frames_on_device = 1). Synchronous. */
+int fd_ctx_stage(fd_ctx *ctx, const void *host, int64_t bytes, const uint8_t **device_out);
 
 /* ---- corner / FAST points ----------------------------------------------------------------------- */
 /*

@@ -1,0 +1,146 @@
+// FeatureLineDetector (LSD): the reference's public API (src/feature_line_detector/
+// feature_line_detector.h:11-79). The level-line map (gradient norm, angle, validity, scan-ordered
+// valid list) is computed on the GPU by libfdhip.so; region growing and rectangle fitting run on the
+// host in the reference's order.
+#ifndef FEATURE_DETECTOR_FEATURE_LINE_DETECTOR_H_
+#define FEATURE_DETECTOR_FEATURE_LINE_DETECTOR_H_
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "fd_types.h"
+
+struct fd_ctx;
+
+namespace feature_detector {
+
+// Fixed-capacity FIFO standing in for Slam_Utility's CircularBuffer<T, N> (feature_line_detector.h:76-77).
+// Overflow policy (unpinned: the reference's implementation is not vendored): PushBack on a full buffer
+// overwrites the oldest element.
+template <typename T, int N>
+class LineRingBuffer {
+public:
+    void Clear() { head_ = size_ = 0; }
+    bool Empty() const { return size_ == 0; }
+    void PushBack(const T &v) {
+        if (size_ == N) {
+            buf_[head_] = v;
+            head_ = (head_ + 1) % N;
+            return;
+        }
+        buf_[(head_ + size_) % N] = v;
+        ++size_;
+    }
+    const T &Front() const { return buf_[head_]; }
+    void PopFront() {
+        head_ = (head_ + 1) % N;
+        --size_;
+    }
+
+private:
+    T buf_[N];
+    int head_ = 0, size_ = 0;
+};
+
+class FeatureLineDetector {
+public:
+    struct PixelParam {
+        int32_t row = 0;
+        int32_t col = 0;
+        float line_level_angle = 0.0f;
+        float gradient_norm = 0.0f;
+        bool is_valid = false;     // Valid when gradient norm is large enough.
+        bool is_used = false;      // Has been used in a region.
+        bool is_occupied = false;  // Has been searched when region is growing. It will be cleared later.
+    };
+
+    struct RegionParam {
+        std::vector<PixelParam *> pixels;
+        float angle = 0.0f;
+    };
+
+    struct RectangleParam {
+        Vec2 start_point = Vec2::Zero();
+        Vec2 end_point = Vec2::Zero();
+        Vec2 center_point = Vec2::Zero();
+        float length = 0.0f;
+        float width = 0.0f;
+        float angle = 0.0f;
+        Vec2 dir_vector = Vec2::Identity();
+        float inlier_ratio = 0.0f;
+    };
+
+    struct Options {
+        float kMinValidGradientNorm = 20.0f;
+        float kMinToleranceAngleResidualInRad = 22.5f * kDegToRad;
+        float kMinValidLineLengthInPixel = 20.0f;
+        float kMaxToleranceInlierRation = 0.6f;
+    };
+
+    // Column-major (rows x cols) matrix of PixelParam, as the reference's
+    // Eigen::Matrix<PixelParam, Dynamic, Dynamic> (feature_line_detector.h:74).
+    class PixelMatrix {
+    public:
+        void resize(int rows, int cols) {
+            if (rows != rows_ || cols != cols_) {  // Eigen keeps the data on a same-size resize
+                rows_ = rows;
+                cols_ = cols;
+                buf_.assign(static_cast<size_t>(rows) * static_cast<size_t>(cols), PixelParam());
+            }
+        }
+        PixelParam &operator()(int r, int c) { return buf_[static_cast<size_t>(c) * rows_ + r]; }
+        const PixelParam &operator()(int r, int c) const { return buf_[static_cast<size_t>(c) * rows_ + r]; }
+        int rows() const { return rows_; }
+        int cols() const { return cols_; }
+
+    private:
+        int rows_ = 0, cols_ = 0;
+        std::vector<PixelParam> buf_;
+    };
+
+public:
+    FeatureLineDetector();
+    virtual ~FeatureLineDetector();
+
+    bool DetectGoodFeatures(const GrayImage &image, const uint32_t needed_feature_num, std::vector<Vec4> &features);
+
+    // Reference for member variables.
+    Options &options() { return options_; }
+    PixelMatrix &pixels() { return pixels_; }
+    std::vector<PixelParam *> &sorted_pixels() { return sorted_pixels_; }
+    std::vector<RectangleParam> &rectangles() { return rectangles_; }
+
+    // Const reference for member variables.
+    const Options &options() const { return options_; }
+    const PixelMatrix &pixels() const { return pixels_; }
+    const std::vector<PixelParam *> &sorted_pixels() const { return sorted_pixels_; }
+    const std::vector<RectangleParam> &rectangles() const { return rectangles_; }
+
+    // MI355X extensions.
+    void set_device(int device);
+    const std::string &last_error() const { return error_; }
+
+private:
+    bool ComputeLineLevelAngleMap(const GrayImage &image);
+    void GrowRegion(PixelParam &seed_pixel, RegionParam &region);
+    void TryToAddPixelIntoCandidates(PixelParam &neighbour);
+    RectangleParam ConvertRegionToRectangle(const RegionParam &region);
+
+private:
+    Options options_;
+
+    PixelMatrix pixels_;
+    std::vector<PixelParam *> sorted_pixels_;
+    LineRingBuffer<PixelParam *, 1000> candidates_;
+    LineRingBuffer<PixelParam *, 1000> visited_pixels_;
+    std::vector<RectangleParam> rectangles_;
+
+    fd_ctx *ctx_ = nullptr;
+    int device_ = -1;
+    std::string error_;
+};
+
+}  // namespace feature_detector
+
+#endif  // FEATURE_DETECTOR_FEATURE_LINE_DETECTOR_H_

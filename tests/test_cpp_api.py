@@ -1,0 +1,95 @@
+"""The C++ drop-in API (include/feature_detector/*, libfeature_detector.so) driven by headless
+restatements of the reference demos (tests/cpp/*.cpp mirror test/test_feature_point_detector.cpp and
+test/test_feature_line_detector.cpp). GPU tests compare with the oracle / the reference's counts."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "feature_detector_amd", "lib")
+KIND = {"harris": 0, "shi_tomasi": 1, "fast": 2, "harris_prior": 0}
+THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0, "harris_prior": 30.0}
+
+
+def _build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "feature_detector_amd", "api")])
+
+
+def _run(prog, img, tmp_path, *extra):
+    raw = tmp_path / "frame.u8"
+    np.ascontiguousarray(img, np.uint8).tofile(raw)
+    out = subprocess.run([os.path.join(LIB, prog), str(raw), str(img.shape[0]), str(img.shape[1]), *map(str, extra)],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    return [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+
+
+def test_api_builds_and_links():
+    _build()
+    for f in ("libfeature_detector.so", "fd_demo_points", "fd_demo_lines"):
+        assert os.path.exists(os.path.join(LIB, f))
+    nm = subprocess.run(["nm", "-DC", os.path.join(LIB, "libfeature_detector.so")], capture_output=True, text=True).stdout
+    for sym in ("feature_detector::FeaturePointDetector::DetectGoodFeatures",
+                "feature_detector::FeaturePointDetector::SparsifyFeatures",
+                "feature_detector::FeatureLineDetector::DetectGoodFeatures"):
+        assert sym in nm
+
+
+def test_without_gpu_calls_fail_loudly(tmp_path, image_png):
+    """No CPU fallback: without a visible GPU every detector call returns false."""
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is visible")
+    except ImportError:
+        pass
+    _build()
+    res = _run("fd_demo_points", image_png, tmp_path)
+    assert all(r["ok"] is False for r in res)
+
+
+@pytest.mark.gpu
+def test_point_demo_matches_oracle(tmp_path, image_png, oracle, ref_counts):
+    _build()
+    res = {r["test"]: r for r in _run("fd_demo_points", image_png, tmp_path)}
+    assert res["null_image"]["ok"] is False
+    prior = np.array([(i * 15, j * 15) for i in range(1, 10) for j in range(1, 10)], np.float32)
+    for name in ("fast", "harris", "shi_tomasi", "harris_prior"):
+        r = res[name]
+        assert r["ok"] is True
+        feats, cands = oracle.detect(KIND[name], image_png, 20, THR[name], 200,
+                                     prior if name == "harris_prior" else None, sort_mode=0)
+        assert np.array_equal(np.array(r["features"], np.float32).reshape(-1, 2), feats), name
+        assert r["n_candidates"] == len(cands[0])
+        if name in ref_counts["image_png"]:
+            assert r["n_candidates"] == ref_counts["image_png"][name]["candidates"]
+            assert len(r["features"]) == ref_counts["image_png"][name]["features"]
+        # candidates() holds the reference's std::sort order (oracle sort_mode 0)
+        top = np.array(r["top_candidates"], np.float64)
+        n = len(top)
+        assert np.array_equal(top[:, 0].astype(np.float32), cands[0][:n])
+        assert np.array_equal(top[:, 1].astype(np.int32), cands[1][:n])
+        assert np.array_equal(top[:, 2].astype(np.int32), cands[2][:n])
+
+
+@pytest.mark.gpu
+def test_line_demo_reference_counts(tmp_path, image_png, oracle, ref_counts):
+    _build()
+    (r,) = _run("fd_demo_lines", image_png, tmp_path)
+    assert r["ok"] is True
+    assert r["n_valid"] == ref_counts["image_png"]["lsd_valid"] == r["n_sorted"]
+    assert len(r["lines"]) == ref_counts["image_png"]["lsd_lines"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rec_i", [0, 1])
+def test_line_demo_synthetic_counts(tmp_path, oracle, ref_counts, rec_i):
+    rec = ref_counts["synthetic_lsd_lines"][rec_i]
+    img = oracle.make_frame(rec["pattern"], 1234, rec["rows"], rec["cols"], rec["period"])
+    _build()
+    (r,) = _run("fd_demo_lines", img, tmp_path)
+    assert len(r["lines"]) == rec["lines"]
