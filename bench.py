@@ -66,18 +66,25 @@ def make_frames(torch, pattern, n, rows, cols, seed, device):
     return (base + noise).clamp(0, 255).to(torch.uint8)
 
 
-def timed_graph(torch, fn, steps, warmup, use_graph, per_graph):
+def timed_graph(torch, fn, steps, warmup, use_graph, per_graph, barrier=None):
     """Run fn(i) (i = step index) `warmup` then `steps` times; returns seconds for the timed steps.
 
-    With graphs, `per_graph` consecutive steps are captured into one hipGraph and replayed."""
+    With graphs, `per_graph` consecutive steps are captured into one hipGraph and replayed. The timed
+    region is bracketed by barrier() (all ranks) + device synchronisation on both sides."""
+    def fence():
+        torch.cuda.synchronize()
+        if barrier is not None:
+            barrier()
+        torch.cuda.synchronize()
+
     if not use_graph:
         for i in range(warmup):
             fn(i)
-        torch.cuda.synchronize()
+        fence()
         t0 = time.perf_counter()
         for i in range(steps):
             fn(i)
-        torch.cuda.synchronize()
+        fence()
         return time.perf_counter() - t0, steps
     for i in range(max(warmup, 1)):  # eager warmup also sizes the library workspace
         fn(i)
@@ -87,12 +94,12 @@ def timed_graph(torch, fn, steps, warmup, use_graph, per_graph):
         for i in range(per_graph):
             fn(i)
     g.replay()
-    torch.cuda.synchronize()
     reps = max(1, (steps + per_graph - 1) // per_graph)
+    fence()
     t0 = time.perf_counter()
     for _ in range(reps):
         g.replay()
-    torch.cuda.synchronize()
+    fence()
     return time.perf_counter() - t0, reps * per_graph
 
 
@@ -117,7 +124,7 @@ def kernel_time_ms(torch, fd, frames_pool, kind, thr, reps=50):
 
 
 def run_config(torch, fd, dev, detector, rows, cols, batch, pool, need, dist, pattern, steps, warmup, use_graph,
-               seed):
+               seed, barrier=None):
     frames_pool = [make_frames(torch, pattern, batch, rows, cols, seed + 7919 * i, dev) for i in range(pool)]
     thr = THR[detector]
     stride = max(need, 1) + 1
@@ -129,7 +136,7 @@ def run_config(torch, fd, dev, detector, rows, cols, batch, pool, need, dist, pa
     def step(i):
         fd.detect_points(detector, frames_pool[i % pool], need, dist, thr, out=(xy, cnt), ctx=ctx)
 
-    secs, done = timed_graph(torch, step, steps, warmup, use_graph, per_graph=pool)
+    secs, done = timed_graph(torch, step, steps, warmup, use_graph, per_graph=pool, barrier=barrier)
     return secs, done, frames_pool, (xy, cnt)
 
 
@@ -141,28 +148,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Control-plane collectives only (barrier, timing max): RCCL by default; FD_BENCH_BACKEND=gloo
+    # rehearses N>1 on fewer GPUs (ranks then share devices round-robin).
+    backend = os.environ.get("FD_BENCH_BACKEND", "nccl")
+    dev_index = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        dist.init_process_group(backend)
     import feature_detector_amd as fd
+    from feature_detector_amd.shard import max_over_ranks
 
     fd.load()
 
     # ---- headline workload (per rank: its own frames; weak scaling) -------------------------------
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    barrier = dist.barrier if world > 1 else None
     secs, done, pool, _ = run_config(torch, fd, dev, args.detector, args.rows, args.cols, args.batch, args.pool,
                                      args.need, args.dist, args.pattern, args.steps, args.warmup,
-                                     not args.no_graph, seed=1234 + 1000003 * rank)
-    torch.cuda.synchronize()
-    t = torch.tensor([secs], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.barrier()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    secs_max = float(t.item())
+                                     not args.no_graph, seed=1234 + 1000003 * rank, barrier=barrier)
+    secs_max = max_over_ranks(secs, dist if world > 1 else None, dev if backend == "nccl" else None)
     px_step = args.batch * args.rows * args.cols
     value = world * done * px_step / secs_max / 1e6  # Mpix/s, all ranks
     ms_per_step = secs_max / done * 1e3
