@@ -10,13 +10,14 @@ constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// Lane i receives lane i-1's value (lane 0 receives 0): DPP wave_shr:1.
+// Lane i receives lane i-1's value (lane 0 receives 0): DPP wave_shr:1 with bound_ctrl, so the
+// invalid source lane reads 0 and no zeroed destination has to be prepared.
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xF, 0xF, false));
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x138, 0xF, 0xF, true));
 }
 // Lane i receives lane i+1's value (lane 63 receives 0): DPP wave_shl:1.
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x130, 0xF, 0xF, false));
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0x130, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float from_left_f(float v) { return __uint_as_float(from_left(__float_as_uint(v))); }
 __device__ __forceinline__ float from_right_f(float v) { return __uint_as_float(from_right(__float_as_uint(v))); }
@@ -40,11 +41,33 @@ __device__ __forceinline__ int win_byte(uint32_t L, uint32_t M, uint32_t R, int 
     return static_cast<int>((w >> sh) & 0xFFu);
 }
 
+// max(a, b, c) as one v_max3_f32. fmaxf would first canonicalize each operand (IEEE mode quiets
+// signalling NaNs), doubling the instruction count; callers only pass finite values.
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// a + b + c (mod 2^32) as one v_add3_u32. Written as asm because LLVM reassociates chains of 3-row
+// sums into shared pair sums (two v_add_u32 per result instead of one v_add3).
+__device__ __forceinline__ uint32_t add3u(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 __device__ __forceinline__ uint64_t lanes_below() {
     const int l = lane_id();
     return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+
+// acc + number of set bits of m in lanes below this one (v_mbcnt_lo / v_mbcnt_hi).
+__device__ __forceinline__ int mbcnt64(uint64_t m, int acc) {
+    const uint32_t lo = __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), static_cast<uint32_t>(acc));
+    return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), lo));
 }
 
 // Order-preserving map of an IEEE float to an unsigned key (larger float -> larger key).

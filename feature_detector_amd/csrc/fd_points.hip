@@ -26,9 +26,10 @@ constexpr float kHarrisAlpha = 0.04f;                  // feature_point_harris_d
 
 // Workgroup -> (frame, 4 consecutive tiles of that frame); returns false for the idle waves of a
 // frame's last workgroup (they still take part in the workgroup barriers).
+// The tile coordinates are made visibly wave-uniform (readfirstlane), so row/tile logic stays scalar.
 __device__ __forceinline__ bool decode_tile(const PointsArgs &a, int &f, int &ty, int &tx) {
     f = blockIdx.x / a.blocks_per_frame;
-    const int t = (blockIdx.x % a.blocks_per_frame) * 4 + (threadIdx.x >> 6);
+    const int t = __builtin_amdgcn_readfirstlane((blockIdx.x % a.blocks_per_frame) * 4 + (threadIdx.x >> 6));
     tx = t % a.tiles_x;
     ty = t / a.tiles_x;
     return t < a.tiles_x * a.tiles_y;
@@ -36,8 +37,10 @@ __device__ __forceinline__ bool decode_tile(const PointsArgs &a, int &f, int &ty
 
 // Dword of frame bytes [off, off+4). `aligned` (cols % 4 == 0) guarantees whole-dword range checks;
 // otherwise assemble from byte loads so that a dword straddling the frame end still returns its bytes.
-__device__ __forceinline__ uint32_t load_px4(__amdgpu_buffer_rsrc_t r, int32_t off, bool aligned) {
-    if (aligned) return buf_load_u32(r, off);
+// A compile-time choice: a runtime branch here makes the waitcnt pass drain the prefetch queue.
+template <bool ALIGNED>
+__device__ __forceinline__ uint32_t load_px4(__amdgpu_buffer_rsrc_t r, int32_t off) {
+    if constexpr (ALIGNED) return buf_load_u32(r, off);
     return buf_load_u8(r, off) | (buf_load_u8(r, off + 1) << 8) | (buf_load_u8(r, off + 2) << 16) |
            (buf_load_u8(r, off + 3) << 24);
 }
@@ -61,45 +64,52 @@ __device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f)
     base = __builtin_amdgcn_readfirstlane(base);
     float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
     uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    // The level-0 histogram is counted here, once per staged candidate, rather than in the per-row
+    // emit path where every (row, column-of-4) slot would pay for the key computation.
     for (int i = lane_id(); i < sk.n; i += kWave) {
+        const float r = sk.resp[i];
+        if (sk.hist) atomicAdd(&sk.hist[float_key(r) >> 20], 1u);
         const int64_t pos = static_cast<int64_t>(base) + i;
         if (pos < a.list_cap) {
-            dr[pos] = sk.resp[i];
+            dr[pos] = r;
             di[pos] = sk.idx[i];
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // Drain the stores here (rare path) so the row loop's waitcnt state stays "loads only" and its
+    // prefetch queue is not flushed at every loop header. s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15).
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     sk.n = 0;
 }
 
 // Emit up to 4 candidates of this lane (columns c0..c0+3 of row `row`), preserving column order.
+// The lane's slot is the count of candidates in lower lanes: one v_mbcnt pair per column ballot.
+// b[m] is the wave ballot of fl[m] (callers that hold it as a compare mask pass it directly).
 template <bool RASTER, int SEGCAP>
 __device__ __forceinline__ void emit_row(Sink &sk, const PointsArgs &a, int f, int tx, int row, int c0,
-                                         const bool (&fl)[4], const float (&v)[4]) {
-    const uint64_t b0 = ballot(fl[0]), b1 = ballot(fl[1]), b2 = ballot(fl[2]), b3 = ballot(fl[3]);
-    const uint64_t lb = lanes_below();
-    int pos = popc64(b0 & lb) + popc64(b1 & lb) + popc64(b2 & lb) + popc64(b3 & lb);
-    const int tot = popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
-    const uint32_t rowbase = static_cast<uint32_t>(row) * static_cast<uint32_t>(a.cols);
+                                         const uint64_t (&b)[4], const bool (&fl)[4], const float (&v)[4]) {
+    const uint64_t b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+    const int tot = popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);  // scalar unit
+    const uint32_t id0 = static_cast<uint32_t>(row) * static_cast<uint32_t>(a.cols) + static_cast<uint32_t>(c0);
     if constexpr (RASTER) {
+        int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, 0))));
         const int64_t seg = (static_cast<int64_t>(f) * a.rows + row) * a.tiles_x + tx;
         if (lane_id() == 0) a.seg_cnt[seg] = tot;
         Cand *dst = a.seg + seg * SEGCAP;
 #pragma unroll
         for (int m = 0; m < 4; ++m)
-            if (fl[m]) dst[pos++] = Cand{v[m], rowbase + static_cast<uint32_t>(c0 + m)};
+            if (fl[m]) dst[pos++] = Cand{v[m], id0 + m};
     } else {
         if (tot == 0) return;
         if (sk.n + tot > kStage) sink_flush(sk, a, f);
-        pos += sk.n;
+        int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, sk.n))));
 #pragma unroll
         for (int m = 0; m < 4; ++m)
             if (fl[m]) {
                 sk.resp[pos] = v[m];
-                sk.idx[pos] = rowbase + static_cast<uint32_t>(c0 + m);
-                if (sk.hist) atomicAdd(&sk.hist[float_key(v[m]) >> 20], 1u);
+                sk.idx[pos] = id0 + m;
                 ++pos;
             }
         sk.n += tot;
@@ -131,35 +141,68 @@ __device__ __forceinline__ void hist_flush(const uint32_t *h, uint32_t *g) {
     }
 }
 
-// Stored response of one pixel (responses_ semantics: 0 unless written).
+// Two pixels' float math at a time: <2 x float> arithmetic compiles to v_pk_mul_f32 / v_pk_add_f32 /
+// v_pk_fma_f32, which round each lane exactly like the scalar op (the kernel is VALU-issue bound, and
+// a packed op retires two pixels' worth of one reference operation per issue slot).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Correctly rounded f32 sqrt of two values that are each 0 or normal: v_sqrt_f32 (within 1 ulp)
+// followed by the two fma residual corrections of the compiler's own IEEE expansion, minus its
+// denormal pre-scaling and inf/nan class fix-up. The Shi-Tomasi radicand d*d + 4b*b is either 0 or
+// >= 2^-54: b is 0 or |b| >= 1/9, and a != c differ by at least ulp(1/9) = 2^-27. For x == 0 the
+// s-1ulp candidate is a NaN whose residual compares false and the s+1ulp residual is -0, so 0 results.
+__device__ __forceinline__ f2 sqrt_rn_normal2(f2 x) {
+    const f2 s = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+    const f2 sdn = {__int_as_float(__float_as_int(s.x) - 1), __int_as_float(__float_as_int(s.y) - 1)};
+    const f2 sup = {__int_as_float(__float_as_int(s.x) + 1), __int_as_float(__float_as_int(s.y) + 1)};
+    const f2 rdn = __builtin_elementwise_fma(-sdn, s, x);
+    const f2 rup = __builtin_elementwise_fma(-sup, s, x);
+    f2 r;
+    r.x = rup.x > 0.0f ? sup.x : (rdn.x <= 0.0f ? sdn.x : s.x);
+    r.y = rup.y > 0.0f ? sup.y : (rdn.y <= 0.0f ? sdn.y : s.y);
+    return r;
+}
+
+// Stored responses of two pixels (responses_ semantics: 0 unless written), from exact integer tensor
+// sums. Same operations in the same order as the reference; only the issue is paired.
+//
+// Integer-to-float without v_cvt: every gradient product carries a bias beta (mod 2^32) chosen so that
+// the nine products of a 3x3 sum carry exactly 9*beta == 0x4B000000 (the bit pattern of 2^23), or
+// 0x4B400000 (2^23 + 2^22) for the signed cross term. Then for 0 <= S < 2^23 (S <= 9*255^2 here,
+// |Sxy| < 2^22) the biased sum read as a float is exactly 2^23 + S, and one exact (packed)
+// subtraction recovers float(S). 9 is odd, so beta = target * 9^-1 mod 2^32 exists.
+constexpr uint32_t kBiasSq = 0xB3000000u;  // 9 * kBiasSq == 0x4B000000 (mod 2^32)
+constexpr uint32_t kBiasXy = 0x41400000u;  // 9 * kBiasXy == 0x4B400000 (mod 2^32)
+static_assert(9u * kBiasSq == 0x4B000000u && 9u * kBiasXy == 0x4B400000u, "bias");
+
 template <int KIND>
-__device__ __forceinline__ float corner_response(int sxx, int syy, int sxy, float thr) {
-    float res = 0.0f;
+__device__ __forceinline__ f2 corner_response2(uint32_t sxx0, uint32_t sxx1, uint32_t syy0, uint32_t syy1,
+                                               uint32_t sxy0, uint32_t sxy1, float thr) {
+    const f2 fxx = f2{__uint_as_float(sxx0), __uint_as_float(sxx1)} - 8388608.0f;
+    const f2 fyy = f2{__uint_as_float(syy0), __uint_as_float(syy1)} - 8388608.0f;
+    const f2 fxy = f2{__uint_as_float(sxy0), __uint_as_float(sxy1)} - 12582912.0f;
+    f2 res;
     if constexpr (KIND == 0) {  // Harris, feature_point_harris_detector.cpp:95-103
-        const float fxx = static_cast<float>(sxx);
-        const float fyy = static_cast<float>(syy);
-        const float trace = fxx + fyy;
-        if (((trace * trace) * 0.21f) * kInvCnt2 > thr) {
-            const float fxy = static_cast<float>(sxy);
-            const float r = (((fxx * fyy) - (fxy * fxy)) - ((kHarrisAlpha * trace) * trace)) * kInvCnt2;
-            if (r > thr) res = r;
-        }
+        const f2 trace = fxx + fyy;
+        const f2 gate = ((trace * trace) * 0.21f) * kInvCnt2;
+        const f2 r = (((fxx * fyy) - (fxy * fxy)) - ((kHarrisAlpha * trace) * trace)) * kInvCnt2;
+        res.x = (gate.x > thr && r.x > thr) ? r.x : 0.0f;
+        res.y = (gate.y > thr && r.y > thr) ? r.y : 0.0f;
     } else {  // Shi-Tomasi, feature_point_shi_tomas_detector.cpp:94-103
-        const float a = static_cast<float>(sxx) * kInvCnt;
-        const float c = static_cast<float>(syy) * kInvCnt;
-        const float ac = a + c;
-        if (ac > thr) {
-            const float b = static_cast<float>(sxy) * kInvCnt;
-            const float d = a - c;
-            const float common = __builtin_sqrtf((d * d) + ((4.0f * b) * b));
-            const float r = (ac + common) * 0.5f;
-            if (r > thr) res = r;
-        }
+        const f2 a = fxx * kInvCnt;
+        const f2 c = fyy * kInvCnt;
+        const f2 ac = a + c;
+        const f2 b = fxy * kInvCnt;
+        const f2 d = a - c;
+        const f2 common = sqrt_rn_normal2((d * d) + ((4.0f * b) * b));
+        const f2 r = (ac + common) * 0.5f;
+        res.x = (ac.x > thr && r.x > thr) ? r.x : 0.0f;
+        res.y = (ac.y > thr && r.y > thr) ? r.y : 0.0f;
     }
     return res;
 }
 
-template <int KIND, bool RASTER, bool MASKED>
+template <int KIND, bool RASTER, bool MASKED, bool ALIGNED>
 __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, int tx, Sink &sk);
 
 // ---------------------------------------------------------------------------------------------------
@@ -167,7 +210,7 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
 // c0 = tx*kTileW + 4(l-1) .. c0+3 and walks the rows keeping 3-row sliding windows in registers:
 // pixels (+ DPP halo dwords), horizontal tensor sums, responses.
 // ---------------------------------------------------------------------------------------------------
-template <int KIND, bool RASTER, bool MASKED>
+template <int KIND, bool RASTER, bool MASKED, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
     __shared__ DetectLds lds_all[1];
     int f, ty, tx;
@@ -178,99 +221,136 @@ __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
         sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0};
         if (a.hist0) hist_clear(lds_all[0].hist);
     }
-    if (active) corner_tile<KIND, RASTER, MASKED>(a, f, ty, tx, sk);
+    if (active) corner_tile<KIND, RASTER, MASKED, ALIGNED>(a, f, ty, tx, sk);
     if constexpr (!RASTER) {
         if (active) sink_flush(sk, a, f);
         if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
     }
 }
 
-template <int KIND, bool RASTER, bool MASKED>
+template <int KIND, bool RASTER, bool MASKED, bool ALIGNED>
 __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, int tx, Sink &sk) {
     const int lane = lane_id();
     const int rows = a.rows, cols = a.cols;
     const int c0 = tx * kTileW + 4 * (lane - 1);
     const int y0 = 2 + ty * a.tile_h;
     const int y1 = min(y0 + a.tile_h, rows - 2);  // output rows [y0, y1) within [2, rows-3]
-    const bool aligned = a.aligned4 != 0;
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
+    // Every lane's 4 columns inside [2, cols-3]: then only the frame's first/last rows need masking.
+    const bool tile_interior = tx * kTileW - 4 >= 2 && tx * kTileW + 4 * 62 + 3 <= cols - 3;
 
     bool cval[4], colv[4];  // column inside [2, cols-3]; and owned by an interior lane (emitted)
+    uint64_t colv_b[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
         cval[m] = c0 + m >= 2 && c0 + m <= cols - 3;
         colv[m] = cval[m] && lane >= 1 && lane <= 62;
+        colv_b[m] = ballot(colv[m]);
     }
 
-    uint32_t P[3] = {0, 0, 0}, L[3] = {0, 0, 0}, R[3] = {0, 0, 0};
-    int hxx[3][4], hyy[3][4], hxy[3][4];
+    uint32_t hxx[3][4], hyy[3][4], hxy[3][4];  // biased horizontal sums (3 products, 3*beta)
     float rsp[3][4];
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
         for (int m = 0; m < 4; ++m) hxx[s][m] = hyy[s][m] = hxy[s][m] = 0, rsp[s][m] = 0.0f;
 
+    // Row ring of 6 dwords: rows ri-2 .. ri are in use while rows ri+1 .. ri+3 are in flight (a row
+    // step is about one HBM latency of wall time at full occupancy). The loop is unrolled by the ring
+    // length so every slot keeps a fixed register (no copies of in-flight loads at the back edge,
+    // which would force a vmcnt(0)). Rows outside the frame (including row -1) fall outside the
+    // buffer resource's range and read as 0.
     const int n_in = (y1 - y0) + 6;
-    for (int i0 = 0; i0 < n_in; i0 += 3) {
+    uint32_t ring[6];
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            const int su = (s + 1) % 3, sc = (s + 2) % 3;  // slots of rows ri-2 and ri-1
-            const int ri = y0 - 3 + i0 + s;                 // row loaded this step (slot s)
-            P[s] = load_px4(rs, ri * cols + c0, aligned);
-            L[s] = from_left(P[s]);
-            R[s] = from_right(P[s]);
+    for (int t = 0; t < 6; ++t) ring[t] = t < 3 ? load_px4<ALIGNED>(rs, (y0 - 3 + t) * cols + c0) : 0u;
+    // Once per wave: land the preheader loads, so the loop header's waitcnt state is the back edge's
+    // (three rows in flight) rather than the preheader's register order.
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    for (int i0 = 0; i0 < n_in; i0 += 6) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            const int s = t % 3, su = (t + 1) % 3, sc = (t + 2) % 3;  // 3-slot roles: rows ri, ri-2, ri-1
+            const int ri = y0 - 3 + i0 + t;                            // row consumed this step
+            ring[(t + 3) % 6] = load_px4<ALIGNED>(rs, (ri + 3) * cols + c0);
+            const uint32_t P_s = ring[t], P_su = ring[(t + 4) % 6], P_sc = ring[(t + 5) % 6];
 
-            // Gradient products of centre row ri-1 at columns c0-1..c0+4 (k = 0..5), then 3-wide
-            // horizontal sums for the lane's own columns (feature_point_harris_detector.cpp:35-62).
-            int qxx[6], qyy[6], qxy[6];
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const int j = k - 1;
-                const int ix = win_byte(L[sc], P[sc], R[sc], j + 1) - win_byte(L[sc], P[sc], R[sc], j - 1);
-                const int iy = win_byte(L[s], P[s], R[s], j) - win_byte(L[su], P[su], R[su], j);
-                qxx[k] = ix * ix;
-                qyy[k] = iy * iy;
-                qxy[k] = ix * iy;
-            }
+            // Gradients of centre row ri-1 at the lane's 4 columns (feature_point_harris_detector.cpp:
+            // 35-62); the two halo bytes of row ri-1 come from the neighbour lanes. Products carry the
+            // float-conversion bias (v_mad_i32_i24 with a constant addend: free).
+            const uint32_t Lc = from_left(P_sc), Rc = from_right(P_sc);
+            uint32_t qxx[6], qyy[6], qxy[6];
+            uint32_t bsq = kBiasSq, bxy = kBiasXy;
+            asm volatile("" : "+s"(bsq), "+s"(bxy));  // opaque: keeps v_mad (else mul + or)  // products at columns c0-1 .. c0+4 (k = m + 1)
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                hxx[sc][m] = qxx[m] + qxx[m + 1] + qxx[m + 2];
-                hyy[sc][m] = qyy[m] + qyy[m + 1] + qyy[m + 2];
-                hxy[sc][m] = qxy[m] + qxy[m + 1] + qxy[m + 2];
+                const int ix = win_byte(Lc, P_sc, Rc, m + 1) - win_byte(Lc, P_sc, Rc, m - 1);
+                const int iy = win_byte(0, P_s, 0, m) - win_byte(0, P_su, 0, m);
+                qxx[m + 1] = static_cast<uint32_t>(ix * ix) + bsq;
+                qyy[m + 1] = static_cast<uint32_t>(iy * iy) + bsq;
+                qxy[m + 1] = static_cast<uint32_t>(ix * iy) + bxy;
+            }
+            // Halo products from the neighbour lanes' edge columns (exact for lanes 0 / 63's inner
+            // columns, whose neighbours are lanes 1 / 62).
+            qxx[0] = from_left(qxx[4]);
+            qyy[0] = from_left(qyy[4]);
+            qxy[0] = from_left(qxy[4]);
+            qxx[5] = from_right(qxx[1]);
+            qyy[5] = from_right(qyy[1]);
+            qxy[5] = from_right(qxy[1]);
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                hxx[sc][m] = add3u(qxx[m], qxx[m + 1], qxx[m + 2]);
+                hyy[sc][m] = add3u(qyy[m], qyy[m + 1], qyy[m + 2]);
+                hxy[sc][m] = add3u(qxy[m], qxy[m + 1], qxy[m + 2]);
             }
 
-            // Response of row rr = ri-2: vertical 3-row sums are exact integers (< 2^24).
+            // Response of row rr = ri-2: vertical 3-row sums are exact integers (< 2^23).
             const int rr = ri - 2;
             const bool rowv = rr >= 2 && rr <= rows - 3;
-            uint32_t mb = 0xFu;
-            if constexpr (MASKED) mb = rowv ? mask_bits4(a, f, rr, c0) : 0u;
+            uint32_t sxx[4], syy[4], sxy[4];
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const int sxx = hxx[s][m] + hxx[su][m] + hxx[sc][m];
-                const int syy = hyy[s][m] + hyy[su][m] + hyy[sc][m];
-                const int sxy = hxy[s][m] + hxy[su][m] + hxy[sc][m];
-                const float r = corner_response<KIND>(sxx, syy, sxy, a.thr);
-                // Lane 0's columns 2-3 and lane 63's columns 0-1 are exact (their halo comes from
-                // lanes 1 / 62) and serve as the NMS neighbours of the tile's edge columns.
-                rsp[su][m] = (rowv && cval[m] && ((mb >> m) & 1u)) ? r : 0.0f;
+                sxx[m] = add3u(hxx[s][m], hxx[su][m], hxx[sc][m]);
+                syy[m] = add3u(hyy[s][m], hyy[su][m], hyy[sc][m]);
+                sxy[m] = add3u(hxy[s][m], hxy[su][m], hxy[sc][m]);
+            }
+            const f2 r01 = corner_response2<KIND>(sxx[0], sxx[1], syy[0], syy[1], sxy[0], sxy[1], a.thr);
+            const f2 r23 = corner_response2<KIND>(sxx[2], sxx[3], syy[2], syy[3], sxy[2], sxy[3], a.thr);
+            const float r[4] = {r01.x, r01.y, r23.x, r23.y};
+            if (!MASKED && rowv && tile_interior) {  // wave-uniform: no per-pixel masking needed
+#pragma unroll
+                for (int m = 0; m < 4; ++m) rsp[su][m] = r[m];
+            } else {
+                uint32_t mb = 0xFu;
+                if constexpr (MASKED) mb = rowv ? mask_bits4(a, f, rr, c0) : 0u;
+                // Lane 0's columns 2-3 and lane 63's columns 0-1 are exact and serve as the NMS
+                // neighbours of the tile's edge columns.
+#pragma unroll
+                for (int m = 0; m < 4; ++m) rsp[su][m] = (rowv && cval[m] && ((mb >> m) & 1u)) ? r[m] : 0.0f;
             }
 
             // NMS of row nr = ri-3 (feature_point_harris_detector.cpp:120-137): strict, 4-neighbour.
+            // x > thr and x > each neighbour  <=>  x > max(thr, neighbours)  (no NaNs; +-0 compare equal).
             const int nr = ri - 3;
             if (nr >= y0 && nr < y1) {  // wave-uniform
                 const float lft = from_left_f(rsp[s][3]);
                 const float rgt = from_right_f(rsp[s][0]);
                 bool fl[4];
                 float v[4];
+                uint64_t b[4];
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
                     const float x = rsp[s][m];
                     const float xl = m == 0 ? lft : rsp[s][m - 1];
                     const float xr = m == 3 ? rgt : rsp[s][m + 1];
+                    const float nb = max3f(max3f(xl, xr, a.thr), rsp[sc][m], rsp[su][m]);
+                    const bool hit = x > nb;
                     v[m] = x;
-                    fl[m] = colv[m] && x > a.thr && x > xl && x > xr && x > rsp[sc][m] && x > rsp[su][m];
+                    fl[m] = colv[m] && hit;
+                    b[m] = ballot(hit) & colv_b[m];  // the compare's lane mask, no bool round trip
                 }
-                emit_row<RASTER, kSegCorner>(sk, a, f, tx, nr, c0, fl, v);
+                emit_row<RASTER, kSegCorner>(sk, a, f, tx, nr, c0, b, fl, v);
                 if constexpr (RASTER) {
                     if (a.resp_map != nullptr) {
                         float *mrow = a.resp_map + (static_cast<int64_t>(f) * rows + nr) * cols;
@@ -326,11 +406,11 @@ __device__ __forceinline__ float fast_offset(int nseg, const int64_t *ks, const 
     return static_cast<float>(os[lo] + static_cast<double>(k - ks[lo]) * inc[lo]);
 }
 
-template <bool RASTER, bool MASKED>
+template <bool RASTER, bool MASKED, bool ALIGNED>
 __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int64_t *seg_k,
                                           const double *seg_o, const double *seg_inc, int f, int ty, int tx, Sink &sk);
 
-template <bool RASTER, bool MASKED>
+template <bool RASTER, bool MASKED, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
     __shared__ DetectLds lds_all[1];
     __shared__ int64_t seg_k[kMaxOffsetSegs];
@@ -350,14 +430,14 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
         sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0};
         if (a.hist0) hist_clear(lds_all[0].hist);
     }
-    if (active) fast_tile<RASTER, MASKED>(a, off, seg_k, seg_o, seg_inc, f, ty, tx, sk);
+    if (active) fast_tile<RASTER, MASKED, ALIGNED>(a, off, seg_k, seg_o, seg_inc, f, ty, tx, sk);
     if constexpr (!RASTER) {
         if (active) sink_flush(sk, a, f);
         if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
     }
 }
 
-template <bool RASTER, bool MASKED>
+template <bool RASTER, bool MASKED, bool ALIGNED>
 __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int64_t *seg_k,
                                           const double *seg_o, const double *seg_inc, int f, int ty, int tx, Sink &sk) {
     const int lane = lane_id();
@@ -365,7 +445,6 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
     const int c0 = tx * kTileW + 4 * (lane - 1);
     const int y0 = 3 + ty * a.tile_h;
     const int y1 = min(y0 + a.tile_h, rows - 3);  // output rows [y0, y1) within [3, rows-4]
-    const bool aligned = a.aligned4 != 0;
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
     const int diff = 15;  // kMinPixelDiffValue (feature_point_fast_detector.h:14)
 
@@ -378,11 +457,13 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
     for (int s = 0; s < 7; ++s) P[s] = L[s] = R[s] = 0;
 
     const int n_in = (y1 - y0) + 6;
+    uint32_t nxt = load_px4<ALIGNED>(rs, (y0 - 3) * cols + c0);  // one row of prefetch
     for (int i0 = 0; i0 < n_in; i0 += 7) {
 #pragma unroll
         for (int s = 0; s < 7; ++s) {
             const int ri = y0 - 3 + i0 + s;
-            P[s] = load_px4(rs, ri * cols + c0, aligned);
+            P[s] = nxt;
+            nxt = load_px4<ALIGNED>(rs, (ri + 1) * cols + c0);
             L[s] = from_left(P[s]);
             R[s] = from_right(P[s]);
             const int orow = ri - 3;  // output row; its window rows orow-3..orow+3 are slots s+1..s (mod 7)
@@ -454,7 +535,8 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
                 fl[m] = cand;
                 v[m] = resp;
             }
-            emit_row<RASTER, kSegFast>(sk, a, f, tx, orow, c0, fl, v);
+            const uint64_t b[4] = {ballot(fl[0]), ballot(fl[1]), ballot(fl[2]), ballot(fl[3])};
+            emit_row<RASTER, kSegFast>(sk, a, f, tx, orow, c0, b, fl, v);
             if constexpr (RASTER) {
                 if (a.resp_map != nullptr) {
                     float *mrow = a.resp_map + (static_cast<int64_t>(f) * rows + orow) * cols;
@@ -620,7 +702,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
             done = true;
         }
         if ((acc_m >> lane) & 1ull) {
-            const int pos = acc + popc64(acc_m & lanes_below());
+            const int pos = mbcnt64(acc_m, acc);
             if (pos < a.out_stride) {
                 float2 *o = reinterpret_cast<float2 *>(a.out_xy) + static_cast<int64_t>(f) * a.out_stride + pos;
                 *o = make_float2(static_cast<float>(x), static_cast<float>(y));
@@ -823,7 +905,7 @@ __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
                         uint32_t off = 0;
                         if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
                         off = __builtin_amdgcn_readfirstlane(off);
-                        if (hit) sup[off + popc64(m & lanes_below())] = sk;
+                        if (hit) sup[mbcnt64(m, off)] = sk;
                     }
                 }
             }
@@ -865,7 +947,7 @@ __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
                             uint32_t off = 0;
                             if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
                             off = __builtin_amdgcn_readfirstlane(off);
-                            if (hit) buf[off + popc64(m & lanes_below())] = sk;
+                            if (hit) buf[mbcnt64(m, off)] = sk;
                         }
                     }
                     __syncthreads();
@@ -1023,8 +1105,12 @@ static inline int blocks_for_waves(const PointsArgs &a) {
 
 hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s) {
     const dim3 grid(blocks_for_waves(a)), block(256);
-    const bool masked = a.mask != nullptr;
-#define FD_CORNER(K, RS, M) hipLaunchKernelGGL((k_corner<K, RS, M>), grid, block, 0, s, a)
+    const bool masked = a.mask != nullptr, aligned = a.aligned4 != 0;
+#define FD_CORNER(K, RS, M)                                                                  \
+    do {                                                                                     \
+        if (aligned) hipLaunchKernelGGL((k_corner<K, RS, M, true>), grid, block, 0, s, a);  \
+        else hipLaunchKernelGGL((k_corner<K, RS, M, false>), grid, block, 0, s, a);         \
+    } while (0)
     if (kind == 0) {
         if (raster) { if (masked) FD_CORNER(0, true, true); else FD_CORNER(0, true, false); }
         else { if (masked) FD_CORNER(0, false, true); else FD_CORNER(0, false, false); }
@@ -1038,14 +1124,15 @@ hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t
 
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s) {
     const dim3 grid(blocks_for_waves(a)), block(256);
-    const bool masked = a.mask != nullptr;
-    if (raster) {
-        if (masked) hipLaunchKernelGGL((k_fast<true, true>), grid, block, 0, s, a, off);
-        else hipLaunchKernelGGL((k_fast<true, false>), grid, block, 0, s, a, off);
-    } else {
-        if (masked) hipLaunchKernelGGL((k_fast<false, true>), grid, block, 0, s, a, off);
-        else hipLaunchKernelGGL((k_fast<false, false>), grid, block, 0, s, a, off);
-    }
+    const bool masked = a.mask != nullptr, aligned = a.aligned4 != 0;
+#define FD_FAST(RS, M)                                                                          \
+    do {                                                                                        \
+        if (aligned) hipLaunchKernelGGL((k_fast<RS, M, true>), grid, block, 0, s, a, off);     \
+        else hipLaunchKernelGGL((k_fast<RS, M, false>), grid, block, 0, s, a, off);            \
+    } while (0)
+    if (raster) { if (masked) FD_FAST(true, true); else FD_FAST(true, false); }
+    else { if (masked) FD_FAST(false, true); else FD_FAST(false, false); }
+#undef FD_FAST
     return hipGetLastError();
 }
 

@@ -86,7 +86,9 @@ T *as(DevBuf &b) {
 // Tile height: a multiple of `period` (3 for the corner walk, 7 for FAST) that still gives the launch
 // enough waves to fill 256 CUs, capped so halo rows stay a small overhead.
 int choose_tile_h(int64_t batch, int tiles_x, int out_rows, int period, int max_mult) {
-    const int64_t target_waves = 8192;
+    int64_t target_waves = 10240;  // ~2 rounds of resident waves at 256 CUs (measured sweep)
+    if (const char *e = std::getenv("FD_TARGET_WAVES")) target_waves = std::max<int64_t>(1, std::atoll(e));  // tuning
+    if (const char *e = std::getenv("FD_TILE_MULT")) max_mult = std::max(1, std::atoi(e));                   // tuning
     int64_t h = (batch * tiles_x * static_cast<int64_t>(out_rows)) / target_waves;
     h = std::max<int64_t>(h, 2 * period);
     h = ((h + period - 1) / period) * period;
@@ -226,8 +228,8 @@ PointGeom point_geom(int kind, int batch, int rows, int cols) {
     const int out_cols = cols - 2 * g.border;
     g.empty = g.out_rows <= 0 || out_cols <= 0;
     g.tiles_x = std::max(1, (cols - g.border + fdk::kTileW - 1) / fdk::kTileW);
-    const int period = kind == FD_FAST ? 7 : 3;
-    g.tile_h = choose_tile_h(batch, g.tiles_x, std::max(g.out_rows, 1), period, kind == FD_FAST ? 9 : 20);
+    const int period = kind == FD_FAST ? 7 : 6;  // rows per unrolled loop iteration of the kernel
+    g.tile_h = choose_tile_h(batch, g.tiles_x, std::max(g.out_rows, 1), period, kind == FD_FAST ? 9 : 100);
     g.tiles_y = std::max(1, (std::max(g.out_rows, 1) + g.tile_h - 1) / g.tile_h);
     g.blocks_per_frame = (g.tiles_x * g.tiles_y + 3) / 4;
     return g;

@@ -1,7 +1,10 @@
-"""Profiling driver (run under rocprofv3): the bench shapes' kernels only, a fixed number of times.
+"""Profiling driver (run under rocprofv3 --kernel-trace --stats): the bench shapes' kernels only, a
+fixed number of times, on seeded uniform-noise frames generated on the GPU.
 
   --shape bench      fd_points_detect, Harris, 640x480, batch 1 (BASELINE configs[1]), 200 calls
-  --shape northstar  fd_points_response (per-pixel kernel alone), Shi-Tomasi 1920x1080 batch 256, 10 calls
+  --shape northstar  fd_points_response (per-pixel kernel alone), 1920x1080 batch 256, 10 calls
+                     (--kind shi_tomasi by default: the north-star kernel)
+  --shape fast720    fd_points_detect, FAST, 1280x720 batch 64 (BASELINE configs[2]), 10 calls
 """
 import argparse
 import os
@@ -12,23 +15,37 @@ import torch  # noqa: E402
 
 import feature_detector_amd as fd  # noqa: E402
 
+THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 p = argparse.ArgumentParser()
 p.add_argument("--shape", default="bench", choices=["bench", "northstar", "fast720"])
+p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast"])
 p.add_argument("--calls", type=int, default=0)
 a = p.parse_args()
 g = torch.Generator(device="cuda")
 g.manual_seed(7)
+
+
+def noise(b, r, c):
+    return torch.randint(0, 256, (b, r, c), generator=g, device="cuda", dtype=torch.int32).to(torch.uint8)
+
+
 if a.shape == "bench":
-    frames = torch.randint(0, 256, (1, 480, 640), generator=g, device="cuda", dtype=torch.int32).to(torch.uint8)
+    kind = a.kind or "harris"
+    frames = noise(1, 480, 640)
     for _ in range(a.calls or 200):
-        fd.detect_points("harris", frames, 200, 20, 30.0)
+        fd.detect_points(kind, frames, 200, 20, THR[kind])
 elif a.shape == "northstar":
-    frames = torch.randint(0, 256, (256, 1080, 1920), generator=g, device="cuda", dtype=torch.int32).to(torch.uint8)
+    kind = a.kind or "shi_tomasi"
+    frames = noise(256, 1080, 1920)
+    cap = 1080 * 1920 if kind == "fast" else 1080 * 1920 // 2 + 64
+    out = (torch.empty((256, cap), dtype=torch.float32, device="cuda"),
+           torch.empty((256, cap), dtype=torch.int32, device="cuda"), torch.empty((256,), dtype=torch.int32, device="cuda"))
     for _ in range(a.calls or 10):
-        fd.point_response("shi_tomasi", frames, 40.0)
+        fd.point_response(kind, frames, THR[kind], out=out)
 else:
-    frames = torch.randint(0, 256, (64, 720, 1280), generator=g, device="cuda", dtype=torch.int32).to(torch.uint8)
+    kind = a.kind or "fast"
+    frames = noise(64, 720, 1280)
     for _ in range(a.calls or 10):
-        fd.detect_points("fast", frames, 200, 20, 10.0)
+        fd.detect_points(kind, frames, 200, 20, THR[kind])
 torch.cuda.synchronize()
-print("done", a.shape)
+print("done", a.shape, kind)
