@@ -1,4 +1,4 @@
-// Kernel argument blocks and host-side launchers (defined in fd_points.hip / fd_lsd.hip).
+// Kernel argument blocks and host-side launchers (defined in fd_points.hip / fd_select.hip / fd_lsd.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -14,7 +14,7 @@ constexpr int kSegFast = kTileW;        // FAST has no NMS
 constexpr int kSelectChunk = 2048;      // candidates sorted per greedy chunk (LDS)
 constexpr int kGridLdsCells = 16384;    // occupancy grid kept in LDS up to this many cells
 constexpr int kMaxOffsetSegs = 48;
-constexpr int kHistBins = 4096;         // level-0 digit of the selection key: top 12 bits of the response
+constexpr int kHistBins = 4096;         // level-0 digit of the selection key: top 12 bits of the mapped response
 
 // A raster-mode segment entry (fd_points_candidates only).
 struct Cand {
@@ -47,6 +47,8 @@ struct PointsArgs {
     int64_t list_cap;
     uint32_t *list_count;
     uint32_t *hist0;  // [batch][kHistBins] or null
+    uint32_t key_base;  // level-0 bin = ((float_key(resp) - key_base) << key_lz) >> 20 (see SelectArgs)
+    int key_lz;
     // raster mode: per (frame, row, tile_x) segments
     int32_t *seg_cnt;
     Cand *seg;
@@ -59,8 +61,8 @@ struct PointsArgs {
 struct SelectArgs {
     const float *list_resp;
     const uint32_t *list_idx;
-    const uint32_t *list_count;
-    const uint32_t *hist0;
+    uint32_t *list_count;  // reset to 0 by the kernel once the frame is done
+    uint32_t *hist0;       // [batch][kHistBins], reset likewise
     int64_t list_cap;
     int rows, cols;
     const uint32_t *mask;
@@ -69,10 +71,15 @@ struct SelectArgs {
     uint32_t need;
     int dist;
     int grid_w, grid_h;
-    uint32_t *grid_global;  // [batch][grid_w * grid_h] when the grid does not fit LDS
+    uint32_t *grid_global;  // [batch][grid_w * grid_h] when the grid does not fit LDS (slow path)
     float *out_xy;
     int out_stride;
     int32_t *out_counts;
+    // key map: 32-bit key = (float_key(response) - key_base) << key_lz; all candidates have
+    // responses > min_valid_response, so key_base = float_key(min_valid_response) and key_lz spreads
+    // the possible response range over the full 32 bits (finer level-0 bins).
+    uint32_t key_base;
+    int key_lz;
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 

@@ -68,7 +68,7 @@ __device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f)
     // emit path where every (row, column-of-4) slot would pay for the key computation.
     for (int i = lane_id(); i < sk.n; i += kWave) {
         const float r = sk.resp[i];
-        if (sk.hist) atomicAdd(&sk.hist[float_key(r) >> 20], 1u);
+        if (sk.hist) atomicAdd(&sk.hist[((float_key(r) - a.key_base) << a.key_lz) >> 20], 1u);
         const int64_t pos = static_cast<int64_t>(base) + i;
         if (pos < a.list_cap) {
             dr[pos] = r;
@@ -608,446 +608,6 @@ __global__ __launch_bounds__(1024) void k_fast_mask_scan(const uint32_t *mask, i
 }
 
 // ---------------------------------------------------------------------------------------------------
-// K4: per-frame greedy selection (SelectGoodFeatures, feature_point_detector.cpp:54-88).
-// Candidates are visited in (response desc, raster index asc) order without a full sort: a radix
-// descent over the 64-bit key sk = (orderable response bits << 32) | ~idx cuts the frame's list into
-// consecutive chunks of <= kSelectChunk keys, each gathered into LDS, bitonic-sorted and scanned by
-// one wave. Accepted features live in an occupancy grid of (d+1)-sized cells: at most one accepted
-// feature per cell, so a Chebyshev-distance test needs the 3x3 neighbouring cells only.
-// ---------------------------------------------------------------------------------------------------
-constexpr int kLevels = 8;
-// digit widths per level: 12 (sign, exponent, 3 mantissa bits of the response), then 8 x 6, then 4
-__device__ __forceinline__ int lvl_width(int l) { return l == 0 ? 12 : (l == 7 ? 4 : 8); }
-__device__ __forceinline__ int lvl_top(int l) { return l == 7 ? 64 : 12 + 8 * l; }  // bits consumed through l
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-
-// Diagnostic phase clocks (only when a.stamps is set): slot 15 keeps the last clock; FD_STAMP(k)
-// adds the time since then to slot k.
-#define FD_STAMP(slot)                                                                  \
-    do {                                                                                \
-        if (a.stamps && threadIdx.x == 0) {                                             \
-            const uint64_t now_ = __builtin_readcyclecounter();                         \
-            uint64_t *st_ = a.stamps + blockIdx.x * 16;                                 \
-            if ((slot) > 0) st_[(slot)] += now_ - st_[15];                              \
-            st_[15] = now_;                                                             \
-        }                                                                               \
-    } while (0)
-
-__device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx) {
-    return (static_cast<uint64_t>(float_key(resp)) << 32) | static_cast<uint64_t>(~idx);
-}
-
-constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
-constexpr int kSubChunk = 512;  // keys sorted per greedy sub-chunk
-
-// One wave scans a sorted chunk in order (SelectGoodFeatures, feature_point_detector.cpp:62-72), a
-// batch of 64 candidates at a time: occupancy-grid test against earlier batches, then the batch is
-// resolved at once from cmask (per candidate: earlier candidates of its batch within distance d,
-// computed beforehand by the whole workgroup).
-// GRID: 0 = no distance test (d <= 0), 1 = occupancy grid in LDS, 2 = grid in global memory.
-template <int GRID>
-__device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
-                                             const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
-                                             uint32_t prior, int &s_acc, int &s_done) {
-    const int lane = lane_id();
-    const int d = a.dist;
-    int acc = s_acc;
-    bool done = false;
-    for (int b0 = 0; b0 < cnt && !done; b0 += kWave) {
-        const int i = b0 + lane;
-        const bool in = i < cnt;
-        const uint32_t e = in ? pxy[i] : kEmpty;
-        bool ok = e != kEmpty;
-        const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-        int cell = gw2 + 1;
-        uint64_t C = 0;
-        if constexpr (GRID != 0) {
-            cell = in ? static_cast<int>(pcell[i]) : gw2 + 1;
-            C = in ? cmask[i] : 0ull;
-            uint32_t g[9];
-#pragma unroll
-            for (int q = 0; q < 9; ++q) {
-                const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
-                if constexpr (GRID == 1) g[q] = grid[o];
-                else g[q] = __hip_atomic_load(&grid[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int q = 0; q < 9; ++q) {
-                const int gx = static_cast<int>(g[q] & 0xFFFFu), gy = static_cast<int>(g[q] >> 16);
-                if (g[q] != kEmpty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
-            }
-        }
-        const uint64_t m = ballot(ok);
-        C &= m;
-        // Fixed point: a lane is decided once all of C is; accepted iff none of C was accepted.
-        uint64_t acc_m = 0, dec_m = ~m;
-        bool mine = !ok;
-        while (dec_m != ~0ull) {
-            const bool can = !mine && (C & ~dec_m) == 0;
-            const bool take = can && (C & acc_m) == 0;
-            dec_m |= ballot(can);
-            acc_m |= ballot(take);
-            mine = mine || can;
-        }
-        // need cutoff (:67-69): features.size() >= need is checked after every append
-        const uint32_t have = prior + static_cast<uint32_t>(acc);
-        const int allow = have < a.need ? static_cast<int>(a.need - have) : 1;
-        if (popc64(acc_m) >= allow) {
-            uint64_t keep = 0, t = acc_m;
-            for (int k = 0; k < allow; ++k) {
-                keep |= t & (~t + 1ull);
-                t &= t - 1ull;
-            }
-            acc_m = keep;
-            done = true;
-        }
-        if ((acc_m >> lane) & 1ull) {
-            const int pos = mbcnt64(acc_m, acc);
-            if (pos < a.out_stride) {
-                float2 *o = reinterpret_cast<float2 *>(a.out_xy) + static_cast<int64_t>(f) * a.out_stride + pos;
-                *o = make_float2(static_cast<float>(x), static_cast<float>(y));
-            }
-            if constexpr (GRID != 0) {
-                const uint32_t ev = (static_cast<uint32_t>(y) << 16) | static_cast<uint32_t>(x);
-                if constexpr (GRID == 1) grid[cell] = ev;
-                else __hip_atomic_store(&grid[cell], ev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        acc += popc64(acc_m);
-        if constexpr (GRID == 2) __builtin_amdgcn_s_waitcnt(0);
-    }
-    if (lane == 0) {
-        s_acc = acc;
-        if (done) s_done = 1;
-    }
-}
-
-__global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
-    __shared__ uint32_t suf0[kHistBins + 1];
-    __shared__ uint32_t sufl[kLevels - 1][257];
-    __shared__ __attribute__((aligned(16))) uint64_t sup[kSelectChunk];  // superchunk keys (unsorted)
-    // sub-chunk keys (merge-sorted between buf and tmp; buf later holds the conflict masks)
-    __shared__ __attribute__((aligned(16))) uint64_t buf[kSelectChunk];
-    __shared__ __attribute__((aligned(16))) uint64_t tmp[kSelectChunk];
-    // sorted chunk, decoded: (y << 16) | x (kEmpty when a prior masks it) and occupancy-grid cell
-    __shared__ __attribute__((aligned(16))) uint32_t pxy[kSelectChunk];
-    __shared__ uint32_t pcell[kSelectChunk];
-    __shared__ uint32_t grid_lds[kGridLdsCells];
-    __shared__ uint64_t prefix[kLevels];
-    __shared__ int resume[kLevels];
-    __shared__ uint32_t gcount;
-    __shared__ int s_done, s_acc;
-
-    const int f = blockIdx.x;
-    const int tid = threadIdx.x, nthr = blockDim.x, lane = lane_id(), wave = tid >> 6;
-    const int rows = a.rows, cols = a.cols;
-    const int64_t n = min(static_cast<int64_t>(a.list_count[f]), a.list_cap);
-    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
-    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
-    const int d = a.dist;
-    const bool use_grid = d >= 1;
-    // Occupancy grid of (d+1)-sized cells with a one-cell border (no bounds checks in the scan).
-    const int gw2 = a.grid_w + 2;
-    const int cells = gw2 * (a.grid_h + 2);
-    const bool grid_in_lds = cells <= kGridLdsCells;
-    uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
-    const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
-    const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
-    FD_STAMP(0);
-
-    if (use_grid) {
-        if (grid_in_lds)
-            for (int i = tid; i < cells; i += nthr) grid_lds[i] = kEmpty;
-        else
-            for (int i = tid; i < cells; i += nthr) grid_g[i] = kEmpty;
-    }
-    if (tid == 0) {
-        s_done = 0;
-        s_acc = 0;
-        prefix[0] = 0;
-    }
-    if (n == 0) {  // RETURN_TRUE_IF(candidates_.empty()) (:55)
-        if (tid == 0) a.out_counts[f] = 0;
-        return;
-    }
-
-    // In-place suffix sums of S[0..nb) by the whole block; S[nb] = 0.
-    __shared__ uint32_t wtot[16];
-    auto suffix = [&](uint32_t *S, int nb) {
-        const int ch = (nb + nthr - 1) / nthr;  // contiguous bins per thread (<= 4)
-        const int b0 = min(tid * ch, nb), b1 = min(b0 + ch, nb);
-        uint32_t v[4] = {0, 0, 0, 0};
-        uint32_t sacc = 0;
-        for (int b = b0; b < b1; ++b) {
-            v[b - b0] = S[b];
-            sacc += v[b - b0];
-        }
-        // suffix over threads: wave-level, then across the 16 waves
-        uint32_t incl = sacc;
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint32_t t = __shfl_down(incl, o);
-            if (lane + o < kWave) incl += t;
-        }
-        if (lane == 0) wtot[wave] = incl;
-        __syncthreads();
-        uint32_t after = 0;
-        for (int q = wave + 1; q < nthr / kWave; ++q) after += wtot[q];
-        uint32_t run = incl - sacc + after;
-        for (int b = b1 - 1; b >= b0; --b) {
-            run += v[b - b0];
-            S[b] = run;
-        }
-        if (tid == 0) S[nb] = 0;
-        __syncthreads();
-    };
-    // Histogram of digit `lvl` (>= 1) over keys in [klo, khi] (one pass over the list).
-    auto build = [&](int lvl, uint64_t klo, uint64_t khi, uint32_t *S) {
-        const int nb = 1 << lvl_width(lvl);
-        const int rem = 64 - lvl_top(lvl);
-        for (int b = tid; b <= nb; b += nthr) S[b] = 0;
-        __syncthreads();
-        for (int64_t b0 = tid; b0 < n; b0 += static_cast<int64_t>(kPassUnroll) * nthr) {
-            float r[kPassUnroll];
-            uint32_t ix[kPassUnroll];
-#pragma unroll
-            for (int u = 0; u < kPassUnroll; ++u) {
-                const int64_t i = min(b0 + static_cast<int64_t>(u) * nthr, n - 1);
-                r[u] = lresp[i];
-                ix[u] = lidx[i];
-            }
-#pragma unroll
-            for (int u = 0; u < kPassUnroll; ++u) {
-                const int64_t i = b0 + static_cast<int64_t>(u) * nthr;
-                const uint64_t sk = make_key(r[u], ix[u]);
-                if (i < n && sk >= klo && sk <= khi) atomicAdd(&S[(sk >> rem) & static_cast<uint64_t>(nb - 1)], 1u);
-            }
-        }
-        __syncthreads();
-        suffix(S, nb);
-    };
-    auto suf = [&](int lvl) -> uint32_t * { return lvl == 0 ? suf0 : sufl[lvl - 1]; };
-
-    // Level-0 histogram: accumulated by the per-pixel kernel while it emitted the candidates.
-    for (int b = tid; b < kHistBins; b += nthr) suf0[b] = a.hist0[static_cast<int64_t>(f) * kHistBins + b];
-    __syncthreads();
-    FD_STAMP(1);
-    suffix(suf0, kHistBins);
-    FD_STAMP(2);
-    int level = 0;
-    int hi = (1 << lvl_width(0)) - 1;
-    while (true) {
-        if (s_done) break;
-        if (hi < 0) {
-            if (level == 0) break;
-            --level;
-            hi = resume[level];
-            continue;
-        }
-        const uint32_t *S = suf(level);
-        const uint32_t base = S[hi + 1];
-        const uint32_t lim = static_cast<uint32_t>(kSelectChunk);
-        // smallest lo in [0, hi] with S[lo] - base <= lim (S is non-increasing in b)
-        int lo_b = 0, hi_b = hi + 1;
-        while (lo_b < hi_b) {
-            const int mid = (lo_b + hi_b) >> 1;
-            if (S[mid] - base <= lim) hi_b = mid; else lo_b = mid + 1;
-        }
-        int lo = lo_b;
-        const int w = lvl_width(level);
-        const int rem = 64 - lvl_top(level);
-        const uint64_t pre = prefix[level];
-        if (lo > hi) {  // bin `hi` alone exceeds a chunk: descend into it
-            __syncthreads();
-            if (tid == 0) {
-                resume[level] = hi - 1;
-                prefix[level + 1] = (pre << w) | static_cast<uint64_t>(hi);
-            }
-            __syncthreads();
-            const uint64_t klo = ((pre << w) | static_cast<uint64_t>(hi)) << rem;
-            const uint64_t khi = klo | ((1ull << rem) - 1ull);
-            ++level;
-            if (a.stamps && tid == 0) a.stamps[blockIdx.x * 16 + 9] += 1;
-            FD_STAMP(7);
-            build(level, klo, khi, suf(level));
-            FD_STAMP(6);  // descent pass
-            hi = (1 << lvl_width(level)) - 1;
-            continue;
-        }
-        const uint32_t cnt = S[lo] - base;
-        FD_STAMP(7);  // loop control
-        if (cnt > 0) {
-            const uint64_t klo = ((pre << w) | static_cast<uint64_t>(lo)) << rem;
-            const uint64_t khi = (((pre << w) | static_cast<uint64_t>(hi)) << rem) | ((1ull << rem) - 1ull);
-            const uint32_t k32lo = static_cast<uint32_t>(klo >> 32), k32hi = static_cast<uint32_t>(khi >> 32);
-            // gather the chunk: wave-uniform loop bounds, one LDS atomic per wave per round
-            if (tid == 0) gcount = 0;
-            __syncthreads();
-            for (int64_t b0 = static_cast<int64_t>(wave) * kWave; b0 < n;
-                 b0 += static_cast<int64_t>(kPassUnroll) * nthr) {
-                float r[kPassUnroll];
-                uint32_t ix[kPassUnroll];
-#pragma unroll
-                for (int u = 0; u < kPassUnroll; ++u) {  // unconditional (clamped) loads: all in flight
-                    const int64_t i = min(b0 + static_cast<int64_t>(u) * nthr + lane, n - 1);
-                    r[u] = lresp[i];
-                    ix[u] = lidx[i];
-                }
-#pragma unroll
-                for (int u = 0; u < kPassUnroll; ++u) {
-                    const int64_t i = b0 + static_cast<int64_t>(u) * nthr + lane;
-                    const uint32_t k32 = float_key(r[u]);
-                    const bool near = i < n && k32 >= k32lo && k32 <= k32hi;  // cheap 32-bit prefilter
-                    if (ballot(near) == 0ull) continue;
-                    const uint64_t sk = make_key(r[u], ix[u]);
-                    const bool hit = near && sk >= klo && sk <= khi;
-                    const uint64_t m = ballot(hit);
-                    if (m) {
-                        uint32_t off = 0;
-                        if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
-                        off = __builtin_amdgcn_readfirstlane(off);
-                        if (hit) sup[mbcnt64(m, off)] = sk;
-                    }
-                }
-            }
-            __syncthreads();
-            FD_STAMP(3);  // gather
-            const uint32_t s1 = static_cast<uint32_t>(d + 1);
-            auto place = [&](int pos, uint64_t sk) {  // decode position, prior mask, grid cell
-                const uint32_t idx = ~static_cast<uint32_t>(sk);
-                const uint32_t y = idx / static_cast<uint32_t>(cols);
-                const uint32_t x = idx - y * static_cast<uint32_t>(cols);
-                bool ok = true;
-                if (fmask) ok = (fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u;
-                pxy[pos] = ok ? ((y << 16) | x) : kEmpty;
-                if (use_grid) pcell[pos] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
-            };
-            // Sub-chunks of <= kSubChunk keys from the top bins of the superchunk (already in LDS):
-            // the greedy usually stops within the first few hundred keys.
-            int shi = hi;
-            while (shi >= lo && !s_done) {
-                const uint32_t sbase = S[shi + 1];
-                int q0 = lo, q1 = shi + 1;
-                while (q0 < q1) {
-                    const int mid = (q0 + q1) >> 1;
-                    if (S[mid] - sbase <= static_cast<uint32_t>(kSubChunk)) q1 = mid; else q0 = mid + 1;
-                }
-                const int slo = min(q0, shi);  // one bin larger than a sub-chunk is taken whole
-                const uint32_t sc = S[slo] - sbase;
-                if (sc > 0) {
-                    const uint64_t sklo = ((pre << w) | static_cast<uint64_t>(slo)) << rem;
-                    const uint64_t skhi = (((pre << w) | static_cast<uint64_t>(shi)) << rem) | ((1ull << rem) - 1ull);
-                    if (tid == 0) gcount = 0;
-                    __syncthreads();
-                    for (int b0 = wave * kWave; b0 < static_cast<int>(cnt); b0 += nthr) {
-                        const int i = b0 + lane;
-                        const uint64_t sk = i < static_cast<int>(cnt) ? sup[i] : 0ull;
-                        const bool hit = i < static_cast<int>(cnt) && sk >= sklo && sk <= skhi;
-                        const uint64_t m = ballot(hit);
-                        if (m) {
-                            uint32_t off = 0;
-                            if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
-                            off = __builtin_amdgcn_readfirstlane(off);
-                            if (hit) buf[mbcnt64(m, off)] = sk;
-                        }
-                    }
-                    __syncthreads();
-                    FD_STAMP(10);  // sub-chunk extract
-                {
-                    // Merge sort of unique keys, descending: rank inside runs of 64 by counting larger
-                    // keys (broadcast LDS reads), then log2 merge levels where each key moves to
-                    // (its offset in its run) + (number of larger keys in the sibling run, by binary search).
-                    const int c = static_cast<int>(sc);
-                    const int c64 = (c + 63) & ~63;
-                    for (int i = c + tid; i < c64; i += nthr) buf[i] = 0ull;
-                    __syncthreads();
-                    for (int p = tid; p < c; p += nthr) {
-                        const uint64_t me = buf[p];
-                        const ulonglong2 *b2 = reinterpret_cast<const ulonglong2 *>(buf + (p & ~63));
-                        int lr = 0;
-    #pragma unroll 8
-                        for (int j = 0; j < 32; ++j) {
-                            const ulonglong2 q = b2[j];
-                            lr += (q.x > me) + (q.y > me);
-                        }
-                        tmp[(p & ~63) + lr] = me;
-                    }
-                    __syncthreads();
-                    FD_STAMP(11);  // run sort
-                    uint64_t *src = tmp, *dst = buf;
-                    for (int w = 64; w < c; w <<= 1) {
-                        for (int p = tid; p < c; p += nthr) {
-                            const uint64_t me = src[p];
-                            const int run = p / w;
-                            const int pair = (run & ~1) * w;
-                            const int sib = (run ^ 1) * w;
-                            int lo2 = 0, hi2 = max(0, min(w, c - sib));  // larger keys in the sibling run
-                            while (lo2 < hi2) {
-                                const int mid = (lo2 + hi2) >> 1;
-                                if (src[sib + mid] > me) lo2 = mid + 1; else hi2 = mid;
-                            }
-                            dst[pair + (p - run * w) + lo2] = me;
-                        }
-                        __syncthreads();
-                        uint64_t *t2 = src;
-                        src = dst;
-                        dst = t2;
-                    }
-                    FD_STAMP(12);  // merges
-                    for (int i = tid; i < c; i += nthr) place(i, src[i]);
-                    __syncthreads();
-                    FD_STAMP(13);  // place
-                    // conflict masks: earlier candidates of the same 64-batch within distance d
-                    if (use_grid) {
-                        for (int p = tid; p < c; p += nthr) {
-                            const uint32_t e = pxy[p];
-                            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-                            uint64_t C = 0;
-                            const int bb = p & ~63, me = p - bb;
-                            const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb);  // broadcast reads
-                            const int n4 = (me + 3) >> 2;  // only earlier entries matter
-#pragma unroll 2
-                            for (int j4 = 0; j4 < n4; ++j4) {
-                                const uint4 e4 = q4[j4];
-                                const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
-                                uint32_t bits = 0;
-#pragma unroll
-                                for (int t = 0; t < 4; ++t) {
-                                    const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
-                                    const bool nb = j4 * 4 + t < me && ev[t] != kEmpty && abs(x - ex) <= d && abs(y - ey) <= d;
-                                    bits |= static_cast<uint32_t>(nb) << t;
-                                }
-                                C |= static_cast<uint64_t>(bits) << (j4 * 4);
-                            }
-                            buf[p] = e == kEmpty ? 0ull : C;
-                        }
-                    }
-                }
-                __syncthreads();
-                FD_STAMP(14);  // conflict masks
-                // greedy scan in order by wave 0 (SelectGoodFeatures :62-72)
-                if (tid < kWave) {
-                    const int c = static_cast<int>(sc);
-                    if (!use_grid)
-                        greedy_chunk<0>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done);
-                    else if (grid_in_lds)
-                        greedy_chunk<1>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done);
-                    else
-                        greedy_chunk<2>(a, f, c, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done);
-                }
-                __syncthreads();
-                FD_STAMP(5);  // greedy
-                }
-                shi = slo - 1;
-            }
-            if (a.stamps && tid == 0) a.stamps[blockIdx.x * 16 + 8] += 1;
-        }
-        hi = lo - 1;
-    }
-    if (tid == 0) a.out_counts[f] = s_acc;
-    FD_STAMP(7);
-}
-
-// ---------------------------------------------------------------------------------------------------
 // K2: raster compaction of the per-(row, tile) segments into the reference's push order.
 // ---------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_compact(CompactArgs a) {
@@ -1149,11 +709,6 @@ hipError_t launch_fast_mask_scan(const uint32_t *mask, int mask_wpr, int batch, 
                                  int32_t *word_pref, hipStream_t s) {
     hipLaunchKernelGGL(k_fast_mask_scan, dim3(batch), dim3(1024), 0, s, mask, mask_wpr, rows, cols, row_base,
                        word_pref);
-    return hipGetLastError();
-}
-
-hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
-    hipLaunchKernelGGL(k_select, dim3(batch), dim3(1024), 0, s, a);
     return hipGetLastError();
 }
 

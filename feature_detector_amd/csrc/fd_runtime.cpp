@@ -32,7 +32,12 @@ struct fd_ctx {
     std::string err;
     // workspace
     DevBuf frames, prior_xy, prior_frame, prior_counts, mask, row_base, word_pref;
-    DevBuf list_resp, list_idx, list_count, hist0, out_xy, out_counts, grid;
+    DevBuf list_resp, list_idx, out_xy, out_counts, grid;
+    // selection control block: [batch][kHistBins] level-0 histograms, then list_count per frame.
+    // Zero between calls: k_select resets what a call used. sel_dirty marks a call whose kernels may
+    // not have run to the end (the next call clears the block first).
+    DevBuf selctl;
+    bool sel_dirty = true;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts;
     DevBuf dbg;
@@ -240,6 +245,48 @@ int64_t detect_list_cap(int kind, int rows, int cols) {
     return (kind == FD_FAST ? px : px / 2) + 64;
 }
 
+struct SelectBufs {
+    uint32_t *hist0, *list_count;
+};
+
+// Candidate lists and the (self-resetting) control block for `batch` frames.
+int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
+    FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
+    FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
+    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 1);
+    if (c->selctl.n < ctl) {
+        FD_HIP_TRY(c, ensure(c->selctl, ctl));
+        c->sel_dirty = true;
+    }
+    if (c->sel_dirty) {
+        FD_HIP_TRY(c, hipMemsetAsync(c->selctl.p, 0, c->selctl.n, c->stream));
+        c->sel_dirty = false;
+    }
+    uint32_t *base = as<uint32_t>(c->selctl);
+    sb.hist0 = base;
+    sb.list_count = base + static_cast<size_t>(batch) * fdk::kHistBins;
+    return FD_OK;
+}
+
+uint32_t host_float_key(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, sizeof(u));
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Key map of the selection (SelectArgs::key_base / key_lz): candidates have responses in
+// (thr, rmax], rmax = +inf for the corner detectors and 16 + the largest FAST offset (+1) for FAST.
+void key_map(int kind, float thr, const fdk::FastOffsets *off, int64_t n_off, uint32_t &base, int &lz) {
+    base = host_float_key(thr);
+    uint32_t kmax = host_float_key(std::numeric_limits<float>::infinity());
+    if (kind == FD_FAST && off && off->nseg > 0 && n_off > 0) {
+        const int s = off->nseg - 1;
+        const double omax = off->o_start[s] + static_cast<double>(n_off - 1 - off->k_start[s]) * off->inc[s];
+        kmax = std::max(base, host_float_key(static_cast<float>(16.0 + omax + 1.0)));
+    }
+    lz = kmax > base ? __builtin_clz(kmax - base) : 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -272,7 +319,7 @@ void fd_ctx_destroy(fd_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->frames,    &c->prior_xy,  &c->prior_frame, &c->prior_counts, &c->mask,       &c->row_base,
-                      &c->word_pref, &c->list_resp, &c->list_idx,  &c->list_count,   &c->hist0,      &c->out_xy,
+                      &c->word_pref, &c->list_resp, &c->list_idx,  &c->selctl,      &c->out_xy,
                       &c->out_counts, &c->grid,     &c->dbg,
                       &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
@@ -320,10 +367,9 @@ int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t m
     if (rc) return rc;
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const int64_t cap = detect_list_cap(kind, rows, cols);
-    FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
-    FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
-    FD_HIP_TRY(c, ensure(c->list_count, sizeof(uint32_t) * batch));
-    FD_HIP_TRY(c, ensure(c->hist0, sizeof(uint32_t) * fdk::kHistBins * batch));
+    SelectBufs sb{};
+    rc = select_buffers(c, batch, cap, sb);
+    if (rc) return rc;
     FD_HIP_TRY(c, ensure(c->prior_counts, sizeof(int32_t) * batch));
     if (max_prior_total > 0) {
         FD_HIP_TRY(c, ensure(c->prior_xy, sizeof(float) * 2 * max_prior_total));
@@ -353,12 +399,9 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
 
     const PointGeom g = point_geom(kind, batch, rows, cols);
     const int64_t cap = detect_list_cap(kind, rows, cols);
-    FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
-    FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
-    FD_HIP_TRY(c, ensure(c->list_count, sizeof(uint32_t) * batch));
-    FD_HIP_TRY(c, ensure(c->hist0, sizeof(uint32_t) * fdk::kHistBins * batch));
-    FD_HIP_TRY(c, hipMemsetAsync(c->list_count.p, 0, sizeof(uint32_t) * batch, c->stream));
-    FD_HIP_TRY(c, hipMemsetAsync(c->hist0.p, 0, sizeof(uint32_t) * fdk::kHistBins * batch, c->stream));
+    SelectBufs sb{};
+    rc = select_buffers(c, batch, cap, sb);
+    if (rc) return rc;
 
     fdk::PointsArgs a{};
     a.frames = dframes;
@@ -376,12 +419,17 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     a.list_resp = as<float>(c->list_resp);
     a.list_idx = as<uint32_t>(c->list_idx);
     a.list_cap = cap;
-    a.list_count = as<uint32_t>(c->list_count);
-    a.hist0 = as<uint32_t>(c->hist0);
+    a.list_count = sb.list_count;
+    a.hist0 = sb.hist0;
+    if (kind == FD_FAST && !g.empty) {
+        rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
+        if (rc) return rc;
+    }
+    key_map(kind, opts->min_valid_response, kind == FD_FAST && !g.empty ? &c->off : nullptr,
+            static_cast<int64_t>(rows - 6) * (cols - 6), a.key_base, a.key_lz);
+    c->sel_dirty = true;  // until k_select is enqueued: it resets the control block
     if (!g.empty) {
         if (kind == FD_FAST) {
-            rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
-            if (rc) return rc;
             if (pi.mask) {
                 if (rows > 4096) return fail(c, FD_ERR_INVALID, "FAST with prior features supports rows <= 4096");
                 FD_HIP_TRY(c, ensure(c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
@@ -430,6 +478,8 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     s.out_xy = dxy;
     s.out_stride = out_stride;
     s.out_counts = dcnt;
+    s.key_base = a.key_base;
+    s.key_lz = a.key_lz;
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
         FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 16 * batch));
@@ -437,16 +487,17 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
         s.stamps = as<uint64_t>(c->dbg);
     }
     FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
+    c->sel_dirty = false;
     if (stamps) {
         uint64_t h[16];
         FD_HIP_TRY(c, hipMemcpyAsync(h, c->dbg.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
-        std::fprintf(stderr, "k_select cycles: init %llu hist0 %llu gather %llu sort %llu greedy %llu descent %llu "
-                             "control %llu | chunks %llu descents %llu | extract %llu runsort %llu merges %llu place %llu cmask %llu\n",
+        std::fprintf(stderr, "k_select cycles: init %llu hist0 %llu gather %llu subkeys %llu greedy %llu descent %llu "
+                             "control %llu | chunks %llu descents %llu subchunks %llu | extract %llu runsort %llu merges %llu place %llu cmask %llu\n",
                      (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
                      (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
                      (unsigned long long)h[7], (unsigned long long)h[8], (unsigned long long)h[9],
-                     (unsigned long long)h[10], (unsigned long long)h[11], (unsigned long long)h[12],
+                     (unsigned long long)h[0], (unsigned long long)h[10], (unsigned long long)h[11], (unsigned long long)h[12],
                      (unsigned long long)h[13], (unsigned long long)h[14]);
     }
     if (!outputs_on_device) {
@@ -454,8 +505,14 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
                                      hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dcnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
-        for (int b = 0; b < batch; ++b)
+        for (int b = 0; b < batch; ++b) {
+            if (static_cast<uint32_t>(out_counts[b]) & 0xFE000000u)
+                return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (flags 0x" +
+                                               [](uint32_t v) { char t[16]; std::snprintf(t, sizeof t, "%x", v); return std::string(t); }(
+                                                   static_cast<uint32_t>(out_counts[b]) >> 25) +
+                                               ", frame " + std::to_string(b) + ")");
             if (out_counts[b] > out_stride) return fail(c, FD_ERR_CAPACITY, "out_stride smaller than the features found");
+        }
     } else if (!frames_on_device) {
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host frames must stay valid until copied
     }

@@ -1,0 +1,62 @@
+"""GPU: the selection kernel (SelectGoodFeatures, feature_point_detector.cpp:54-88) against the
+oracle's restatement across the regimes of its radix descent: no distance test, tiny and huge
+cells (LDS grid and global grid), needs that finish inside the first chunk and needs that are never
+reached (every candidate visited: many chunks and descents), batches of mixed frames, and repeated
+calls of different shapes and kinds (the kernel resets its own counters and histograms)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
+KIND = {"harris": 0, "shi_tomasi": 1, "fast": 2}
+
+
+@pytest.fixture(scope="module")
+def fd():
+    import feature_detector_amd as fd
+
+    fd.load()
+    return fd
+
+
+def _detect(fd, name, frames, need, dist):
+    res = fd.detect_points(name, frames, need, dist, THR[name])
+    return [res.features(i).copy() for i in range(frames.shape[0])]
+
+
+@pytest.mark.parametrize("dist,need", [(0, 50), (1, 500), (3, 200), (20, 200), (60, 100), (254, 10), (255, 10),
+                                       (20, 100000)])
+@pytest.mark.parametrize("name", ["harris", "shi_tomasi", "fast"])
+def test_select_regimes_against_oracle(fd, oracle, name, dist, need):
+    frames = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 300 + i, 240, 320) for i in range(3)])
+    got = _detect(fd, name, frames, need, dist)
+    for i, g in enumerate(got):
+        exp = oracle.detect(KIND[name], frames[i], dist, THR[name], need, sort_mode=1)[0]
+        np.testing.assert_array_equal(g, exp)
+
+
+@pytest.mark.parametrize("name", ["harris", "fast"])
+def test_batch1_720p(fd, oracle, name):
+    # FAST 720p noise consumes ~5k candidates: many sub-chunks of the first chunks
+    img = oracle.make_frame("noise", 77, 720, 1280)
+    got = _detect(fd, name, img[None], 200, 20)[0]
+    exp = oracle.detect(KIND[name], img, 20, THR[name], 200, sort_mode=1)[0]
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_repeated_calls_reset_state(fd, oracle):
+    a = oracle.make_frame("noise", 5, 200, 300)
+    b = oracle.make_frame("checker", 6, 333, 251)
+    for _ in range(3):
+        for name, img in (("harris", a), ("fast", b), ("shi_tomasi", a), ("harris", b)):
+            got = _detect(fd, name, img[None], 150, 7)[0]
+            exp = oracle.detect(KIND[name], img, 7, THR[name], 150, sort_mode=1)[0]
+            np.testing.assert_array_equal(got, exp)
+    # batch sizes changing between calls re-lay the control block; it must still read as zero
+    for bsz in (4, 1, 7, 2):
+        frames = np.stack([oracle.make_frame("noise", 40 + i, 120, 160) for i in range(bsz)])
+        got = _detect(fd, "harris", frames, 60, 5)
+        for i in range(bsz):
+            exp = oracle.detect(0, frames[i], 5, 30.0, 60, sort_mode=1)[0]
+            np.testing.assert_array_equal(got[i], exp)
