@@ -58,6 +58,7 @@ __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const Sel
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
 constexpr int kSubChunk = 512;  // keys sorted per greedy sub-chunk
+constexpr int kRegGather = 16;  // list responses per thread and round in the level-0 gather
 
 // One wave scans a sorted chunk in order (SelectGoodFeatures, feature_point_detector.cpp:62-72), a
 // batch of 64 candidates at a time: occupancy-grid test against earlier batches, then the batch is
@@ -270,11 +271,100 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     auto suf = [&](int lvl) -> uint32_t * { return lvl == 0 ? suf0 : sufl[lvl - 1]; };
 
     // Level-0 histogram: accumulated by the per-pixel kernel while it emitted the candidates.
+    // First round of the level-0 gather's list responses, in flight while the histogram is scanned.
+    float pre_r[kRegGather];
+#pragma unroll
+    for (int k = 0; k < kRegGather; ++k)
+        pre_r[k] = lresp[min(static_cast<uint32_t>(tid + k * nthr), static_cast<uint32_t>(n) - 1u)];
+
     for (int b = tid; b < kHistBins; b += nthr) suf0[b] = a.hist0[static_cast<int64_t>(f) * kHistBins + b];
     __syncthreads();
     FD_STAMP(1);
     suffix(suf0, kHistBins);
     FD_STAMP(2);
+
+    // Register-blocked gather of the keys whose 32-bit key lies in [k32lo, k32hi] (exact for chunks
+    // cut at 32-bit key boundaries, e.g. level-0 bins): each thread tests kRegGather responses per
+    // round, hits are placed by a block prefix and staged as (response, list index) in buf, then the
+    // staged entries fetch their pixel index densely into sup. `pre` = this thread's first round,
+    // already loaded. Sets gcount to the number of keys found.
+    auto gather_exact = [&](uint32_t k32lo, uint32_t k32hi, const float *pre) {
+        if (tid == 0) gcount = 0;
+        __syncthreads();
+        const uint32_t nn = static_cast<uint32_t>(n);  // list indices fit 32 bits (cap < 2^32)
+        const uint32_t step = static_cast<uint32_t>(nthr);
+        uint32_t staged = 0;  // uniform
+        auto round = [&](const float (&rr)[kRegGather], uint32_t base) {
+            uint32_t hm = 0;
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) {
+                const uint32_t k32 = map_key32(rr[k], a);
+                const bool hit = base + tid + k * step < nn && k32 >= k32lo && k32 <= k32hi;
+                hm |= static_cast<uint32_t>(hit) << k;
+            }
+            const uint32_t cntt = __popc(hm);
+            uint32_t incl = cntt;  // wave inclusive prefix
+            for (int o = 1; o < kWave; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o);
+                if (lane >= o) incl += t;
+            }
+            if (lane == kWave - 1) wtot[wave] = incl;
+            __syncthreads();
+            uint32_t before = staged, total = staged;
+            for (int q = 0; q < nthr / kWave; ++q) {
+                const uint32_t wq = wtot[q];
+                before += q < wave ? wq : 0u;
+                total += wq;
+            }
+            uint32_t pos = before + incl - cntt;
+            while (hm) {  // this thread's hits, in index order
+                const int k = __builtin_ctz(hm);
+                hm &= hm - 1u;
+                if (pos < static_cast<uint32_t>(kSelectChunk))
+                    buf[pos] = (static_cast<uint64_t>(__float_as_uint(rr[k])) << 32) | (base + tid + k * step);
+                ++pos;
+            }
+            staged = total;
+            __syncthreads();  // wtot reuse
+        };
+        uint32_t base = 0;
+        if (pre) {
+            float rr[kRegGather];
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) rr[k] = pre[k];
+            round(rr, 0);
+            base = kRegGather * step;
+        }
+        for (; base < nn; base += kRegGather * step) {
+            float rr[kRegGather];
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) rr[k] = lresp[min(base + tid + k * step, nn - 1u)];
+            round(rr, base);
+        }
+        if (tid == 0) gcount = staged;
+        const int ns = min(static_cast<int>(staged), kSelectChunk);
+        for (int j = tid; j < ns; j += nthr) {
+            const uint64_t e = buf[j];
+            const uint32_t li = lidx[static_cast<uint32_t>(e)];
+            sup[j] = make_key(__uint_as_float(static_cast<uint32_t>(e >> 32)), li, a);
+        }
+    };
+
+    // The first level-0 chunk (the loop's first cut: the highest bins holding <= kSelectChunk keys),
+    // gathered here so that the prefetched responses die before the sort and greedy code.
+    bool first_ready = false;
+    {
+        int lo_b = 0, hi_b = kHistBins;
+        while (lo_b < hi_b) {
+            const int mid = (lo_b + hi_b) >> 1;
+            if (suf0[mid] <= static_cast<uint32_t>(kSelectChunk)) hi_b = mid; else lo_b = mid + 1;
+        }
+        if (lo_b < kHistBins && suf0[lo_b] > 0) {
+            gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, pre_r);
+            first_ready = true;
+        }
+    }
+    FD_STAMP(3);
     int level = 0;
     int hi = (1 << lvl_width(0)) - 1;
     for (int64_t iter = 0;; ++iter) {
@@ -332,9 +422,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             const uint64_t klo = ((pre << w) | static_cast<uint64_t>(lo)) << rem;
             const uint64_t khi = (((pre << w) | static_cast<uint64_t>(hi)) << rem) | ((1ull << rem) - 1ull);
             const uint32_t k32lo = static_cast<uint32_t>(klo >> 32), k32hi = static_cast<uint32_t>(khi >> 32);
+            const bool k32_exact = rem >= 32;  // [klo, khi] == all keys whose top 32 bits are in [k32lo, k32hi]
             // gather the chunk: wave-uniform loop bounds, one LDS atomic per wave per round
             if (tid == 0) gcount = 0;
             __syncthreads();
+            if (first_ready && level == 0) {  // gathered before the loop (sup holds it)
+                first_ready = false;
+                if (tid == 0) gcount = cnt;
+            } else if (k32_exact) {
+                gather_exact(k32lo, k32hi, nullptr);            } else
             for (int64_t b0 = static_cast<int64_t>(wave) * kWave; b0 < n;
                  b0 += static_cast<int64_t>(kPassUnroll) * nthr) {
                 float r[kPassUnroll];
@@ -349,11 +445,13 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 for (int u = 0; u < kPassUnroll; ++u) {
                     const int64_t i = b0 + static_cast<int64_t>(u) * nthr + lane;
                     const uint32_t k32 = map_key32(r[u], a);
-                    const bool near = i < n && k32 >= k32lo && k32 <= k32hi;  // cheap 32-bit prefilter
-                    if (ballot(near) == 0ull) continue;
+                    const bool near = i < n && k32 >= k32lo && k32 <= k32hi;  // 32-bit prefilter
                     const uint64_t sk = make_key(r[u], ix[u], a);
-                    const bool hit = near && sk >= klo && sk <= khi;
-
+                    bool hit = near;
+                    if (!k32_exact) {  // chunk bounds inside the 32-bit key: full 64-bit test
+                        if (ballot(near) == 0ull) continue;
+                        hit = near && sk >= klo && sk <= khi;
+                    }
                     const uint64_t m = ballot(hit);
                     if (m) {
                         uint32_t off = 0;
@@ -401,21 +499,26 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     }
                     const uint64_t sklo = ((pre << w) | static_cast<uint64_t>(slo)) << rem;
                     const uint64_t skhi = (((pre << w) | static_cast<uint64_t>(shi)) << rem) | ((1ull << rem) - 1ull);
-                    if (tid == 0) gcount = 0;
-                    __syncthreads();
-                    for (int b0 = wave * kWave; b0 < static_cast<int>(cnt); b0 += nthr) {
-                        const int i = b0 + lane;
-                        const uint64_t sk = i < static_cast<int>(cnt) ? sup[i] : 0ull;
-                        const bool hit = i < static_cast<int>(cnt) && sk >= sklo && sk <= skhi;
-                        const uint64_t m = ballot(hit);
-                        if (m) {
-                            uint32_t off = 0;
-                            if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
-                            off = __builtin_amdgcn_readfirstlane(off);
-                            if (hit) buf[mbcnt64(m, off)] = sk;
+                    // the sub-chunk's unsorted keys: the whole chunk in place, or extracted into buf
+                    const bool whole = sc == cnt;
+                    uint64_t *unsorted = whole ? sup : buf;
+                    if (!whole) {
+                        if (tid == 0) gcount = 0;
+                        __syncthreads();
+                        for (int b0 = wave * kWave; b0 < static_cast<int>(cnt); b0 += nthr) {
+                            const int i = b0 + lane;
+                            const uint64_t sk = i < static_cast<int>(cnt) ? sup[i] : 0ull;
+                            const bool hit = i < static_cast<int>(cnt) && sk >= sklo && sk <= skhi;
+                            const uint64_t m = ballot(hit);
+                            if (m) {
+                                uint32_t off = 0;
+                                if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
+                                off = __builtin_amdgcn_readfirstlane(off);
+                                if (hit) buf[mbcnt64(m, off)] = sk;
+                            }
                         }
+                        __syncthreads();
                     }
-                    __syncthreads();
                     FD_STAMP(10);  // sub-chunk extract
                 {
                     // Merge sort of unique keys, descending: rank inside runs of 64 by counting larger
@@ -423,11 +526,11 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     // (its offset in its run) + (number of larger keys in the sibling run, by binary search).
                     const int c = static_cast<int>(sc);
                     const int c64 = (c + 63) & ~63;
-                    for (int i = c + tid; i < c64; i += nthr) buf[i] = 0ull;
+                    for (int i = c + tid; i < c64; i += nthr) unsorted[i] = 0ull;
                     __syncthreads();
                     for (int p = tid; p < c; p += nthr) {
-                        const uint64_t me = buf[p];
-                        const ulonglong2 *b2 = reinterpret_cast<const ulonglong2 *>(buf + (p & ~63));
+                        const uint64_t me = unsorted[p];
+                        const ulonglong2 *b2 = reinterpret_cast<const ulonglong2 *>(unsorted + (p & ~63));
                         int lr = 0;
     #pragma unroll 8
                         for (int j = 0; j < 32; ++j) {
@@ -461,29 +564,34 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     for (int i = tid; i < c; i += nthr) place(i, src[i]);
                     __syncthreads();
                     FD_STAMP(13);  // place
-                    // conflict masks: earlier candidates of the same 64-batch within distance d
+                    // conflict masks: earlier candidates of the same 64-batch within distance d. One work
+                    // item per (candidate, quarter of its batch): 16 entries each, no divergent trip
+                    // counts; each item writes its 16 bits of the candidate's 64-bit mask directly.
                     if (use_grid) {
-                        for (int p = tid; p < c; p += nthr) {
-                            const uint32_t e = pxy[p];
-                            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-                            uint64_t C = 0;
+                        uint16_t *cm16 = reinterpret_cast<uint16_t *>(buf);
+                        for (int item = tid; item < 4 * c; item += nthr) {
+                            const int p = item >> 2, q = item & 3;
                             const int bb = p & ~63, me = p - bb;
-                            const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb);  // broadcast reads
-                            const int n4 = (me + 3) >> 2;  // only earlier entries matter
-#pragma unroll 2
-                            for (int j4 = 0; j4 < n4; ++j4) {
-                                const uint4 e4 = q4[j4];
-                                const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
-                                uint32_t bits = 0;
+                            const uint32_t e = pxy[p];
+                            uint32_t bits = 0;
+                            if (e != kEmpty && 16 * q < me) {
+                                const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+                                const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb + 16 * q);  // broadcast
+                                const int lim = me - 16 * q;  // entries j < lim of this quarter are earlier
 #pragma unroll
-                                for (int t = 0; t < 4; ++t) {
-                                    const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
-                                    const bool nb = j4 * 4 + t < me && ev[t] != kEmpty && abs(x - ex) <= d && abs(y - ey) <= d;
-                                    bits |= static_cast<uint32_t>(nb) << t;
+                                for (int j4 = 0; j4 < 4; ++j4) {
+                                    const uint4 e4 = q4[j4];
+                                    const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                                    for (int t = 0; t < 4; ++t) {
+                                        const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
+                                        const bool nb = j4 * 4 + t < lim && ev[t] != kEmpty && abs(x - ex) <= d &&
+                                                        abs(y - ey) <= d;
+                                        bits |= static_cast<uint32_t>(nb) << (j4 * 4 + t);
+                                    }
                                 }
-                                C |= static_cast<uint64_t>(bits) << (j4 * 4);
                             }
-                            buf[p] = e == kEmpty ? 0ull : C;
+                            cm16[4 * p + q] = static_cast<uint16_t>(bits);
                         }
                     }
                 }
