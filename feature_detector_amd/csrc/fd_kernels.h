@@ -80,6 +80,11 @@ struct SelectArgs {
     // the possible response range over the full 32 bits (finer level-0 bins).
     uint32_t key_base;
     int key_lz;
+    // gather kernel (k_gather, batch x gather_groups workgroups) -> first level-0 chunk per frame;
+    // null pre_keys: k_select gathers it itself
+    uint64_t *pre_keys;   // [batch][kSelectChunk]
+    uint32_t *pre_count;  // [batch], reset by k_select
+    int gather_groups;
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 
@@ -114,7 +119,7 @@ hipError_t launch_fast_mask_scan(const uint32_t *mask, int mask_wpr, int batch, 
                                  int32_t *word_pref, hipStream_t s);
 hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s);
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s);
-hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);
+hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
 

@@ -36,7 +36,7 @@ struct fd_ctx {
     // selection control block: [batch][kHistBins] level-0 histograms, then list_count per frame.
     // Zero between calls: k_select resets what a call used. sel_dirty marks a call whose kernels may
     // not have run to the end (the next call clears the block first).
-    DevBuf selctl;
+    DevBuf selctl, pre_keys;
     bool sel_dirty = true;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts;
@@ -246,14 +246,16 @@ int64_t detect_list_cap(int kind, int rows, int cols) {
 }
 
 struct SelectBufs {
-    uint32_t *hist0, *list_count;
+    uint32_t *hist0, *list_count, *pre_count;
+    uint64_t *pre_keys;
 };
 
 // Candidate lists and the (self-resetting) control block for `batch` frames.
 int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
     FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
-    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 1);
+    FD_HIP_TRY(c, ensure(c->pre_keys, sizeof(uint64_t) * fdk::kSelectChunk * batch));
+    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 2);
     if (c->selctl.n < ctl) {
         FD_HIP_TRY(c, ensure(c->selctl, ctl));
         c->sel_dirty = true;
@@ -265,6 +267,8 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     uint32_t *base = as<uint32_t>(c->selctl);
     sb.hist0 = base;
     sb.list_count = base + static_cast<size_t>(batch) * fdk::kHistBins;
+    sb.pre_count = sb.list_count + batch;
+    sb.pre_keys = as<uint64_t>(c->pre_keys);
     return FD_OK;
 }
 
@@ -319,7 +323,7 @@ void fd_ctx_destroy(fd_ctx *c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf *bufs[] = {&c->frames,    &c->prior_xy,  &c->prior_frame, &c->prior_counts, &c->mask,       &c->row_base,
-                      &c->word_pref, &c->list_resp, &c->list_idx,  &c->selctl,      &c->out_xy,
+                      &c->word_pref, &c->list_resp, &c->list_idx,  &c->selctl,      &c->pre_keys,   &c->out_xy,
                       &c->out_counts, &c->grid,     &c->dbg,
                       &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
@@ -480,6 +484,14 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     s.out_counts = dcnt;
     s.key_base = a.key_base;
     s.key_lz = a.key_lz;
+    // Small batches of large frames: spread the first chunk's gather over ~256 workgroups in its own
+    // kernel (~9 us of fixed cost: pays off once one workgroup's pass over the list costs more, i.e.
+    // from about a megapixel per frame; measured at 640x480: break-even).
+    const bool big = static_cast<int64_t>(rows) * cols >= (1 << 20);
+    s.gather_groups = big ? std::max(1, std::min(64, 256 / std::max(batch, 1))) : 1;
+    if (const char *e = std::getenv("FD_GATHER_GROUPS")) s.gather_groups = std::max(1, std::atoi(e));  // A/B
+    s.pre_count = sb.pre_count;
+    s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
         FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 16 * batch));

@@ -273,9 +273,11 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // Level-0 histogram: accumulated by the per-pixel kernel while it emitted the candidates.
     // First round of the level-0 gather's list responses, in flight while the histogram is scanned.
     float pre_r[kRegGather];
+    if (!a.pre_keys) {
 #pragma unroll
-    for (int k = 0; k < kRegGather; ++k)
-        pre_r[k] = lresp[min(static_cast<uint32_t>(tid + k * nthr), static_cast<uint32_t>(n) - 1u)];
+        for (int k = 0; k < kRegGather; ++k)
+            pre_r[k] = lresp[min(static_cast<uint32_t>(tid + k * nthr), static_cast<uint32_t>(n) - 1u)];
+    }
 
     for (int b = tid; b < kHistBins; b += nthr) suf0[b] = a.hist0[static_cast<int64_t>(f) * kHistBins + b];
     __syncthreads();
@@ -360,7 +362,17 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             if (suf0[mid] <= static_cast<uint32_t>(kSelectChunk)) hi_b = mid; else lo_b = mid + 1;
         }
         if (lo_b < kHistBins && suf0[lo_b] > 0) {
-            gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, pre_r);
+            const uint32_t want = suf0[lo_b];
+            if (a.pre_keys && a.pre_count[f] == want) {  // k_gather's result (previous kernel)
+                const uint64_t *pk = a.pre_keys + static_cast<int64_t>(f) * kSelectChunk;
+                for (int i = tid; i < static_cast<int>(want); i += nthr) sup[i] = pk[i];
+                if (tid == 0) gcount = want;
+                __syncthreads();
+            } else {
+                if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
+                    atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x02000000u);
+                gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, a.pre_keys ? nullptr : pre_r);
+            }
             first_ready = true;
         }
     }
@@ -632,7 +644,112 @@ __device__ __forceinline__ void finish_frame(const SelectArgs &a, const int f) {
     uint32_t *h = a.hist0 + static_cast<int64_t>(f) * kHistBins;
     for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
         __hip_atomic_store(&h[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) __hip_atomic_store(&a.list_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&a.list_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.pre_count) __hip_atomic_store(&a.pre_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Gather kernel (small batches): G workgroups per frame each derive the frame's first level-0 chunk
+// (the highest bins holding <= kSelectChunk candidates) from the histogram and append the keys of
+// their slice of the list to pre_keys. k_select, the next kernel, reads them: the kernel boundary is
+// the visibility point, so no hand-off happens inside either kernel.
+__global__ __launch_bounds__(1024) void k_gather(SelectArgs a) {
+    __shared__ uint32_t S[kHistBins + 1];
+    __shared__ uint32_t wtot[16];
+    const int G = a.gather_groups;
+    const int f = blockIdx.x / G, g = blockIdx.x % G;
+    const int tid = threadIdx.x, nthr = blockDim.x, lane = lane_id(), wave = tid >> 6;
+    const int64_t n = min(static_cast<int64_t>(a.list_count[f]), a.list_cap);
+    const int64_t s0 = n * g / G, s1 = n * (g + 1) / G;
+    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    // this slice's responses, in flight during the histogram scan (slices <= kRegGather * nthr)
+    float rr[kRegGather];
+    const bool fits = s1 - s0 <= static_cast<int64_t>(kRegGather) * nthr;
+#pragma unroll
+    for (int k = 0; k < kRegGather; ++k)
+        rr[k] = (fits && s1 > s0) ? lresp[min(s0 + tid + static_cast<int64_t>(k) * nthr, s1 - 1)] : 0.0f;
+    const uint32_t *h0 = a.hist0 + static_cast<int64_t>(f) * kHistBins;
+    for (int b = tid; b < kHistBins; b += nthr) S[b] = h0[b];
+    __syncthreads();
+    {  // in-place suffix sums (4 bins per thread)
+        const int b0 = tid * 4;
+        uint32_t v[4], sacc = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sacc += (v[q] = S[b0 + q]);
+        uint32_t incl = sacc;
+        for (int o = 1; o < kWave; o <<= 1) {
+            const uint32_t t = __shfl_down(incl, o);
+            if (lane + o < kWave) incl += t;
+        }
+        if (lane == 0) wtot[wave] = incl;
+        __syncthreads();
+        uint32_t after = 0;
+        for (int q = wave + 1; q < nthr / kWave; ++q) after += wtot[q];
+        uint32_t run = incl - sacc + after;
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+            run += v[q];
+            S[b0 + q] = run;
+        }
+        if (tid == 0) S[kHistBins] = 0;
+        __syncthreads();
+    }
+    int lo = 0, hi = kHistBins;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (S[mid] <= static_cast<uint32_t>(kSelectChunk)) hi = mid; else lo = mid + 1;
+    }
+    if (lo >= kHistBins || S[lo] == 0) return;  // top bin alone exceeds a chunk (k_select descends)
+    const uint32_t k32lo = static_cast<uint32_t>(lo) << 20;
+    uint64_t *pk = a.pre_keys + static_cast<int64_t>(f) * kSelectChunk;
+    __shared__ uint32_t wg_base;
+    // One reservation per workgroup and round: hits counted per thread (bit mask), placed by a block
+    // prefix, then a single atomic on the frame's counter.
+    auto emit = [&](const float (&r)[kRegGather], int64_t base) {
+        uint32_t hm = 0;
+#pragma unroll
+        for (int k = 0; k < kRegGather; ++k) {
+            const int64_t i = base + tid + static_cast<int64_t>(k) * nthr;
+            hm |= static_cast<uint32_t>(i < s1 && map_key32(r[k], a) >= k32lo) << k;
+        }
+        const uint32_t cntt = __popc(hm);
+        uint32_t incl = cntt;
+        for (int o = 1; o < kWave; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if (lane >= o) incl += t;
+        }
+        if (lane == kWave - 1) wtot[wave] = incl;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (int q = 0; q < nthr / kWave; ++q) {
+            const uint32_t wq = wtot[q];
+            before += q < wave ? wq : 0u;
+            total += wq;
+        }
+        if (tid == 0) wg_base = total ? atomicAdd(&a.pre_count[f], total) : 0u;
+        __syncthreads();
+        uint32_t pos = wg_base + before + incl - cntt;
+        while (hm) {
+            const int k = __builtin_ctz(hm);
+            hm &= hm - 1u;
+            const int64_t i = base + tid + static_cast<int64_t>(k) * nthr;
+            if (pos < static_cast<uint32_t>(kSelectChunk)) pk[pos] = make_key(r[k], lidx[i], a);
+            ++pos;
+        }
+        __syncthreads();  // wtot / wg_base reuse
+    };
+    if (fits) {
+        emit(rr, s0);
+    } else {
+        for (int64_t base = s0; base < s1; base += static_cast<int64_t>(kRegGather) * nthr) {
+            float r2[kRegGather];
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) r2[k] = lresp[min(base + tid + static_cast<int64_t>(k) * nthr, s1 - 1)];
+            emit(r2, base);
+        }
+    }
 }
 
 __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
@@ -645,6 +762,11 @@ __global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
 }  // namespace
 
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
+    if (a.pre_keys) {
+        hipLaunchKernelGGL(k_gather, dim3(static_cast<unsigned>(batch * a.gather_groups)), dim3(1024), 0, s, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_select, dim3(static_cast<unsigned>(batch)), dim3(1024), 0, s, a);
     return hipGetLastError();
 }

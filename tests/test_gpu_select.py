@@ -60,3 +60,15 @@ def test_repeated_calls_reset_state(fd, oracle):
         for i in range(bsz):
             exp = oracle.detect(0, frames[i], 5, 30.0, 60, sort_mode=1)[0]
             np.testing.assert_array_equal(got[i], exp)
+
+
+@pytest.mark.parametrize("groups", ["1", "3", "64"])
+def test_gather_kernel_groups(fd, oracle, groups, monkeypatch):
+    # FD_GATHER_GROUPS=1: k_select gathers its first chunk itself; >1: k_gather (own kernel) does
+    monkeypatch.setenv("FD_GATHER_GROUPS", groups)
+    frames = np.stack([oracle.make_frame("noise", 90 + i, 240, 320) for i in range(2)])
+    for name in ("harris", "fast"):
+        got = _detect(fd, name, frames, 200, 20)
+        for i in range(2):
+            exp = oracle.detect(KIND[name], frames[i], 20, THR[name], 200, sort_mode=1)[0]
+            np.testing.assert_array_equal(got[i], exp)
