@@ -11,9 +11,10 @@ Multi-GPU (torchrun, one process per GPU): frames are independent, so every rank
 batch (weak scaling) with no collective on the data path; only the timing barrier / max-reduce uses
 the process group. value = pixels processed by all ranks / max-over-ranks time.
 
-Also reported: the roofline of the dominant kernel (HIP-event timed, algorithmic bytes = 1 B/px of
-frame input for the corner kernel), the north-star shape (Shi-Tomasi 1920x1080 batch 256), and the
-CPU baseline (the oracle restatement, single thread, bounded sample of the same workload).
+Also reported: the roofline of the per-pixel kernel (HIP-event timed, algorithmic bytes = 1 B/px of
+frame input; traffic = measured FETCH_SIZE from profiles/r01_traffic.json), the north-star shape
+(Shi-Tomasi 1920x1080 batch 256), and the CPU baseline (the oracle restatement on a bounded sample of
+the same workload: single thread, and a pool of up to 16 threads).
 """
 from __future__ import annotations
 
@@ -29,6 +30,30 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
+# HBM traffic per launch measured with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) and
+# corrected by the calibrated gfx950 factor (tools/gpu_traffic.sh, tools/calib/fetch_calib.hip).
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic.json")
+VALU_FILE = "profiles/r01_k1_northstar_st_pmc_sq.csv"
+
+
+def measured_traffic(key):
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            t = json.load(fh)
+        return int(t[key]["read_bytes_corrected"]), os.path.relpath(TRAFFIC_FILE, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 KIND = {"harris": 0, "shi_tomasi": 1, "fast": 2}
 THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 
@@ -104,17 +129,48 @@ def timed_graph(torch, fn, steps, warmup, use_graph, per_graph, barrier=None):
 
 
 def kernel_time_ms(torch, fd, frames_pool, kind, thr, reps=50):
-    """Average duration of the per-pixel kernel alone (fd_points_response), HIP events on the
-    stream it is launched on (torch's current stream, which the library context follows)."""
+    """Average duration of the per-pixel kernel alone, HIP events on the stream it is launched on
+    (torch's current stream, which the library context follows).
+
+    A launch of a small frame batch is shorter than the host's per-call overhead, so back-to-back
+    calls would time the host. When the output lists fit, the reps are fd_points_response_append
+    calls (the kernel alone, no count reset; each rep appends after the previous) captured in one
+    HIP graph and replayed between the events. Otherwise (the north-star batch, ~0.7 ms a launch)
+    plain fd_points_response calls, whose 1-word count memset is noise at that size.
+    """
     b, r, c = frames_pool[0].shape
-    cap = r * c if kind == "fast" else r * c // 2 + 64
+    base = r * c if kind == "fast" else r * c // 2 + 64
     dev = frames_pool[0].device
+    graph = b * base * (reps + 3) * 8 <= (1 << 30)
+    cap = base * (reps + 3) if graph else base
     out = (torch.empty((b, cap), dtype=torch.float32, device=dev), torch.empty((b, cap), dtype=torch.int32, device=dev),
            torch.empty((b,), dtype=torch.int32, device=dev))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            out[2].zero_()
+            for i in range(3):
+                fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=out, append=True)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(reps):
+                fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=out, append=True)
+        out[2].zero_()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        del g
+        return ms
     for i in range(3):
         fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=out)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for i in range(reps):
         fd.point_response(kind, frames_pool[i % len(frames_pool)], thr, out=out)
@@ -175,7 +231,7 @@ def main():
     k_ms = kernel_time_ms(torch, fd, pool, args.detector, THR[args.detector])
     k_bytes = px_step  # algorithmic: 1 B/px frame read
     kernels = {"corner_or_fast_ms": k_ms, "step_ms": ms_per_step}
-    # the remainder of a step is the per-frame selection (one workgroup per frame) and its memset
+    # the remainder of a step is the per-frame selection (one workgroup per frame)
     sel_ms = max(ms_per_step - k_ms, 0.0)
     kernels["select_and_rest_ms"] = sel_ms
     dominant = "k_corner" if args.detector != "fast" else "k_fast"
@@ -185,9 +241,15 @@ def main():
     else:
         dominant_note = f"{dominant} dominates the step"
     achieved = k_bytes / (k_ms * 1e-3) / 1e9
+    traffic, traffic_src = (measured_traffic("bench_k_corner") if (args.detector == "harris" and args.rows == 480
+                                                                     and args.cols == 640 and args.batch == 1)
+                            else (None, None))
     roofline = {"kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "bytes_per_launch": k_bytes, "avg_launch_ms": round(k_ms, 5), "note": dominant_note}
+    if traffic_src:
+        roofline["traffic_source"] = (traffic_src + ": FETCH_SIZE x calibrated 2.0; at batch 1 short tiles re-read "
+                                      "their halo rows and the level-0 histogram atomics are memory-side")
     del pool
 
     out = {
@@ -218,7 +280,10 @@ def main():
             "kernel": "k_corner<ShiTomasi>", "kernel_ms": round(kms, 4),
             "kernel_mpix_s": round(kb / (kms * 1e-3) / 1e6, 1),
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb},
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb,
+                         "traffic": measured_traffic("northstar_k_corner")[0]},
+            "valu_bound": ("~90% VALU busy (SQ_ACTIVE_INST_VALU vs SIMD issue capacity; " + VALU_FILE + "): "
+                           "~40 VALU lane-instr/px, so VALU issue, not HBM, bounds this kernel (DESIGN.md)"),
         }
         del pool2
 
@@ -237,7 +302,22 @@ def main():
             "value": round(n * args.rows * args.cols / el / 1e6, 3), "unit": "Mpix/s", "cores": 1, "kind": "port",
             "sample": f"{n} frames of the same workload ({args.detector}, {args.cols}x{args.rows}, dist {args.dist}, "
                       f"need {args.need}) through oracle.detect (full DetectGoodFeatures restatement), "
-                      f"{el:.1f} s, 1 thread, host {os.cpu_count()} logical CPUs visible",
+                      f"{el:.1f} s, 1 thread, host {os.cpu_count()} logical CPUs visible ({cpu_model()})",
+        }
+        # a pool of workers, one frame each at a time (ctypes releases the GIL)
+        from concurrent.futures import ThreadPoolExecutor
+
+        workers = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+        per_worker = max(1, n // 2)
+        t1 = time.perf_counter()
+        with ThreadPoolExecutor(workers) as ex:
+            list(ex.map(lambda i: O.detect(KIND[args.detector], frames[i % len(frames)], args.dist,
+                                           THR[args.detector], args.need), range(per_worker * workers)))
+        el2 = time.perf_counter() - t1
+        out["cpu_baseline_pool"] = {
+            "value": round(per_worker * workers * args.rows * args.cols / el2 / 1e6, 3), "unit": "Mpix/s",
+            "cores": workers, "kind": "port",
+            "sample": f"{per_worker * workers} frames over a pool of {workers} threads, {el2:.1f} s ({cpu_model()})",
         }
     if rank == 0:
         print(json.dumps(out), flush=True)

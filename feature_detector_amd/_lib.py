@@ -17,6 +17,7 @@ EXPORTS = (
     "fd_ctx_create", "fd_ctx_destroy", "fd_last_error", "fd_ctx_set_stream", "fd_ctx_use_own_stream",
     "fd_ctx_get_stream",
     "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_points_detect", "fd_points_candidates", "fd_points_response",
+    "fd_points_response_append",
     "fd_lsd_map",
     "fd_build_info",
 )
@@ -67,6 +68,7 @@ def load() -> ctypes.CDLL:
         "fd_points_candidates": (i32, [P, i32, P, i32, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, P, P, P,
                                        i64, P, P, i32]),
         "fd_points_response": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
+        "fd_points_response_append": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
         "fd_lsd_map": (i32, [P, P, i32, i32, i32, i32, f32, P, P, P, P, i64, P, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
     }

@@ -95,7 +95,7 @@ int choose_tile_h(int64_t batch, int tiles_x, int out_rows, int period, int max_
     if (const char *e = std::getenv("FD_TARGET_WAVES")) target_waves = std::max<int64_t>(1, std::atoll(e));  // tuning
     if (const char *e = std::getenv("FD_TILE_MULT")) max_mult = std::max(1, std::atoi(e));                   // tuning
     int64_t h = (batch * tiles_x * static_cast<int64_t>(out_rows)) / target_waves;
-    h = std::max<int64_t>(h, 2 * period);
+    h = std::max<int64_t>(h, period);  // small batches: short tiles, more single-wave SIMDs busy
     h = ((h + period - 1) / period) * period;
     h = std::min<int64_t>(h, static_cast<int64_t>(period) * max_mult);
     return static_cast<int>(h);
@@ -531,16 +531,16 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     return FD_OK;
 }
 
-int fd_points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,
-                       const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
-                       uint32_t *out_counts) {
+static int points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,
+                           const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
+                           uint32_t *out_counts, bool reset_counts) {
     int rc = check_shape(c, kind, batch, rows, cols);
     if (rc) return rc;
     if (!opts || !frames || !out_resp || !out_idx || !out_counts || cand_cap < 1)
         return fail(c, FD_ERR_INVALID, "bad arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const PointGeom g = point_geom(kind, batch, rows, cols);
-    FD_HIP_TRY(c, hipMemsetAsync(out_counts, 0, sizeof(uint32_t) * batch, c->stream));
+    if (reset_counts) FD_HIP_TRY(c, hipMemsetAsync(out_counts, 0, sizeof(uint32_t) * batch, c->stream));
     if (g.empty) return FD_OK;
     fdk::PointsArgs a{};
     a.frames = frames;
@@ -565,6 +565,18 @@ int fd_points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, in
         FD_HIP_TRY(c, fdk::launch_corner(kind, false, a, c->stream));
     }
     return FD_OK;
+}
+
+int fd_points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,
+                       const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
+                       uint32_t *out_counts) {
+    return points_response(c, kind, frames, batch, rows, cols, opts, out_resp, out_idx, cand_cap, out_counts, true);
+}
+
+int fd_points_response_append(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,
+                              const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
+                              uint32_t *out_counts) {
+    return points_response(c, kind, frames, batch, rows, cols, opts, out_resp, out_idx, cand_cap, out_counts, false);
 }
 
 int fd_points_candidates(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_device, int batch, int rows,

@@ -169,11 +169,14 @@ def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_v
     return DetectResult(xy, cnt)
 
 
-def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx: Context | None = None):
+def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx: Context | None = None,
+                   append: bool = False):
     """The per-pixel stage alone (fd_points_response) on torch device frames [B, R, C].
 
     Returns (resp, idx, counts): resp float32 [B, cap], idx int32 [B, cap] (raster index), in
-    unspecified order, counts int32 [B]. Asynchronous on torch's current stream.
+    unspecified order, counts int32 [B]. Asynchronous on torch's current stream. append=True
+    (fd_points_response_append, needs out=) keeps the counts in out and appends after them, so the
+    call is the per-pixel kernel alone (no count reset).
     """
     import torch
 
@@ -191,10 +194,14 @@ def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx:
     else:
         resp, idx, counts = out
         cap = resp.shape[1]
+    if append and out is None:
+        raise ValueError("append=True needs out=(resp, idx, counts)")
     opts = fd_point_opts(15, float(min_valid_response))
-    rc = _lib.load().fd_points_response(ctx.ptr, kind, ctypes.c_void_p(ptr), b, r, c, ctypes.byref(opts),
-                                        ctypes.c_void_p(resp.data_ptr()), ctypes.c_void_p(idx.data_ptr()), int(cap),
-                                        ctypes.c_void_p(counts.data_ptr()))
+    L = _lib.load()
+    fn = L.fd_points_response_append if append else L.fd_points_response
+    rc = fn(ctx.ptr, kind, ctypes.c_void_p(ptr), b, r, c, ctypes.byref(opts),
+            ctypes.c_void_p(resp.data_ptr()), ctypes.c_void_p(idx.data_ptr()), int(cap),
+            ctypes.c_void_p(counts.data_ptr()))
     _lib.check(ctx.ptr, rc)
     del keep
     return resp, idx, counts

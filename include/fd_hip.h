@@ -112,6 +112,16 @@ int fd_points_response(fd_ctx *ctx, int kind, const uint8_t *frames, int batch, 
                        const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
                        uint32_t *out_counts);
 
+/*
+ * fd_points_response_append -- fd_points_response without resetting out_counts: each frame's
+ * candidates are appended after the out_counts[b] entries already there (slots past cand_cap are
+ * counted but not written). A launch is then the corner/segment-test kernel alone, so a caller can
+ * issue many back to back (or capture them in a HIP graph) to time the kernel by itself.
+ */
+int fd_points_response_append(fd_ctx *ctx, int kind, const uint8_t *frames, int batch, int rows, int cols,
+                              const fd_point_opts *opts, float *out_resp, uint32_t *out_idx, int64_t cand_cap,
+                              uint32_t *out_counts);
+
 /* ---- LSD level-line map ------------------------------------------------------------------------ */
 /*
  * fd_lsd_map -- FeatureLineDetector::ComputeLineLevelAngleMap (feature_line_detector.cpp:56-97).

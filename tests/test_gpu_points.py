@@ -219,3 +219,36 @@ def test_device_tensor_path_matches_host(fd, oracle):
         assert np.array_equal(dres.counts.cpu().numpy(), hres.counts)
         for b in range(3):
             assert np.array_equal(dres.features(b), hres.features(b))
+
+
+@pytest.mark.parametrize("name", ["harris", "shi_tomasi", "fast"])
+def test_point_response_and_append(fd, oracle, name):
+    """fd_points_response (unordered candidates) equals the oracle's candidate set; the append
+    variant (no count reset) adds a second copy after the first."""
+    torch = pytest.importorskip("torch")
+    frames = np.stack([oracle.make_frame(p, s, 240, 320) for p, s in (("noise", 5), ("checker", 6))])
+    dev = torch.from_numpy(frames).cuda()
+    resp, idx, cnt = fd.point_response(name, dev, THR[name])
+    torch.cuda.synchronize()
+    cnt = cnt.cpu().numpy()
+    cap = resp.shape[1]
+    for b in range(2):
+        er, ex, ey = oracle_candidates(oracle, name, frames[b], THR[name])
+        gi = idx[b, :cnt[b]].cpu().numpy()
+        gr = resp[b, :cnt[b]].cpu().numpy()
+        order = np.argsort(gi, kind="stable")
+        assert np.array_equal(gi[order], ey.astype(np.int64) * 320 + ex)
+        assert np.array_equal(gr[order].view(np.uint32), er.view(np.uint32))
+    big = (torch.empty((2, 2 * cap), dtype=torch.float32, device="cuda"),
+           torch.empty((2, 2 * cap), dtype=torch.int32, device="cuda"),
+           torch.zeros((2,), dtype=torch.int32, device="cuda"))
+    fd.point_response(name, dev, THR[name], out=big, append=True)
+    fd.point_response(name, dev, THR[name], out=big, append=True)
+    torch.cuda.synchronize()
+    c2 = big[2].cpu().numpy()
+    assert np.array_equal(c2, 2 * cnt)
+    for b in range(2):
+        gi = np.sort(big[1][b, :c2[b]].cpu().numpy())
+        assert np.array_equal(gi[0::2], gi[1::2])
+    with pytest.raises(ValueError):
+        fd.point_response(name, dev, THR[name], append=True)
