@@ -112,6 +112,17 @@ struct LsdArgs {
     int64_t *counts;
 };
 
+struct BriefArgs {
+    const uint8_t *frames;
+    int batch, rows, cols;
+    const float *uv;        // [batch][stride][2] (x, y)
+    const int32_t *counts;  // [batch] or null (= stride)
+    int stride;
+    int length, half, sampler;
+    uint32_t *out_bits;  // [batch][stride][ceil(length / 32)]
+    uint8_t *out_valid;  // [batch][stride] or null
+};
+
 // Launchers (stream-ordered, no allocation, no synchronisation: graph-capturable).
 hipError_t launch_mask_boxes(const float *prior_xy, const int32_t *prior_frame, int n_prior, int dist, int rows,
                              int cols, uint32_t *mask, int mask_wpr, hipStream_t s);
@@ -122,5 +133,6 @@ hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off,
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
+hipError_t launch_brief(const BriefArgs &a, hipStream_t s);
 
 }  // namespace fdk

@@ -40,6 +40,7 @@ struct fd_ctx {
     bool sel_dirty = true;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts;
+    DevBuf b_uv, b_counts, b_bits, b_valid;
     DevBuf dbg;
     // FAST offset table cache
     int64_t off_n = -1;
@@ -327,7 +328,7 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->out_counts, &c->grid,     &c->dbg,
                       &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
-                      &c->l_idx,    &c->l_counts};
+                      &c->l_idx,    &c->l_counts, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid};
     for (DevBuf *b : bufs) release(*b);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -782,6 +783,76 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
             if (valid_counts[b] > idx_cap) return fail(c, FD_ERR_CAPACITY, "idx_cap smaller than the valid pixels");
     } else if (!frames_on_device) {
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    return FD_OK;
+}
+
+int fd_brief_compute(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
+                     const fd_brief_opts *opts, const float *uv, const int32_t *counts, int32_t stride,
+                     uint32_t *out_bits, uint8_t *out_valid, int io_on_device) {
+    int rc = check_shape(c, FD_HARRIS, batch, rows, cols, false);
+    if (rc) return rc;
+    if (!opts || !uv || !out_bits || stride < 0) return fail(c, FD_ERR_INVALID, "bad arguments");
+    // pattern_idx_ holds 256 pairs (descriptor_brief.h:36): a longer kLength would read past it
+    if (opts->length < 1 || opts->length > 256) return fail(c, FD_ERR_INVALID, "length must be in [1, 256]");
+    if (opts->half_patch_size < 0 || opts->half_patch_size > 255)
+        return fail(c, FD_ERR_INVALID, "half_patch_size must be in [0, 255]");
+    if (opts->sampler != FD_SAMPLE_BILINEAR && opts->sampler != FD_SAMPLE_TRUNCATE)
+        return fail(c, FD_ERR_INVALID, "unknown sampler");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    if (stride == 0) return FD_OK;
+    const uint8_t *dframes = nullptr;
+    rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
+    if (rc) return rc;
+    const size_t slots = static_cast<size_t>(batch) * stride;
+    const int nw = (opts->length + 31) / 32;
+    fdk::BriefArgs a{};
+    a.frames = dframes;
+    a.batch = batch;
+    a.rows = rows;
+    a.cols = cols;
+    a.stride = stride;
+    a.length = opts->length;
+    a.half = opts->half_patch_size;
+    a.sampler = opts->sampler;
+    if (io_on_device) {
+        a.uv = uv;
+        a.counts = counts;
+        a.out_bits = out_bits;
+        a.out_valid = out_valid;
+    } else {
+        FD_HIP_TRY(c, ensure(c->b_uv, sizeof(float) * 2 * slots));
+        FD_HIP_TRY(c, ensure(c->b_bits, sizeof(uint32_t) * nw * slots));
+        FD_HIP_TRY(c, hipMemcpyAsync(c->b_uv.p, uv, sizeof(float) * 2 * slots, hipMemcpyHostToDevice, c->stream));
+        a.uv = as<float>(c->b_uv);
+        a.out_bits = as<uint32_t>(c->b_bits);
+        if (counts) {
+            FD_HIP_TRY(c, ensure(c->b_counts, sizeof(int32_t) * batch));
+            FD_HIP_TRY(c, hipMemcpyAsync(c->b_counts.p, counts, sizeof(int32_t) * batch, hipMemcpyHostToDevice,
+                                         c->stream));
+            a.counts = as<int32_t>(c->b_counts);
+        }
+        if (out_valid) {
+            FD_HIP_TRY(c, ensure(c->b_valid, slots));
+            a.out_valid = as<uint8_t>(c->b_valid);
+        }
+    }
+    FD_HIP_TRY(c, fdk::launch_brief(a, c->stream));
+    if (!io_on_device) {
+        // Slots past counts[b] are not written by the kernel; copy back only the written prefix of each
+        // frame so the caller's buffer keeps its contents there, as the device path does.
+        for (int b = 0; b < batch; ++b) {
+            const int n = counts ? std::min<int64_t>(static_cast<uint32_t>(counts[b]) & 0x01FFFFFFu, stride) : stride;
+            if (n <= 0) continue;
+            const size_t s0 = static_cast<size_t>(b) * stride;
+            FD_HIP_TRY(c, hipMemcpyAsync(out_bits + s0 * nw, a.out_bits + s0 * nw, sizeof(uint32_t) * nw * n,
+                                         hipMemcpyDeviceToHost, c->stream));
+            if (out_valid)
+                FD_HIP_TRY(c, hipMemcpyAsync(out_valid + s0, a.out_valid + s0, n, hipMemcpyDeviceToHost, c->stream));
+        }
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    } else if (!frames_on_device) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host frames must stay valid until copied
     }
     return FD_OK;
 }

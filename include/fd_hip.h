@@ -138,6 +138,32 @@ int fd_lsd_map(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int bat
                float *norm, float *angle, uint8_t *valid, int32_t *valid_idx, int64_t idx_cap, int64_t *valid_counts,
                int outputs_on_device);
 
+/* ---- steered BRIEF descriptor ------------------------------------------------------------------- */
+/* BriefDescriptor::Options (descriptor_brief.h:17-20) plus the float-coordinate sampler of the
+ * un-vendored GrayImage (descriptor_brief.cpp:24,42-43; see DESIGN.md: parity unpinned). */
+enum fd_sampler { FD_SAMPLE_BILINEAR = 0, FD_SAMPLE_TRUNCATE = 1 };
+typedef struct fd_brief_opts {
+    int32_t length;          /* kLength, bits per descriptor, 1..256 (default 256) */
+    int32_t half_patch_size; /* kHalfPatchSize, moment patch half size, 0..255 (default 8) */
+    int32_t sampler;         /* enum fd_sampler */
+} fd_brief_opts;
+
+/*
+ * fd_brief_compute -- Descriptor<BriefType>::Compute (descriptor.h:27-40) with
+ * BriefDescriptor::ComputeForOneFeature (descriptor_brief.cpp:8-50) per keypoint, for a batch of frames.
+ * uv: [batch][stride][2] float (x = col, y = row), the layout fd_points_detect writes, so a device-side
+ * detect -> describe chain needs no host round trip. counts: keypoints per frame (int32 [batch]; NULL =
+ * stride each; bits 25..31 are ignored, so fd_points_detect's device counts can be passed as they are).
+ * out_bits: [batch][stride][ceil(length/32)] uint32, descriptor bit i = bit (i % 32) of word i / 32
+ * (bit i set <=> I(p1_i) < I(p2_i), descriptor_brief.cpp:44-46); keypoints outside the border
+ * (:13-17) or with zero moment (:30) get all-zero words and out_valid 0 (NULL to skip out_valid).
+ * Slots k >= counts[b] are not written. uv, counts, out_bits and out_valid are all device pointers
+ * when io_on_device, all host pointers otherwise.
+ */
+int fd_brief_compute(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
+                     const fd_brief_opts *opts, const float *uv, const int32_t *counts, int32_t stride,
+                     uint32_t *out_bits, uint8_t *out_valid, int io_on_device);
+
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);
 

@@ -393,6 +393,82 @@ uint32_t orc_lsd_min_region_size(int rows, int cols, float tol_rad) {
     return static_cast<uint32_t>(-log_nt / std::log10(p));
 }
 
+// -----------------------------------------------------------------------------------------------------
+// Steered BRIEF, BriefDescriptor::ComputeForOneFeature (feature_descriptor/descriptor_brief.cpp:8-50),
+// looped over keypoints as Descriptor<BriefType>::Compute (descriptor.h:27-40).
+// pattern: the reference's pattern_idx_ (descriptor_brief.cpp:52-309) as int16[4 * 256]
+// (dcol1, drow1, dcol2, drow2), passed in by the caller.
+// sampler: GrayImage::GetPixelValueNoCheck(float row, float col) is un-vendored Slam_Utility code
+// (parity unpinned): 0 = bilinear ((1-ex)(1-ey), ex(1-ey), (1-ex)ey, ex*ey, summed left to right),
+// 1 = truncation. Reads use the row-major linear index row * cols + col like the NoCheck accessor;
+// an index outside the frame reads 0 (the reference would read out of bounds).
+// kZeroFloat (slam_basic_math.h, un-vendored) = 1e-6f: only |m| in (0, 1) could depend on it, which
+// integer keypoints never produce.
+// out_bits: n x ceil(length/32) words, bit i of the descriptor = bit i%32 of word i/32.
+// out_valid (may be NULL): ComputeForOneFeature's return value. out_m (may be NULL): m10, m01, m.
+// -----------------------------------------------------------------------------------------------------
+static float BriefPixel(const uint8_t *img, int rows, int cols, int32_t r, int32_t c) {
+    const int64_t idx = static_cast<int64_t>(r) * cols + c;
+    if (idx < 0 || idx >= static_cast<int64_t>(rows) * cols) return 0.0f;
+    return static_cast<float>(img[idx]);
+}
+
+static float BriefSample(const uint8_t *img, int rows, int cols, float row, float col, int sampler) {
+    const int32_t r0 = static_cast<int32_t>(row);
+    const int32_t c0 = static_cast<int32_t>(col);
+    if (sampler == 1) return BriefPixel(img, rows, cols, r0, c0);
+    const float ex = col - static_cast<float>(c0);
+    const float ey = row - static_cast<float>(r0);
+    const float ex1 = 1.0f - ex;
+    const float ey1 = 1.0f - ey;
+    return ex1 * ey1 * BriefPixel(img, rows, cols, r0, c0) + ex * ey1 * BriefPixel(img, rows, cols, r0, c0 + 1) +
+           ex1 * ey * BriefPixel(img, rows, cols, r0 + 1, c0) + ex * ey * BriefPixel(img, rows, cols, r0 + 1, c0 + 1);
+}
+
+void orc_brief(const uint8_t *img, int rows, int cols, const float *uv, int n, int length, int half, int sampler,
+               const int16_t *pattern, uint32_t *out_bits, uint8_t *out_valid, float *out_m) {
+    const int nw = (length + 31) / 32;
+    for (int k = 0; k < n; ++k) {
+        uint32_t *bits = out_bits + static_cast<size_t>(k) * nw;
+        for (int j = 0; j < nw; ++j) bits[j] = 0;  // :10 descriptor.assign(kLength, 0)
+        if (out_valid) out_valid[k] = 0;
+        if (out_m) out_m[3 * k] = out_m[3 * k + 1] = out_m[3 * k + 2] = 0.0f;
+        const float x = uv[2 * k], y = uv[2 * k + 1];
+        constexpr float kPatternMaxBound = 19.0f;  // :13
+        const float max_bound = std::max(kPatternMaxBound, static_cast<float>(half) * 2.0f);  // :14
+        if (x < max_bound || x > cols - max_bound || y < max_bound || y > rows - max_bound) continue;  // :15-17
+        if (x != x || y != y) continue;  // NaN: outside (the reference would read arbitrary memory)
+        float m01 = 0.0f;  // :20-28
+        float m10 = 0.0f;
+        for (int32_t dx = -half; dx <= half; ++dx) {
+            for (int32_t dy = -half; dy <= half; ++dy) {
+                const float value = BriefSample(img, rows, cols, y + dy, x + dx, sampler);
+                m10 += dx * value;
+                m01 += dy * value;
+            }
+        }
+        const float m = std::sqrt(m01 * m01 + m10 * m10);  // :29
+        if (out_m) {
+            out_m[3 * k] = m10;
+            out_m[3 * k + 1] = m01;
+            out_m[3 * k + 2] = m;
+        }
+        if (m < 1e-6f) continue;  // :30
+        const float sin_theta = m01 / m;  // :32-35
+        const float cos_theta = m10 / m;
+        const float r00 = cos_theta, r01 = -sin_theta, r10 = sin_theta, r11 = cos_theta;
+        for (int32_t i = 0; i < length; ++i) {  // :38-47
+            const float ax = pattern[4 * i], ay = pattern[4 * i + 1], bx = pattern[4 * i + 2], by = pattern[4 * i + 3];
+            const float p1x = r00 * ax + r01 * ay + x, p1y = r10 * ax + r11 * ay + y;
+            const float p2x = r00 * bx + r01 * by + x, p2y = r10 * bx + r11 * by + y;
+            const float value_1 = BriefSample(img, rows, cols, p1y, p1x, sampler);
+            const float value_2 = BriefSample(img, rows, cols, p2y, p2x, sampler);
+            if (value_1 < value_2) bits[i >> 5] |= 1u << (i & 31);
+        }
+        if (out_valid) out_valid[k] = 1;
+    }
+}
+
 }  // extern "C"
 
 #include <random>

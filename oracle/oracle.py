@@ -49,6 +49,7 @@ def lib():
             "orc_lsd_sort": (None, [_P, _P, i64, i32]),
             "orc_lsd_min_region_size": (u32, [i32, i32, f32]),
             "orc_make_frame": (None, [i32, u32, i32, i32, i32, _P]),
+            "orc_brief": (None, [_P, i32, i32, _P, i32, i32, i32, i32, _P, _P, _P, _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -166,3 +167,37 @@ def lsd_sort(norm, idx, sort_mode=0):
 
 def lsd_min_region_size(rows, cols, tol_rad=22.5 * 3.14159265358979323846 / 180.0):
     return int(lib().orc_lsd_min_region_size(rows, cols, np.float32(tol_rad)))
+
+
+# ------------------------------------------------------------------------------------- BRIEF (f1)
+PATTERN_INC = os.path.join(HERE, "..", "feature_detector_amd", "csrc", "fd_brief_pattern.inc")
+
+
+def brief_pattern() -> np.ndarray:
+    """pattern_idx_ (descriptor_brief.cpp:52-309) as int16[1024], from the generated table
+    (tools/gen_brief_pattern.py; tests/test_brief_host.py checks it against the reference source)."""
+    import re
+
+    words = [int(t, 16) for t in re.findall(r"0x[0-9a-fA-F]{8}", open(PATTERN_INC).read())]
+    assert len(words) == 256
+    b = np.array(words, np.uint32).view(np.uint8).reshape(256, 4).view(np.int8)
+    return b.astype(np.int16).reshape(-1)
+
+
+def brief(img, uv, length=256, half=8, sampler=0):
+    """BriefDescriptor::ComputeForOneFeature (descriptor_brief.cpp:8-50) per keypoint.
+
+    Returns (bits uint32 [n, ceil(length/32)], valid uint8 [n], moments float32 [n, 3] = m10, m01, m).
+    sampler 0 = bilinear, 1 = truncation (the reference's float sampler is un-vendored: unpinned)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    R, C = img.shape
+    uv = np.ascontiguousarray(np.asarray(uv, np.float32).reshape(-1, 2))
+    n = len(uv)
+    nw = (length + 31) // 32
+    bits = np.zeros((max(n, 1), nw), np.uint32)
+    valid = np.zeros(max(n, 1), np.uint8)
+    mom = np.zeros((max(n, 1), 3), np.float32)
+    pat = brief_pattern()
+    lib().orc_brief(_ptr(img), R, C, _ptr(uv), n, length, half, sampler, _ptr(pat), _ptr(bits), _ptr(valid),
+                    _ptr(mom))
+    return bits[:n], valid[:n], mom[:n]
