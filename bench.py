@@ -73,6 +73,7 @@ def parse():
     p.add_argument("--pattern", default="noise", choices=["noise", "checker"])
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-north-star", action="store_true")
+    p.add_argument("--no-config3", action="store_true", help="skip the FAST + BRIEF (configs[2]) leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
@@ -196,6 +197,48 @@ def run_config(torch, fd, dev, detector, rows, cols, batch, pool, need, dist, pa
     return secs, done, frames_pool, (xy, cnt)
 
 
+def run_config3(torch, fd, dev, seed, batch=64, rows=720, cols=1280, need=200, dist=20, steps=20, reps=20):
+    """FAST-12 (thr 10) + greedy selection + steered BRIEF-256 on the selected keypoints, all on the
+    device: the detector writes keypoints/counts, the descriptor kernel reads them in place."""
+    pool = [make_frames(torch, "noise", batch, rows, cols, seed + 7919 * i, dev) for i in range(2)]
+    stride = need + 1
+    xy = torch.empty((batch, stride, 2), dtype=torch.float32, device=dev)
+    cnt = torch.empty((batch,), dtype=torch.int32, device=dev)
+    bits = torch.empty((batch, stride, 8), dtype=torch.int32, device=dev)
+    ctx = fd.default_context(dev.index or 0)
+    ctx.reserve(fd.FD_FAST, batch, rows, cols)
+
+    def step(i):
+        fd.detect_points("fast", pool[i % 2], need, dist, THR["fast"], out=(xy, cnt), ctx=ctx)
+        fd.brief_compute(pool[i % 2], xy, cnt, length=256, half_patch_size=8, out=bits, ctx=ctx)
+
+    secs, done = timed_graph(torch, step, steps, 2, True, per_graph=2)
+    # the descriptor kernel alone: reps launches captured in one graph (keypoints from the last step)
+    fd.detect_points("fast", pool[0], need, dist, THR["fast"], out=(xy, cnt), ctx=ctx)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fd.brief_compute(pool[0], xy, cnt, length=256, half_patch_size=8, out=bits, ctx=ctx)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    brief_ms = e0.elapsed_time(e1) / reps
+    kp = int(cnt.sum().item())
+    px = batch * rows * cols
+    return {
+        "workload": f"fast (thr 10) + grid NMS (need {need}, dist {dist}) + BRIEF-256 (half 8, bilinear), "
+                    f"{cols}x{rows} gray noise, batch {batch}/GPU (BASELINE configs[2])",
+        "mpix_s": round(done * px / secs / 1e6, 1), "ms_per_step": round(secs / done * 1e3, 4),
+        "keypoints_per_step": kp, "brief_kernel_ms": round(brief_ms, 4),
+        "brief_keypoints_per_s": round(kp / (brief_ms * 1e-3), 1),
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -286,6 +329,10 @@ def main():
                            "~40 VALU lane-instr/px, so VALU issue, not HBM, bounds this kernel (DESIGN.md)"),
         }
         del pool2
+
+    # ---- BASELINE configs[2]: FAST-12 + BRIEF-256, 1280x720 batch 64 (detect -> describe on device) --
+    if not args.no_config3:
+        out["config3_fast_brief"] = run_config3(torch, fd, dev, seed=777 + rank)
 
     # ---- CPU baseline: the oracle (single thread), bounded sample, rank 0 at N=1 ------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -20,14 +20,16 @@ SAMPLERS = {"bilinear": FD_SAMPLE_BILINEAR, "truncate": FD_SAMPLE_TRUNCATE}
 
 
 def brief_compute(frames, uv, counts=None, length: int = 256, half_patch_size: int = 8, sampler="bilinear",
-                  with_valid: bool = False, ctx: Context | None = None):
+                  with_valid: bool = False, out=None, ctx: Context | None = None):
     """Descriptor<BriefType>::Compute (descriptor.h:27-40) for a batch.
 
     frames: u8 [B, R, C] or [R, C]; uv: float32 [B, S, 2] or [S, 2] keypoints (x, y); counts: int32 [B]
     keypoints per frame (None = S each). Host (numpy) frames/uv give numpy outputs; torch device uv
     (with device frames) gives torch outputs, asynchronous on torch's current stream.
     Returns bits uint32 [B, S, ceil(length/32)] (bit i of a descriptor = bit i%32 of word i/32;
-    slots >= counts[b] are left zero), and valid uint8 [B, S] if with_valid.
+    slots >= counts[b] are left zero), and valid uint8 [B, S] if with_valid. Device path only: out=
+    a preallocated int32 [B, S, words] tensor (slots >= counts[b] then keep their contents), so the
+    call is the kernel alone (graph-capturable without an allocation or fill).
     """
     smp = SAMPLERS[sampler] if isinstance(sampler, str) else int(sampler)
     fptr, f_on_dev, b, r, c, keep_f = _frames(frames)
@@ -44,7 +46,12 @@ def brief_compute(frames, uv, counts=None, length: int = 256, half_patch_size: i
             raise ValueError("uv must be [batch, S, 2] matching frames")
         s = int(uv_t.shape[1])
         cnt_t = None if counts is None else counts.to(torch.int32).contiguous()
-        bits = torch.zeros((b, s, nw), dtype=torch.int32, device=uv_t.device)
+        if out is not None:
+            if tuple(out.shape) != (b, s, nw) or out.dtype != torch.int32 or not out.is_contiguous():
+                raise ValueError(f"out must be a contiguous int32 tensor of shape {(b, s, nw)}")
+            bits = out
+        else:
+            bits = torch.zeros((b, s, nw), dtype=torch.int32, device=uv_t.device)
         valid = torch.zeros((b, s), dtype=torch.uint8, device=uv_t.device) if with_valid else None
         _bind_stream(ctx, True)
         rc = _lib.load().fd_brief_compute(

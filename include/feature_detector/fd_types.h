@@ -71,6 +71,31 @@ using Vec2 = FdVec<float, 2>;
 using Vec4 = FdVec<float, 4>;
 using Pixel = FdVec<int32_t, 2>;  // (col, row)
 
+// ---- dynamic column vector (Vec = Eigen::VectorXf in the reference's basic_type.h) ------------------
+template <typename T>
+class FdVecX {
+public:
+    FdVecX() = default;
+    explicit FdVecX(int n) : buf_(static_cast<size_t>(n), T(0)) {}
+    void resize(int n) { buf_.resize(static_cast<size_t>(n)); }
+    void setZero(int n) { buf_.assign(static_cast<size_t>(n), T(0)); }
+    void setZero(int rows, int cols) { setZero(rows * cols); }  // descriptor.h:49 setZero(size, 1)
+    void setZero() { for (auto &e : buf_) e = T(0); }
+    T &operator[](int i) { return buf_[static_cast<size_t>(i)]; }
+    const T &operator[](int i) const { return buf_[static_cast<size_t>(i)]; }
+    T &operator()(int i) { return buf_[static_cast<size_t>(i)]; }
+    const T &operator()(int i) const { return buf_[static_cast<size_t>(i)]; }
+    int size() const { return static_cast<int>(buf_.size()); }
+    int rows() const { return size(); }
+    int cols() const { return 1; }
+    T *data() { return buf_.data(); }
+    const T *data() const { return buf_.data(); }
+
+private:
+    std::vector<T> buf_;
+};
+using Vec = FdVecX<float>;
+
 // ---- row-major dynamic matrix (MatInt, MatImgF) -------------------------------------------------
 template <typename T>
 class FdMat {

@@ -29,12 +29,13 @@ def _run(prog, img, tmp_path, *extra):
 
 def test_api_builds_and_links():
     _build()
-    for f in ("libfeature_detector.so", "fd_demo_points", "fd_demo_lines"):
+    for f in ("libfeature_detector.so", "fd_demo_points", "fd_demo_lines", "fd_demo_descriptor"):
         assert os.path.exists(os.path.join(LIB, f))
     nm = subprocess.run(["nm", "-DC", os.path.join(LIB, "libfeature_detector.so")], capture_output=True, text=True).stdout
     for sym in ("feature_detector::FeaturePointDetector::DetectGoodFeatures",
                 "feature_detector::FeaturePointDetector::SparsifyFeatures",
-                "feature_detector::FeatureLineDetector::DetectGoodFeatures"):
+                "feature_detector::FeatureLineDetector::DetectGoodFeatures",
+                "feature_detector::BriefDescriptor::ComputeForAllFeatures"):
         assert sym in nm
 
 
@@ -93,3 +94,20 @@ def test_line_demo_synthetic_counts(tmp_path, oracle, ref_counts, rec_i):
     _build()
     (r,) = _run("fd_demo_lines", img, tmp_path)
     assert len(r["lines"]) == rec["lines"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sampler", [0, 1])
+def test_descriptor_demo_matches_oracle(tmp_path, image_png, oracle, sampler):
+    """test_feature_descriptor.cpp: Harris (dist 20, thr 20, need 10) then BRIEF kLength 128, half 8."""
+    _build()
+    res = {r["test"]: r for r in _run("fd_demo_descriptor", image_png, tmp_path, sampler)}
+    h, b = res["harris"], res["brief"]
+    assert h["ok"] is True and b["ok"] is True and b["float_overload_ok"] is True
+    feats, _ = oracle.detect(0, image_png, 20, 20.0, 10, None, sort_mode=0)
+    xy = np.array(h["features"], np.float32).reshape(-1, 2)
+    assert np.array_equal(xy, feats)
+    bits, _, _ = oracle.brief(image_png, xy, 128, 8, sampler)
+    exp = ["".join(str((w[j >> 5] >> (j & 31)) & 1) for j in range(128)) for w in bits]
+    assert b["descriptors"] == exp
+    assert res["brief_false_cases"] == {"test": "brief_false_cases", "empty_uv": False, "null_image": False}
