@@ -495,14 +495,14 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
-        FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 16 * batch));
-        FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 16 * batch, c->stream));
+        FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 32 * batch));
+        FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 32 * batch, c->stream));
         s.stamps = as<uint64_t>(c->dbg);
     }
     FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
     c->sel_dirty = false;
     if (stamps) {
-        uint64_t h[16];
+        uint64_t h[32];
         FD_HIP_TRY(c, hipMemcpyAsync(h, c->dbg.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         std::fprintf(stderr, "k_select cycles: init %llu hist0 %llu gather %llu subkeys %llu greedy %llu descent %llu "
@@ -512,6 +512,9 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
                      (unsigned long long)h[7], (unsigned long long)h[8], (unsigned long long)h[9],
                      (unsigned long long)h[0], (unsigned long long)h[10], (unsigned long long)h[11], (unsigned long long)h[12],
                      (unsigned long long)h[13], (unsigned long long)h[14]);
+        std::fprintf(stderr, "  fine:");
+        for (int i = 16; i < 32; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
+        std::fprintf(stderr, "\n");
     }
     if (!outputs_on_device) {
         FD_HIP_TRY(c, hipMemcpyAsync(out_xy, dxy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
@@ -729,9 +732,6 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         FD_HIP_TRY(c, ensure(c->l_valid, nmap));
         dv = as<uint8_t>(c->l_valid);
     }
-    if (dn) FD_HIP_TRY(c, hipMemsetAsync(dn, 0, sizeof(float) * nmap, c->stream));
-    if (da) FD_HIP_TRY(c, hipMemsetAsync(da, 0, sizeof(float) * nmap, c->stream));
-    FD_HIP_TRY(c, hipMemsetAsync(dv, 0, nmap, c->stream));
 
     int32_t *di = valid_idx;
     int64_t *dc = valid_counts;
@@ -743,15 +743,18 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
     }
     const int work_rows = rows - 3;  // rows [1, rows-3]
     const int work_cols = cols - 3;  // cols [1, cols-3]
-    if (work_rows <= 0 || work_cols <= 0) {
+    if (work_rows <= 0 || work_cols <= 0) {  // nothing scanned: all-zero maps
+        if (dn) FD_HIP_TRY(c, hipMemsetAsync(dn, 0, sizeof(float) * nmap, c->stream));
+        if (da) FD_HIP_TRY(c, hipMemsetAsync(da, 0, sizeof(float) * nmap, c->stream));
+        FD_HIP_TRY(c, hipMemsetAsync(dv, 0, nmap, c->stream));
         FD_HIP_TRY(c, hipMemsetAsync(dc, 0, sizeof(int64_t) * batch, c->stream));
-    } else {
+    } else {  // k_lsd_map writes every map entry (zeros outside the scanned rows/columns)
         fdk::LsdArgs a{};
         a.frames = dframes;
         a.batch = batch;
         a.rows = rows;
         a.cols = cols;
-        a.strips = (cols - 2 + 63) / 64;
+        a.strips = (cols - 1 + 63) / 64;  // map columns [0, cols-2]
         const int64_t target = 8192;
         int64_t ch = (static_cast<int64_t>(batch) * a.strips * work_rows) / target;
         ch = std::max<int64_t>(16, std::min<int64_t>(ch, 256));

@@ -34,16 +34,20 @@ __device__ __forceinline__ int lvl_width(int l) { return l == 0 ? 12 : (l == 7 ?
 __device__ __forceinline__ int lvl_top(int l) { return l == 7 ? 64 : 12 + 8 * l; }  // bits consumed through l
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
-// Diagnostic phase clocks (only when a.stamps is set): slot 15 keeps the last clock; FD_STAMP(k)
-// adds the time since then to slot k.
+// Diagnostic phase clocks (only when a.stamps is set), accumulated by thread 0 in LDS (L.st) and
+// written to a.stamps at the end: slot 15 keeps the last clock; FD_STAMP(k) adds the time since then
+// to slot k. Slots 0, 4, 8, 9 are event counters (FD_COUNT).
 #define FD_STAMP(slot)                                                                  \
     do {                                                                                \
         if (a.stamps && threadIdx.x == 0) {                                             \
             const uint64_t now_ = __builtin_readcyclecounter();                         \
-            uint64_t *st_ = a.stamps + static_cast<int64_t>(f) * 16;                    \
-            if ((slot) > 0 && (slot) != 4) st_[(slot)] += now_ - st_[15];               \
-            st_[15] = now_;                                                             \
+            if ((slot) > 0 && (slot) != 4) L.st[(slot)] += now_ - L.st[15];             \
+            L.st[15] = now_;                                                            \
         }                                                                               \
+    } while (0)
+#define FD_COUNT(slot, v)                                                               \
+    do {                                                                                \
+        if (a.stamps && threadIdx.x == 0) L.st[(slot)] += (v);                          \
     } while (0)
 
 // Selection key of a candidate: the response through the frame's key map (order-preserving,
@@ -58,6 +62,9 @@ __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const Sel
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
 constexpr int kSubChunk = 512;  // keys sorted per greedy sub-chunk
+constexpr int kSelectThreads = 1024;  // k_select workgroup size (launch_select)
+constexpr int kHistPerThread = kHistBins / kSelectThreads;
+static_assert(kHistBins % kSelectThreads == 0, "histogram bins per thread");
 constexpr int kRegGather = 16;  // list responses per thread and round in the level-0 gather
 
 // One wave scans a sorted chunk in order (SelectGoodFeatures, feature_point_detector.cpp:62-72), a
@@ -165,6 +172,7 @@ struct alignas(16) SelectLds {
     uint32_t wtot[16];
     uint32_t gcount;
     int s_done, s_acc;
+    uint64_t st[32];  // diagnostic phase clocks (a.stamps only); 16..31 free for ad-hoc probes
 };
 
 __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, SelectLds &L) {
@@ -196,14 +204,31 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
     const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
     const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
+    if (a.stamps && tid == 0)
+        for (int i = 0; i < 32; ++i) L.st[i] = 0;
     FD_STAMP(0);
-
-    if (use_grid) {
-        if (grid_in_lds)
-            for (int i = tid; i < cells; i += nthr) grid_lds[i] = kEmpty;
-        else
-            for (int i = tid; i < cells; i += nthr) grid_g[i] = kEmpty;
+    // One memory round trip for everything the first phase needs: the level-0 histogram (accumulated
+    // by the per-pixel kernel while it emitted the candidates) and the first round of the level-0
+    // gather's list responses (clamped to the list capacity, not the count, so that these loads do
+    // not wait for list_count; entries past the count are masked in the gather). Issued in this
+    // order, waiting for the histogram leaves the list loads in flight.
+    // The list loads go straight to LDS (global_load_lds: no VGPRs held across the histogram scan),
+    // into the occupancy grid's space, which is initialised only after this first round is consumed.
+    uint32_t hv[kHistPerThread];
+#pragma unroll
+    for (int j = 0; j < kHistPerThread; ++j) hv[j] = a.hist0[static_cast<int64_t>(f) * kHistBins + tid + j * kSelectThreads];
+    float *const pre_lds = reinterpret_cast<float *>(grid_lds);
+    static_assert(kRegGather * kSelectThreads <= kGridLdsCells, "first gather round fits the grid's LDS");
+    if (!a.pre_keys) {
+        const uint32_t last = static_cast<uint32_t>(min(a.list_cap, static_cast<int64_t>(0xFFFFFFFF))) - 1u;
+#pragma unroll
+        for (int k = 0; k < kRegGather; ++k)
+            __builtin_amdgcn_global_load_lds(lresp + min(static_cast<uint32_t>(tid + k * nthr), last),
+                                             pre_lds + k * nthr + wave * kWave, 4, 0, 0);
     }
+
+    if (use_grid && !grid_in_lds)
+        for (int i = tid; i < cells; i += nthr) grid_g[i] = kEmpty;
     if (tid == 0) {
         s_done = 0;
         s_acc = 0;
@@ -270,16 +295,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     };
     auto suf = [&](int lvl) -> uint32_t * { return lvl == 0 ? suf0 : sufl[lvl - 1]; };
 
-    // Level-0 histogram: accumulated by the per-pixel kernel while it emitted the candidates.
-    // First round of the level-0 gather's list responses, in flight while the histogram is scanned.
-    float pre_r[kRegGather];
-    if (!a.pre_keys) {
-#pragma unroll
-        for (int k = 0; k < kRegGather; ++k)
-            pre_r[k] = lresp[min(static_cast<uint32_t>(tid + k * nthr), static_cast<uint32_t>(n) - 1u)];
-    }
-
-    for (int b = tid; b < kHistBins; b += nthr) suf0[b] = a.hist0[static_cast<int64_t>(f) * kHistBins + b];
+    for (int j = 0; j < kHistPerThread; ++j) suf0[tid + j * kSelectThreads] = hv[j];
     __syncthreads();
     FD_STAMP(1);
     suffix(suf0, kHistBins);
@@ -295,7 +311,10 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         __syncthreads();
         const uint32_t nn = static_cast<uint32_t>(n);  // list indices fit 32 bits (cap < 2^32)
         const uint32_t step = static_cast<uint32_t>(nthr);
-        uint32_t staged = 0;  // uniform
+        // One round: kRegGather responses per thread. Hits are packed densely into buf in no particular
+        // order (the chunk is sorted afterwards): per k a ballot, the wave's total claimed with one LDS
+        // atomic on gcount, each hit placed at that offset + the hits of lower lanes (mbcnt). No
+        // barrier and no cross-lane scan inside a round.
         auto round = [&](const float (&rr)[kRegGather], uint32_t base) {
             uint32_t hm = 0;
 #pragma unroll
@@ -304,36 +323,29 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 const bool hit = base + tid + k * step < nn && k32 >= k32lo && k32 <= k32hi;
                 hm |= static_cast<uint32_t>(hit) << k;
             }
-            const uint32_t cntt = __popc(hm);
-            uint32_t incl = cntt;  // wave inclusive prefix
-            for (int o = 1; o < kWave; o <<= 1) {
-                const uint32_t t = __shfl_up(incl, o);
-                if (lane >= o) incl += t;
-            }
-            if (lane == kWave - 1) wtot[wave] = incl;
-            __syncthreads();
-            uint32_t before = staged, total = staged;
-            for (int q = 0; q < nthr / kWave; ++q) {
-                const uint32_t wq = wtot[q];
-                before += q < wave ? wq : 0u;
-                total += wq;
-            }
-            uint32_t pos = before + incl - cntt;
-            while (hm) {  // this thread's hits, in index order
-                const int k = __builtin_ctz(hm);
-                hm &= hm - 1u;
-                if (pos < static_cast<uint32_t>(kSelectChunk))
+            uint32_t wtotal = 0;
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) wtotal += popc64(ballot((hm >> k) & 1u));
+            if (wtotal == 0) return;
+            uint32_t off = 0;
+            if (lane == 0) off = atomicAdd(&gcount, wtotal);
+            off = __builtin_amdgcn_readfirstlane(off);
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) {
+                const bool hit = (hm >> k) & 1u;
+                const uint64_t m = ballot(hit);
+                const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
+                if (hit && pos < static_cast<uint32_t>(kSelectChunk))
                     buf[pos] = (static_cast<uint64_t>(__float_as_uint(rr[k])) << 32) | (base + tid + k * step);
-                ++pos;
+                off += popc64(m);
             }
-            staged = total;
-            __syncthreads();  // wtot reuse
         };
         uint32_t base = 0;
         if (pre) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this thread's LDS-direct loads have landed
             float rr[kRegGather];
 #pragma unroll
-            for (int k = 0; k < kRegGather; ++k) rr[k] = pre[k];
+            for (int k = 0; k < kRegGather; ++k) rr[k] = pre[tid + k * step];
             round(rr, 0);
             base = kRegGather * step;
         }
@@ -343,13 +355,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             for (int k = 0; k < kRegGather; ++k) rr[k] = lresp[min(base + tid + k * step, nn - 1u)];
             round(rr, base);
         }
-        if (tid == 0) gcount = staged;
+        __syncthreads();
+        const uint32_t staged = gcount;
         const int ns = min(static_cast<int>(staged), kSelectChunk);
         for (int j = tid; j < ns; j += nthr) {
             const uint64_t e = buf[j];
             const uint32_t li = lidx[static_cast<uint32_t>(e)];
             sup[j] = make_key(__uint_as_float(static_cast<uint32_t>(e >> 32)), li, a);
         }
+        __syncthreads();  // sup complete; gcount read by every thread before anyone reuses it
     };
 
     // The first level-0 chunk (the loop's first cut: the highest bins holding <= kSelectChunk keys),
@@ -371,10 +385,16 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             } else {
                 if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
                     atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x02000000u);
-                gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, a.pre_keys ? nullptr : pre_r);
+                gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, a.pre_keys ? nullptr : pre_lds);
             }
             first_ready = true;
         }
+    }
+    if (use_grid && grid_in_lds) {  // the first round's LDS-direct loads are consumed (or never used)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load still landing in this space
+        __syncthreads();
+        for (int i = tid; i < cells; i += nthr) grid_lds[i] = kEmpty;
+        __syncthreads();
     }
     FD_STAMP(3);
     int level = 0;
@@ -419,7 +439,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             const uint64_t khi = klo | ((1ull << rem) - 1ull);
             const uint32_t expect = S[hi] - S[hi + 1];
             ++level;
-            if (a.stamps && tid == 0) a.stamps[static_cast<int64_t>(f) * 16 + 9] += 1;
+            FD_COUNT(9, 1);
             FD_STAMP(7);
             build(level, klo, khi, suf(level));
             if (tid == 0 && suf(level)[0] != expect)  // consistency guard: descent histogram == parent bin
@@ -505,10 +525,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 const int slo = min(q0, shi);  // one bin larger than a sub-chunk is taken whole
                 const uint32_t sc = S[slo] - sbase;
                 if (sc > 0) {
-                    if (a.stamps && tid == 0) {  // diagnostics: sub-chunk count and total keys
-                        a.stamps[static_cast<int64_t>(f) * 16 + 0] += 1;
-                        a.stamps[static_cast<int64_t>(f) * 16 + 4] += sc;
-                    }
+                    FD_COUNT(0, 1);  // diagnostics: sub-chunk count and total keys
+                    FD_COUNT(4, sc);
                     const uint64_t sklo = ((pre << w) | static_cast<uint64_t>(slo)) << rem;
                     const uint64_t skhi = (((pre << w) | static_cast<uint64_t>(shi)) << rem) | ((1ull << rem) - 1ull);
                     // the sub-chunk's unsorted keys: the whole chunk in place, or extracted into buf
@@ -624,7 +642,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 }
                 shi = slo - 1;
             }
-            if (a.stamps && tid == 0) a.stamps[static_cast<int64_t>(f) * 16 + 8] += 1;
+            FD_COUNT(8, 1);
         }
         hi = lo - 1;
     }
@@ -633,6 +651,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         a.out_counts[f] = static_cast<int32_t>(static_cast<uint32_t>(s_acc) | flags);
     }
     FD_STAMP(7);
+    if (a.stamps && tid == 0)
+        for (int i = 0; i < 32; ++i) a.stamps[static_cast<int64_t>(f) * 32 + i] = L.st[i];
 }
 
 // Resets the frame's counters and level-0 histogram for the next call (stream order puts that call's
@@ -752,7 +772,7 @@ __global__ __launch_bounds__(1024) void k_gather(SelectArgs a) {
     }
 }
 
-__global__ __launch_bounds__(1024) void k_select(SelectArgs a) {
+__global__ __launch_bounds__(kSelectThreads) void k_select(SelectArgs a) {
     __shared__ SelectLds L;
     const int f = blockIdx.x;
     select_frame(a, f, L);
@@ -767,7 +787,7 @@ hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_select, dim3(static_cast<unsigned>(batch)), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_select, dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
     return hipGetLastError();
 }
 
