@@ -74,19 +74,20 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-north-star", action="store_true")
     p.add_argument("--no-config3", action="store_true", help="skip the FAST + BRIEF (configs[2]) leg")
+    p.add_argument("--no-lsd", action="store_true", help="skip the LSD map (configs[3]) leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
 
 
-def make_frames(torch, pattern, n, rows, cols, seed, device):
-    """Seeded synthetic u8 frames generated on the GPU (noise, or 16-px 60/180 checker + U[-10,10])."""
+def make_frames(torch, pattern, n, rows, cols, seed, device, period=16):
+    """Seeded synthetic u8 frames generated on the GPU (noise, or period-px 60/180 checker + U[-10,10])."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     if pattern == "noise":
         return torch.randint(0, 256, (n, rows, cols), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
-    r = torch.arange(rows, device=device).view(1, rows, 1) // 16
-    c = torch.arange(cols, device=device).view(1, 1, cols) // 16
+    r = torch.arange(rows, device=device).view(1, rows, 1) // period
+    c = torch.arange(cols, device=device).view(1, 1, cols) // period
     base = torch.where(((r + c) % 2) == 1, 180, 60)
     noise = torch.randint(-10, 11, (n, rows, cols), generator=g, device=device, dtype=torch.int32)
     return (base + noise).clamp(0, 255).to(torch.uint8)
@@ -239,6 +240,73 @@ def run_config3(torch, fd, dev, seed, batch=64, rows=720, cols=1280, need=200, d
     }
 
 
+def graph_time_ms(torch, fn, reps):
+    """Average time of fn() replayed `reps` times from one captured hipGraph (HIP events)."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    del g
+    return e0.elapsed_time(e1) / reps
+
+
+def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5):
+    """BASELINE configs[3]: LSD level-line map (norm, angle, valid + column-major valid list) on
+    structured 64-px checker frames, all on the device (the host region growing is not timed)."""
+    frames = make_frames(torch, "checker", batch, rows, cols, seed, dev, period=64)
+    out = fd.lsd_map(frames)
+    torch.cuda.synchronize()
+    valid = int(out[4].sum().item())
+    ms = graph_time_ms(torch, lambda: fd.lsd_map(frames, out=out), reps)
+    px = batch * rows * cols
+    mpx = batch * (rows - 1) * (cols - 1)
+    alg = px + 9 * mpx + 4 * valid  # read u8 frame; write norm f32 + angle f32 + valid u8; 4 B per listed pixel
+    del out, frames
+    return {
+        "workload": f"LSD level-line map, {cols}x{rows} gray 64-px checker + noise, batch {batch}/GPU "
+                    "(BASELINE configs[3]; host region growing not timed)",
+        "ms_per_batch": round(ms, 4), "mpix_s": round(px / (ms * 1e-3) / 1e6, 1), "valid_pixels": valid,
+        "kernels": "k_lsd_map + k_lsd_scan + k_lsd_scatter",
+        "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "bytes_per_launch": alg},
+    }
+
+
+def copy_bandwidth(torch, dev, nbytes=1 << 30, reps=5):
+    """Measured device-to-device copy bandwidth (read + write bytes / time): the practical HBM ceiling."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    ms = graph_time_ms(torch, lambda: b.copy_(a), reps)
+    del a, b
+    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+
+
+def run_end_to_end(torch, fd, args, seconds=3.0):
+    """PCIe-inclusive rate of the headline workload: host frames staged by the library, features
+    copied back (what the C++ drop-in class does per call). Reported beside `value`, never as it."""
+    import numpy as np
+
+    frames = make_frames(torch, args.pattern, 16, args.rows, args.cols, 31337, torch.device("cuda")).cpu().numpy()
+    fd.detect_points(args.detector, frames[0], args.need, args.dist, THR[args.detector])
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fd.detect_points(args.detector, frames[n % len(frames)], args.need, args.dist, THR[args.detector])
+        n += 1
+    el = time.perf_counter() - t0
+    return {"mpix_s": round(n * args.rows * args.cols / el / 1e6, 1), "ms_per_frame": round(el / n * 1e3, 4),
+            "frames": n, "note": "host numpy frame -> H2D staging -> detect -> D2H features, synchronous per frame"}
+
+
 def main():
     args = parse()
     import torch
@@ -333,6 +401,13 @@ def main():
     # ---- BASELINE configs[2]: FAST-12 + BRIEF-256, 1280x720 batch 64 (detect -> describe on device) --
     if not args.no_config3:
         out["config3_fast_brief"] = run_config3(torch, fd, dev, seed=777 + rank)
+
+    # ---- BASELINE configs[3]: LSD map, 1920x1080 batch 256 per GPU ----------------------------------
+    if not args.no_lsd:
+        out["config4_lsd_map"] = run_lsd(torch, fd, dev, seed=4242 + rank)
+    out["device_copy_gbs"] = copy_bandwidth(torch, dev)
+    if world == 1:
+        out["end_to_end_host_frames"] = run_end_to_end(torch, fd, args)
 
     # ---- CPU baseline: the oracle (single thread), bounded sample, rank 0 at N=1 ------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

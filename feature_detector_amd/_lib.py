@@ -18,7 +18,7 @@ EXPORTS = (
     "fd_ctx_get_stream",
     "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_points_detect", "fd_points_candidates", "fd_points_response",
     "fd_points_response_append",
-    "fd_lsd_map", "fd_brief_compute",
+    "fd_lsd_map", "fd_brief_compute", "fd_nn_select", "fd_nn_descriptors",
     "fd_build_info",
 )
 
@@ -34,6 +34,11 @@ class fd_point_opts(ctypes.Structure):
 
 
 FD_SAMPLE_BILINEAR, FD_SAMPLE_TRUNCATE = 0, 1
+
+
+class fd_nn_opts(ctypes.Structure):
+    _fields_ = [("invalid_boundary", ctypes.c_int32), ("min_feature_distance", ctypes.c_int32),
+                ("max_features", ctypes.c_int32), ("min_response", ctypes.c_float)]
 
 
 class fd_brief_opts(ctypes.Structure):
@@ -78,6 +83,8 @@ def load() -> ctypes.CDLL:
         "fd_points_response_append": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
         "fd_lsd_map": (i32, [P, P, i32, i32, i32, i32, f32, P, P, P, P, i64, P, i32]),
         "fd_brief_compute": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_brief_opts), P, P, i32, P, P, i32]),
+        "fd_nn_select": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_nn_opts), P, P, P, i32, P, i32]),
+        "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

@@ -80,6 +80,7 @@ struct SelectArgs {
     // the possible response range over the full 32 bits (finer level-0 bins).
     uint32_t key_base;
     int key_lz;
+    int tie_idx_desc;  // equal responses by descending raster index (SuperPoint) instead of ascending
     // gather kernel (k_gather, batch x gather_groups workgroups) -> first level-0 chunk per frame;
     // null pre_keys: k_select gathers it itself
     uint64_t *pre_keys;   // [batch][kSelectChunk]
@@ -123,6 +124,34 @@ struct BriefArgs {
     uint8_t *out_valid;  // [batch][stride] or null
 };
 
+// SuperPoint heatmap -> candidate lists (the K1 list format + level-0 histogram), for K4.
+struct HeatArgs {
+    const float *heat;  // [batch][rows][cols]
+    int batch, rows, cols;
+    int blocks_per_frame;
+    float thr;
+    int border;            // kInvalidBoundary: rows/cols within it are masked out
+    const uint32_t *mask;  // prior-feature bitmap (null = none)
+    int mask_wpr;
+    float *list_resp;
+    uint32_t *list_idx;
+    int64_t list_cap;
+    uint32_t *list_count;
+    uint32_t *hist0;
+    uint32_t key_base;
+    int key_lz;
+};
+
+// Bilinear descriptor sampling from the 1/8-resolution descriptor map.
+struct NnDescArgs {
+    const float *map;  // [batch][channels][map_rows][map_cols]
+    int batch, channels, map_rows, map_cols;
+    const float *xy;        // [batch][stride][2]
+    const int32_t *counts;  // [batch] or null (= stride)
+    int stride;
+    float *out;  // [batch][stride][channels]
+};
+
 // Launchers (stream-ordered, no allocation, no synchronisation: graph-capturable).
 hipError_t launch_mask_boxes(const float *prior_xy, const int32_t *prior_frame, int n_prior, int dist, int rows,
                              int cols, uint32_t *mask, int mask_wpr, hipStream_t s);
@@ -134,5 +163,8 @@ hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_g
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
 hipError_t launch_brief(const BriefArgs &a, hipStream_t s);
+hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s);
+int heat_blocks_per_frame(int64_t npx);
+hipError_t launch_nn_desc(const NnDescArgs &a, hipStream_t s);
 
 }  // namespace fdk

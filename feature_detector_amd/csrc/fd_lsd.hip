@@ -122,6 +122,7 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
     const int r0 = 1 + chunk * a.chunk_h;
     const int r1 = min(r0 + a.chunk_h, rows - 2);  // rows [r0, r1) within [1, rows-3]
     const bool colv = col >= 1 && col <= cols - 3;
+    const bool colw = col <= cols - 2;  // the map has columns [0, cols-2]; outside the scan they are 0
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
     const int64_t mbase = static_cast<int64_t>(f) * (rows - 1) * mc;
 
@@ -132,6 +133,17 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
         if (lane == 63) nb = buf_load_u8(rs, r * cols + col + 1);
         p1 = nb;
     };
+    // Map rows 0 and rows-2 lie outside the scan (:71): written as zeros by the first / last chunk, so
+    // every map entry is written exactly once and the host needs no memset.
+    auto zero_row = [&](int r) {
+        if (!colw) return;
+        const int64_t i = mbase + static_cast<int64_t>(r) * mc + col;
+        if (a.norm) a.norm[i] = 0.0f;
+        if (a.angle) a.angle[i] = 0.0f;
+        a.valid[i] = 0;
+    };
+    if (chunk == 0) zero_row(0);
+    if (r1 == rows - 2) zero_row(rows - 2);
     uint32_t t0, t1;
     load_pair(r0, t0, t1);
     int cnt = 0;
@@ -146,9 +158,9 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
         const bool v = colv && nrm > a.min_norm;
         float ang = 0.0f;
         if (v) ang = fd_atan2f(gx, -gy);
-        if (colv) {
+        if (colw) {
             const int64_t i = mbase + static_cast<int64_t>(r) * mc + col;
-            if (a.norm) a.norm[i] = nrm;
+            if (a.norm) a.norm[i] = colv ? nrm : 0.0f;
             if (a.angle) a.angle[i] = ang;
             a.valid[i] = v ? 1 : 0;
         }

@@ -1,0 +1,118 @@
+// SuperPoint post-processing for gfx950, around a network that runs in
+// PyTorch-ROCm (feature_detector_amd/superpoint.py).
+//
+// Reference: NNFeaturePointDetector, src/nn_feature_point_detector/nn_feature_point_detector.cpp
+//   CreateMask (:59-73)                      -> border test here + K0 prior boxes (fd_points.hip)
+//   SelectKeypointCandidatesFromHeatMap (:128-139) -> k_heat_candidates: every heatmap value
+//       > kMinResponse becomes a candidate (unordered list + level-0 key histogram, as K1 emits)
+//   SelectGoodFeaturesFromCandidates (:141-155)   -> K4 (fd_select.hip) with tie_idx_desc: the
+//       multimap is walked from crbegin, i.e. response descending and, among equal responses,
+//       raster index descending (equal keys are inserted at the upper bound of their range)
+//   ExtractDescriptorsForSelectedFeatures (:163-193) -> k_nn_desc: bilinear sampling of the
+//       1/8-resolution descriptor map, the reference's float sequence (-ffp-contract=off)
+#include "fd_device.h"
+#include "fd_kernels.h"
+
+namespace fdk {
+namespace {
+
+constexpr int kHeatPerThread = 4;
+constexpr int kHeatBlock = 256;
+
+// One workgroup = kHeatPerThread * 256 consecutive pixels of one frame (coalesced f32 loads).
+__global__ __launch_bounds__(kHeatBlock) void k_heat_candidates(HeatArgs a) {
+    const int f = blockIdx.y;
+    const int64_t npx = static_cast<int64_t>(a.rows) * a.cols;
+    const float *h = a.heat + static_cast<int64_t>(f) * npx;
+    const int64_t p0 = static_cast<int64_t>(blockIdx.x) * (kHeatPerThread * kHeatBlock) + threadIdx.x;
+    float v[kHeatPerThread];
+#pragma unroll
+    for (int j = 0; j < kHeatPerThread; ++j) {
+        const int64_t p = p0 + j * kHeatBlock;
+        v[j] = p < npx ? h[p] : 0.0f;
+    }
+    const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * a.rows * a.mask_wpr : nullptr;
+    float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+#pragma unroll
+    for (int j = 0; j < kHeatPerThread; ++j) {
+        const int64_t p = p0 + j * kHeatBlock;
+        bool ok = p < npx && v[j] > a.thr;  // :133-135 (NaN never passes)
+        int r = 0, c = 0;
+        if (ok) {
+            r = static_cast<int>(p / a.cols);
+            c = static_cast<int>(p - static_cast<int64_t>(r) * a.cols);
+            // CreateMask (:61-68): the kInvalidBoundary outermost rows/columns are 0; prior boxes (:69-71)
+            ok = r >= a.border && r < a.rows - a.border && c >= a.border && c < a.cols - a.border;
+            if (ok && fmask) ok = (fmask[static_cast<int64_t>(r) * a.mask_wpr + (c >> 5)] >> (c & 31)) & 1u;
+        }
+        const uint64_t m = ballot(ok);
+        if (m == 0) continue;
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(&a.list_count[f], static_cast<uint32_t>(popc64(m)));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (ok) {
+            const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(base)));
+            if (pos < a.list_cap) {
+                dr[pos] = v[j];
+                di[pos] = static_cast<uint32_t>(p);
+            }
+            const uint32_t bin = ((float_key(v[j]) - a.key_base) << a.key_lz) >> 20;
+            atomicAdd(&a.hist0[static_cast<int64_t>(f) * kHistBins + bin], 1u);
+        }
+    }
+}
+
+// One wave per (frame, feature slot); lanes over descriptor channels.
+__global__ __launch_bounds__(256) void k_nn_desc(NnDescArgs a) {
+    const int64_t slot = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (slot >= static_cast<int64_t>(a.batch) * a.stride) return;
+    const int f = static_cast<int>(slot / a.stride);
+    const int k = static_cast<int>(slot - static_cast<int64_t>(f) * a.stride);
+    if (a.counts && k >= static_cast<int>(static_cast<uint32_t>(a.counts[f]) & 0x01FFFFFFu)) return;
+    const float x = a.xy[2 * slot], y = a.xy[2 * slot + 1];
+    // :170-178
+    const float row = y / 8.0f;
+    const float col = x / 8.0f;
+    const int32_t int_row = static_cast<int32_t>(row);
+    const int32_t int_col = static_cast<int32_t>(col);
+    const float sub_row = row - floorf(row);
+    const float sub_col = col - floorf(col);
+    const float inv_sub_row = 1.0f - sub_row;
+    const float inv_sub_col = 1.0f - sub_col;
+    const float w0 = inv_sub_col * inv_sub_row, w1 = sub_col * inv_sub_row, w2 = inv_sub_col * sub_row,
+                w3 = sub_col * sub_row;
+    // :184-187 (row / col ranges of the channel map; the last row and column are excluded)
+    const bool inside = int_row >= 0 && int_row < a.map_rows - 1 && int_col >= 0 && int_col < a.map_cols - 1;
+    const int64_t plane = static_cast<int64_t>(a.map_rows) * a.map_cols;
+    const float *m = a.map + static_cast<int64_t>(f) * a.channels * plane;
+    float *o = a.out + slot * a.channels;
+    for (int j = lane_id(); j < a.channels; j += kWave) {
+        float d = 0.0f;
+        if (inside) {
+            const float *mp = m + j * plane + static_cast<int64_t>(int_row) * a.map_cols + int_col;
+            d = w0 * mp[0] + w1 * mp[1] + w2 * mp[a.map_cols] + w3 * mp[a.map_cols + 1];  // :188-189
+        }
+        o[j] = d;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s) {
+    if (a.blocks_per_frame == 0 || a.batch == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_heat_candidates, dim3(static_cast<unsigned>(a.blocks_per_frame), static_cast<unsigned>(a.batch)),
+                       dim3(kHeatBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+int heat_blocks_per_frame(int64_t npx) { return static_cast<int>((npx + kHeatPerThread * kHeatBlock - 1) / (kHeatPerThread * kHeatBlock)); }
+
+hipError_t launch_nn_desc(const NnDescArgs &a, hipStream_t s) {
+    const int64_t waves = static_cast<int64_t>(a.batch) * a.stride;
+    if (waves == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_nn_desc, dim3(static_cast<unsigned>((waves + 3) / 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace fdk

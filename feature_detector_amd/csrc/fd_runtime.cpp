@@ -41,6 +41,7 @@ struct fd_ctx {
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts;
     DevBuf b_uv, b_counts, b_bits, b_valid;
+    DevBuf n_heat, n_map, n_xy, n_counts, n_out;
     DevBuf dbg;
     // FAST offset table cache
     int64_t off_n = -1;
@@ -292,6 +293,107 @@ void key_map(int kind, float thr, const fdk::FastOffsets *off, int64_t n_off, ui
     lz = kmax > base ? __builtin_clz(kmax - base) : 0;
 }
 
+// Inputs of the selection stage (K4) after a candidate kernel filled the lists of `sb`.
+struct SelectCall {
+    int batch = 0, rows = 0, cols = 0, dist = 0;
+    uint32_t need = 0;
+    int64_t cap = 0;
+    uint32_t key_base = 0;
+    int key_lz = 0;
+    int tie_idx_desc = 0;  // equal responses: raster index descending (SuperPoint multimap) instead of ascending
+};
+
+// K4 (k_gather + k_select) on the candidate lists, features into out_xy / out_counts (device, or copied
+// back to the host and checked when !outputs_on_device).
+int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const SelectBufs &sb, float *out_xy,
+               int32_t out_stride, int32_t *out_counts, int outputs_on_device, int frames_on_device) {
+    fdk::SelectArgs s{};
+    const int batch = q.batch, rows = q.rows, cols = q.cols;
+    s.list_resp = as<float>(c->list_resp);
+    s.list_idx = as<uint32_t>(c->list_idx);
+    s.list_count = sb.list_count;
+    s.hist0 = sb.hist0;
+    s.list_cap = q.cap;
+    s.rows = rows;
+    s.cols = cols;
+    s.tie_idx_desc = q.tie_idx_desc;
+    s.mask = pi.mask;
+    s.mask_wpr = pi.wpr;
+    s.prior_counts = pi.counts_dev;
+    s.need = q.need;
+    s.dist = q.dist;
+    if (s.dist >= 1) {
+        s.grid_w = (cols + s.dist) / (s.dist + 1);
+        s.grid_h = (rows + s.dist) / (s.dist + 1);
+        const int64_t cells = static_cast<int64_t>(s.grid_w + 2) * (s.grid_h + 2);  // bordered grid
+        if (cells > fdk::kGridLdsCells) {
+            FD_HIP_TRY(c, ensure(c->grid, sizeof(uint32_t) * cells * batch));
+            s.grid_global = as<uint32_t>(c->grid);
+        }
+    }
+    float *dxy = out_xy;
+    int32_t *dcnt = out_counts;
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, ensure(c->out_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch));
+        FD_HIP_TRY(c, ensure(c->out_counts, sizeof(int32_t) * batch));
+        dxy = as<float>(c->out_xy);
+        dcnt = as<int32_t>(c->out_counts);
+    }
+    s.out_xy = dxy;
+    s.out_stride = out_stride;
+    s.out_counts = dcnt;
+    s.key_base = q.key_base;
+    s.key_lz = q.key_lz;
+    // Small batches of large frames: spread the first chunk's gather over ~256 workgroups in its own
+    // kernel (~9 us of fixed cost: pays off once one workgroup's pass over the list costs more, i.e.
+    // from about a megapixel per frame; measured at 640x480: break-even).
+    const bool big = static_cast<int64_t>(rows) * cols >= (1 << 20);
+    s.gather_groups = big ? std::max(1, std::min(64, 256 / std::max(batch, 1))) : 1;
+    if (const char *e = std::getenv("FD_GATHER_GROUPS")) s.gather_groups = std::max(1, std::atoi(e));  // A/B
+    s.pre_count = sb.pre_count;
+    s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
+    static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
+    if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
+        FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 32 * batch));
+        FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 32 * batch, c->stream));
+        s.stamps = as<uint64_t>(c->dbg);
+    }
+    FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
+    c->sel_dirty = false;
+    if (stamps) {
+        uint64_t h[32];
+        FD_HIP_TRY(c, hipMemcpyAsync(h, c->dbg.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        std::fprintf(stderr, "k_select cycles: init %llu hist0 %llu gather %llu subkeys %llu greedy %llu descent %llu "
+                             "control %llu | chunks %llu descents %llu subchunks %llu | extract %llu runsort %llu merges %llu place %llu cmask %llu\n",
+                     (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
+                     (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
+                     (unsigned long long)h[7], (unsigned long long)h[8], (unsigned long long)h[9],
+                     (unsigned long long)h[0], (unsigned long long)h[10], (unsigned long long)h[11], (unsigned long long)h[12],
+                     (unsigned long long)h[13], (unsigned long long)h[14]);
+        std::fprintf(stderr, "  fine:");
+        for (int i = 16; i < 32; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
+        std::fprintf(stderr, "\n");
+    }
+    if (!outputs_on_device) {
+        FD_HIP_TRY(c, hipMemcpyAsync(out_xy, dxy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
+                                     hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dcnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (int b = 0; b < batch; ++b) {
+            if (static_cast<uint32_t>(out_counts[b]) & 0xFE000000u)
+                return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (flags 0x" +
+                                               [](uint32_t v) { char t[16]; std::snprintf(t, sizeof t, "%x", v); return std::string(t); }(
+                                                   static_cast<uint32_t>(out_counts[b]) >> 25) +
+                                               ", frame " + std::to_string(b) + ")");
+            if (out_counts[b] > out_stride) return fail(c, FD_ERR_CAPACITY, "out_stride smaller than the features found");
+        }
+    } else if (!frames_on_device) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host frames must stay valid until copied
+    }
+    return FD_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -328,7 +430,8 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->out_counts, &c->grid,     &c->dbg,
                       &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
-                      &c->l_idx,    &c->l_counts, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid};
+                      &c->l_idx,    &c->l_counts, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
+                      &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out};
     for (DevBuf *b : bufs) release(*b);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -450,89 +553,16 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
         }
     }
 
-    fdk::SelectArgs s{};
-    s.list_resp = a.list_resp;
-    s.list_idx = a.list_idx;
-    s.list_count = a.list_count;
-    s.hist0 = a.hist0;
-    s.list_cap = cap;
-    s.rows = rows;
-    s.cols = cols;
-    s.mask = pi.mask;
-    s.mask_wpr = pi.wpr;
-    s.prior_counts = pi.counts_dev;
-    s.need = need;
-    s.dist = opts->min_feature_distance;
-    if (s.dist >= 1) {
-        s.grid_w = (cols + s.dist) / (s.dist + 1);
-        s.grid_h = (rows + s.dist) / (s.dist + 1);
-        const int64_t cells = static_cast<int64_t>(s.grid_w + 2) * (s.grid_h + 2);  // bordered grid
-        if (cells > fdk::kGridLdsCells) {
-            FD_HIP_TRY(c, ensure(c->grid, sizeof(uint32_t) * cells * batch));
-            s.grid_global = as<uint32_t>(c->grid);
-        }
-    }
-    float *dxy = out_xy;
-    int32_t *dcnt = out_counts;
-    if (!outputs_on_device) {
-        FD_HIP_TRY(c, ensure(c->out_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch));
-        FD_HIP_TRY(c, ensure(c->out_counts, sizeof(int32_t) * batch));
-        dxy = as<float>(c->out_xy);
-        dcnt = as<int32_t>(c->out_counts);
-    }
-    s.out_xy = dxy;
-    s.out_stride = out_stride;
-    s.out_counts = dcnt;
-    s.key_base = a.key_base;
-    s.key_lz = a.key_lz;
-    // Small batches of large frames: spread the first chunk's gather over ~256 workgroups in its own
-    // kernel (~9 us of fixed cost: pays off once one workgroup's pass over the list costs more, i.e.
-    // from about a megapixel per frame; measured at 640x480: break-even).
-    const bool big = static_cast<int64_t>(rows) * cols >= (1 << 20);
-    s.gather_groups = big ? std::max(1, std::min(64, 256 / std::max(batch, 1))) : 1;
-    if (const char *e = std::getenv("FD_GATHER_GROUPS")) s.gather_groups = std::max(1, std::atoi(e));  // A/B
-    s.pre_count = sb.pre_count;
-    s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
-    static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
-    if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
-        FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 32 * batch));
-        FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 32 * batch, c->stream));
-        s.stamps = as<uint64_t>(c->dbg);
-    }
-    FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
-    c->sel_dirty = false;
-    if (stamps) {
-        uint64_t h[32];
-        FD_HIP_TRY(c, hipMemcpyAsync(h, c->dbg.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
-        std::fprintf(stderr, "k_select cycles: init %llu hist0 %llu gather %llu subkeys %llu greedy %llu descent %llu "
-                             "control %llu | chunks %llu descents %llu subchunks %llu | extract %llu runsort %llu merges %llu place %llu cmask %llu\n",
-                     (unsigned long long)h[1], (unsigned long long)h[2], (unsigned long long)h[3],
-                     (unsigned long long)h[4], (unsigned long long)h[5], (unsigned long long)h[6],
-                     (unsigned long long)h[7], (unsigned long long)h[8], (unsigned long long)h[9],
-                     (unsigned long long)h[0], (unsigned long long)h[10], (unsigned long long)h[11], (unsigned long long)h[12],
-                     (unsigned long long)h[13], (unsigned long long)h[14]);
-        std::fprintf(stderr, "  fine:");
-        for (int i = 16; i < 32; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
-        std::fprintf(stderr, "\n");
-    }
-    if (!outputs_on_device) {
-        FD_HIP_TRY(c, hipMemcpyAsync(out_xy, dxy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
-                                     hipMemcpyDeviceToHost, c->stream));
-        FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dcnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
-        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
-        for (int b = 0; b < batch; ++b) {
-            if (static_cast<uint32_t>(out_counts[b]) & 0xFE000000u)
-                return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (flags 0x" +
-                                               [](uint32_t v) { char t[16]; std::snprintf(t, sizeof t, "%x", v); return std::string(t); }(
-                                                   static_cast<uint32_t>(out_counts[b]) >> 25) +
-                                               ", frame " + std::to_string(b) + ")");
-            if (out_counts[b] > out_stride) return fail(c, FD_ERR_CAPACITY, "out_stride smaller than the features found");
-        }
-    } else if (!frames_on_device) {
-        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host frames must stay valid until copied
-    }
-    return FD_OK;
+    SelectCall sc{};
+    sc.batch = batch;
+    sc.rows = rows;
+    sc.cols = cols;
+    sc.dist = opts->min_feature_distance;
+    sc.need = need;
+    sc.cap = cap;
+    sc.key_base = a.key_base;
+    sc.key_lz = a.key_lz;
+    return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
 }
 
 static int points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,
@@ -856,6 +886,116 @@ int fd_brief_compute(fd_ctx *c, const uint8_t *frames, int frames_on_device, int
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
     } else if (!frames_on_device) {
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host frames must stay valid until copied
+    }
+    return FD_OK;
+}
+
+int fd_nn_select(fd_ctx *c, const float *heatmap, int heatmap_on_device, int batch, int rows, int cols,
+                 const fd_nn_opts *opts, const float *prior_xy, const int32_t *prior_counts, float *out_xy,
+                 int32_t out_stride, int32_t *out_counts, int outputs_on_device) {
+    int rc = check_shape(c, FD_HARRIS, batch, rows, cols);
+    if (rc) return rc;
+    if (!heatmap) return fail(c, FD_ERR_INVALID, "heatmap is NULL");
+    if (!opts || !out_xy || !out_counts || out_stride < 1) return fail(c, FD_ERR_INVALID, "bad output arguments");
+    if (opts->invalid_boundary < 0) return fail(c, FD_ERR_INVALID, "invalid_boundary must be >= 0");
+    if (opts->max_features < 0) return fail(c, FD_ERR_INVALID, "max_features must be >= 0");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    const int64_t npx = static_cast<int64_t>(rows) * cols;
+    const float *dheat = heatmap;
+    if (!heatmap_on_device) {
+        FD_HIP_TRY(c, ensure(c->n_heat, sizeof(float) * npx * batch));
+        FD_HIP_TRY(c, hipMemcpyAsync(c->n_heat.p, heatmap, sizeof(float) * npx * batch, hipMemcpyHostToDevice, c->stream));
+        dheat = as<float>(c->n_heat);
+    }
+    PriorInfo pi;
+    rc = setup_priors(c, batch, rows, cols, opts->min_feature_distance, prior_xy, prior_counts, pi);
+    if (rc) return rc;
+    const int64_t cap = npx + 64;
+    SelectBufs sb{};
+    rc = select_buffers(c, batch, cap, sb);
+    if (rc) return rc;
+    fdk::HeatArgs h{};
+    h.heat = dheat;
+    h.batch = batch;
+    h.rows = rows;
+    h.cols = cols;
+    h.blocks_per_frame = fdk::heat_blocks_per_frame(npx);
+    h.thr = opts->min_response;
+    h.border = opts->invalid_boundary;
+    h.mask = pi.mask;
+    h.mask_wpr = pi.wpr;
+    h.list_resp = as<float>(c->list_resp);
+    h.list_idx = as<uint32_t>(c->list_idx);
+    h.list_cap = cap;
+    h.list_count = sb.list_count;
+    h.hist0 = sb.hist0;
+    key_map(FD_HARRIS, opts->min_response, nullptr, 0, h.key_base, h.key_lz);  // responses in (thr, +inf]
+    c->sel_dirty = true;  // until k_select is enqueued: it resets the control block
+    FD_HIP_TRY(c, fdk::launch_heat_candidates(h, c->stream));
+    SelectCall sc{};
+    sc.batch = batch;
+    sc.rows = rows;
+    sc.cols = cols;
+    sc.dist = opts->min_feature_distance;
+    sc.need = static_cast<uint32_t>(opts->max_features);
+    sc.cap = cap;
+    sc.key_base = h.key_base;
+    sc.key_lz = h.key_lz;
+    sc.tie_idx_desc = 1;
+    return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, heatmap_on_device);
+}
+
+int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int batch, int channels, int map_rows,
+                      int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
+                      int io_on_device) {
+    if (!c) return FD_ERR_INVALID;
+    if (!map || !xy || !out) return fail(c, FD_ERR_INVALID, "bad arguments");
+    if (batch < 1 || channels < 1 || map_rows < 1 || map_cols < 1 || stride < 0)
+        return fail(c, FD_ERR_INVALID, "batch, channels, map_rows, map_cols must be >= 1");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    if (stride == 0) return FD_OK;
+    const size_t mapn = static_cast<size_t>(batch) * channels * map_rows * map_cols;
+    const size_t slots = static_cast<size_t>(batch) * stride;
+    fdk::NnDescArgs a{};
+    a.batch = batch;
+    a.channels = channels;
+    a.map_rows = map_rows;
+    a.map_cols = map_cols;
+    a.stride = stride;
+    a.map = map;
+    if (!map_on_device) {
+        FD_HIP_TRY(c, ensure(c->n_map, sizeof(float) * mapn));
+        FD_HIP_TRY(c, hipMemcpyAsync(c->n_map.p, map, sizeof(float) * mapn, hipMemcpyHostToDevice, c->stream));
+        a.map = as<float>(c->n_map);
+    }
+    if (io_on_device) {
+        a.xy = xy;
+        a.counts = counts;
+        a.out = out;
+    } else {
+        FD_HIP_TRY(c, ensure(c->n_xy, sizeof(float) * 2 * slots));
+        FD_HIP_TRY(c, ensure(c->n_out, sizeof(float) * channels * slots));
+        FD_HIP_TRY(c, hipMemcpyAsync(c->n_xy.p, xy, sizeof(float) * 2 * slots, hipMemcpyHostToDevice, c->stream));
+        a.xy = as<float>(c->n_xy);
+        a.out = as<float>(c->n_out);
+        if (counts) {
+            FD_HIP_TRY(c, ensure(c->n_counts, sizeof(int32_t) * batch));
+            FD_HIP_TRY(c, hipMemcpyAsync(c->n_counts.p, counts, sizeof(int32_t) * batch, hipMemcpyHostToDevice, c->stream));
+            a.counts = as<int32_t>(c->n_counts);
+        }
+    }
+    FD_HIP_TRY(c, fdk::launch_nn_desc(a, c->stream));
+    if (!io_on_device) {
+        for (int b = 0; b < batch; ++b) {
+            const int n = counts ? std::min<int64_t>(static_cast<uint32_t>(counts[b]) & 0x01FFFFFFu, stride) : stride;
+            if (n <= 0) continue;
+            const size_t s0 = static_cast<size_t>(b) * stride;
+            FD_HIP_TRY(c, hipMemcpyAsync(out + s0 * channels, a.out + s0 * channels, sizeof(float) * channels * n,
+                                         hipMemcpyDeviceToHost, c->stream));
+        }
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    } else if (!map_on_device) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
     return FD_OK;
 }

@@ -56,8 +56,10 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t map_key32(float resp, const SelectArgs &a) {
     return (float_key(resp) - a.key_base) << a.key_lz;
 }
+// (tie_idx_desc: idx itself, so that equal responses order by descending raster index, the order in
+// which SuperPoint's std::multimap is walked from crbegin, nn_feature_point_detector.cpp:144.)
 __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const SelectArgs &a) {
-    return (static_cast<uint64_t>(map_key32(resp, a)) << 32) | static_cast<uint64_t>(~idx);
+    return (static_cast<uint64_t>(map_key32(resp, a)) << 32) | static_cast<uint64_t>(a.tie_idx_desc ? idx : ~idx);
 }
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
@@ -499,7 +501,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             FD_STAMP(3);  // gather
             const uint32_t s1 = static_cast<uint32_t>(d + 1);
             auto place = [&](int pos, uint64_t sk) {  // decode position, prior mask, grid cell
-                uint32_t idx = ~static_cast<uint32_t>(sk);
+                uint32_t idx = a.tie_idx_desc ? static_cast<uint32_t>(sk) : ~static_cast<uint32_t>(sk);
                 bool ok = true;
                 if (idx >= static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols)) {  // consistency guard
                     ok = false;

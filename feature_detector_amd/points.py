@@ -242,18 +242,41 @@ def point_candidates(kind, frames, min_feature_distance: int = 15, min_valid_res
     return (out, rmap) if response_map else out
 
 
-def lsd_map(frames, min_norm: float = 20.0, cap: int | None = None, ctx: Context | None = None):
-    """ComputeLineLevelAngleMap (fd_lsd_map) on host frames.
+def lsd_map(frames, min_norm: float = 20.0, cap: int | None = None, ctx: Context | None = None, out=None):
+    """ComputeLineLevelAngleMap (fd_lsd_map).
 
-    Returns per frame (norm, angle, valid, valid_idx_colmajor); maps are (rows-1, cols-1).
+    Host (numpy) frames: returns per frame (norm, angle, valid, valid_idx_colmajor); maps are
+    (rows-1, cols-1). Torch device frames: returns device tensors (norm [B, R-1, C-1] f32, angle f32,
+    valid u8, valid_idx int32 [B, cap], counts int64 [B]), asynchronous on torch's current stream;
+    `out` may pass them preallocated (graph capture); any of norm/angle/valid may be None to skip.
     """
     ptr, on_dev, b, r, c, keep = _frames(frames)
-    if on_dev:
-        raise TypeError("lsd_map takes host frames")
     ctx = ctx or default_context()
-    _bind_stream(ctx, False)
     mr, mc = r - 1, c - 1
     cap = mr * mc if cap is None else cap
+    if on_dev:
+        import torch
+
+        if out is None:
+            dev = frames.device
+            out = (torch.empty((b, mr, mc), dtype=torch.float32, device=dev),
+                   torch.empty((b, mr, mc), dtype=torch.float32, device=dev),
+                   torch.empty((b, mr, mc), dtype=torch.uint8, device=dev),
+                   torch.empty((b, max(cap, 1)), dtype=torch.int32, device=dev),
+                   torch.empty((b,), dtype=torch.int64, device=dev))
+        norm, ang, val, idx, cnt = out
+        cap = idx.shape[1]
+        _bind_stream(ctx, True)
+
+        def p(t):
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        rc = _lib.load().fd_lsd_map(ctx.ptr, ctypes.c_void_p(ptr), 1, b, r, c, float(min_norm), p(norm), p(ang),
+                                    p(val), p(idx), int(cap), p(cnt), 1)
+        _lib.check(ctx.ptr, rc)
+        del keep
+        return out
+    _bind_stream(ctx, False)
     norm = np.zeros((b, mr, mc), np.float32)
     ang = np.zeros((b, mr, mc), np.float32)
     val = np.zeros((b, mr, mc), np.uint8)

@@ -164,6 +164,39 @@ int fd_brief_compute(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, i
                      const fd_brief_opts *opts, const float *uv, const int32_t *counts, int32_t stride,
                      uint32_t *out_bits, uint8_t *out_valid, int io_on_device);
 
+/* ---- SuperPoint post-processing (the network runs in PyTorch-ROCm) -------------------------------- */
+/* NNFeaturePointDetector::Options (nn_feature_point_detector.h:22-31) fields of the heatmap path. */
+typedef struct fd_nn_opts {
+    int32_t invalid_boundary;     /* kInvalidBoundary, default 3 */
+    int32_t min_feature_distance; /* kMinFeatureDistance, default 15 */
+    int32_t max_features;         /* kMaxNumberOfDetectedFeatures, default 240 (counts prior features) */
+    float min_response;           /* kMinResponse, default 0.1 */
+} fd_nn_opts;
+
+/*
+ * fd_nn_select -- CreateMask + SelectKeypointCandidatesFromHeatMap + SelectGoodFeaturesFromCandidates
+ * (nn_feature_point_detector.cpp:59-73, 128-155) for a batch of full-resolution heatmaps
+ * [batch][rows][cols] (float). Candidates are heatmap values > min_response outside the invalid
+ * boundary and the prior boxes; they are visited in the reference's std::multimap order (response
+ * descending, equal responses by raster index descending) and kept greedily with the
+ * min_feature_distance box rule until max_features (including the priors) exist. out_xy / out_counts
+ * as fd_points_detect (new features only, selection order).
+ */
+int fd_nn_select(fd_ctx *ctx, const float *heatmap, int heatmap_on_device, int batch, int rows, int cols,
+                 const fd_nn_opts *opts, const float *prior_xy, const int32_t *prior_counts, float *out_xy,
+                 int32_t out_stride, int32_t *out_counts, int outputs_on_device);
+
+/*
+ * fd_nn_descriptors -- ExtractDescriptorsForSelectedFeatures (nn_feature_point_detector.cpp:163-193):
+ * per feature (x, y) in xy [batch][stride][2] (counts as fd_brief_compute), bilinear samples at
+ * (y / 8, x / 8) of each of the `channels` planes of map [batch][channels][map_rows][map_cols]
+ * (zero outside [0, map_rows-1) x [0, map_cols-1)), into out [batch][stride][channels].
+ * xy, counts and out are all device pointers when io_on_device, host pointers otherwise.
+ */
+int fd_nn_descriptors(fd_ctx *ctx, const float *map, int map_on_device, int batch, int channels, int map_rows,
+                      int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
+                      int io_on_device);
+
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);
 

@@ -20,6 +20,7 @@
 // reference's operation order.
 // =====================================================================================================
 #include <algorithm>
+#include <map>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -466,6 +467,78 @@ void orc_brief(const uint8_t *img, int rows, int cols, const float *uv, int n, i
             if (value_1 < value_2) bits[i >> 5] |= 1u << (i & 31);
         }
         if (out_valid) out_valid[k] = 1;
+    }
+}
+
+// -----------------------------------------------------------------------------------------------------
+// SuperPoint post-processing, NNFeaturePointDetector (nn_feature_point_detector/nn_feature_point_detector.cpp).
+// CreateMask (:59-73): ones, kInvalidBoundary outermost rows/cols zero (topRows/bottomRows/leftCols/
+// rightCols), then a (2d+1)^2 box (clipped, :75-82) around each truncated prior feature (:84-90).
+// SelectKeypointCandidatesFromHeatMap (:128-139): std::multimap<float, Pixel> of every value > thr.
+// SelectGoodFeaturesFromCandidates (:141-155): crbegin -> crend; skip masked; append; stop at
+// max_features (priors included); draw the box.
+// Returns the number of new features written to out_xy (x, y).
+// -----------------------------------------------------------------------------------------------------
+int orc_nn_select(const float *heat, int rows, int cols, int border, int dist, int max_features, float thr,
+                  const float *prior_xy, int n_prior, float *out_xy, int out_cap) {
+    std::vector<int32_t> mask(static_cast<size_t>(rows) * cols, 1);
+    auto draw = [&](int32_t row, int32_t col, int32_t radius) {  // DrawRectangleInMask (:75-82)
+        const int32_t r0 = std::max(0, row - radius), r1 = std::min(rows - 1, row + radius);
+        const int32_t c0 = std::max(0, col - radius), c1 = std::min(cols - 1, col + radius);
+        for (int32_t r = r0; r <= r1; ++r)
+            for (int32_t c = c0; c <= c1; ++c) mask[static_cast<size_t>(r) * cols + c] = 0;
+    };
+    if (border) {
+        for (int r = 0; r < rows; ++r)
+            for (int c = 0; c < cols; ++c)
+                if (r < border || r >= rows - border || c < border || c >= cols - border)
+                    mask[static_cast<size_t>(r) * cols + c] = 0;
+    }
+    for (int i = 0; i < n_prior; ++i) draw(static_cast<int32_t>(prior_xy[2 * i + 1]), static_cast<int32_t>(prior_xy[2 * i]), dist);
+    std::multimap<float, std::pair<int32_t, int32_t>> candidates;  // response -> (col, row)
+    for (int32_t row = 0; row < rows; ++row)
+        for (int32_t col = 0; col < cols; ++col) {
+            const float response = heat[static_cast<size_t>(row) * cols + col];
+            if (response > thr) candidates.insert(std::make_pair(response, std::make_pair(col, row)));
+        }
+    size_t size = static_cast<size_t>(n_prior);
+    int n = 0;
+    for (auto it = candidates.crbegin(); it != candidates.crend(); ++it) {
+        const int32_t col = it->second.first, row = it->second.second;
+        if (!mask[static_cast<size_t>(row) * cols + col]) continue;
+        if (n < out_cap) {
+            out_xy[2 * n] = static_cast<float>(col);
+            out_xy[2 * n + 1] = static_cast<float>(row);
+        }
+        ++n;
+        ++size;
+        if (size >= static_cast<size_t>(max_features)) break;
+        draw(row, col, dist);
+    }
+    return n;
+}
+
+// ExtractDescriptorsForSelectedFeatures (:163-193): map is [channels][map_rows][map_cols].
+void orc_nn_descriptors(const float *map, int channels, int map_rows, int map_cols, const float *xy, int n, float *out) {
+    for (int i = 0; i < n; ++i) {
+        const float row = xy[2 * i + 1] / 8.0f;
+        const float col = xy[2 * i] / 8.0f;
+        const int32_t int_row = static_cast<int32_t>(row);
+        const int32_t int_col = static_cast<int32_t>(col);
+        const float sub_row = row - std::floor(row);
+        const float sub_col = col - std::floor(col);
+        const float inv_sub_row = 1.0f - sub_row;
+        const float inv_sub_col = 1.0f - sub_col;
+        const float weights[4] = {inv_sub_col * inv_sub_row, sub_col * inv_sub_row, inv_sub_col * sub_row, sub_col * sub_row};
+        for (int j = 0; j < channels; ++j) {
+            float &d = out[static_cast<size_t>(i) * channels + j];
+            if (int_row < 0 || int_row >= map_rows - 1 || int_col < 0 || int_col >= map_cols - 1) {
+                d = 0.0f;
+                continue;
+            }
+            const float *p = map + (static_cast<size_t>(j) * map_rows + int_row) * map_cols + int_col;
+            d = weights[0] * p[0] + weights[1] * p[1] + weights[2] * p[map_cols] + weights[3] * p[map_cols + 1];
+        }
     }
 }
 

@@ -50,6 +50,8 @@ def lib():
             "orc_lsd_min_region_size": (u32, [i32, i32, f32]),
             "orc_make_frame": (None, [i32, u32, i32, i32, i32, _P]),
             "orc_brief": (None, [_P, i32, i32, _P, i32, i32, i32, i32, _P, _P, _P, _P]),
+            "orc_nn_select": (i32, [_P, i32, i32, i32, i32, i32, f32, _P, i32, _P, i32]),
+            "orc_nn_descriptors": (None, [_P, i32, i32, i32, _P, i32, _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -201,3 +203,28 @@ def brief(img, uv, length=256, half=8, sampler=0):
     lib().orc_brief(_ptr(img), R, C, _ptr(uv), n, length, half, sampler, _ptr(pat), _ptr(bits), _ptr(valid),
                     _ptr(mom))
     return bits[:n], valid[:n], mom[:n]
+
+
+# ------------------------------------------------------------------------------ SuperPoint (f3)
+def nn_select(heat, border=3, dist=15, max_features=240, thr=0.1, prior=None):
+    """CreateMask + SelectKeypointCandidatesFromHeatMap + SelectGoodFeaturesFromCandidates
+    (nn_feature_point_detector.cpp:59-73, 128-155) on one heatmap; returns new features (n, 2) (x, y)."""
+    heat = np.ascontiguousarray(heat, np.float32)
+    R, C = heat.shape
+    pr = np.zeros((1, 2), np.float32) if prior is None or len(prior) == 0 else np.ascontiguousarray(prior, np.float32)
+    n_prior = 0 if prior is None else len(prior)
+    cap = max(max_features, 1) + 1
+    out = np.zeros((cap, 2), np.float32)
+    n = lib().orc_nn_select(_ptr(heat), R, C, border, dist, max_features, np.float32(thr), _ptr(pr), n_prior,
+                            _ptr(out), cap)
+    return out[:min(n, cap)].copy()
+
+
+def nn_descriptors(desc_map, xy):
+    """ExtractDescriptorsForSelectedFeatures (nn_feature_point_detector.cpp:163-193); desc_map [C, h, w]."""
+    desc_map = np.ascontiguousarray(desc_map, np.float32)
+    ch, h, w = desc_map.shape
+    xy = np.ascontiguousarray(np.asarray(xy, np.float32).reshape(-1, 2))
+    out = np.zeros((max(len(xy), 1), ch), np.float32)
+    lib().orc_nn_descriptors(_ptr(desc_map), ch, h, w, _ptr(xy), len(xy), _ptr(out))
+    return out[:len(xy)]

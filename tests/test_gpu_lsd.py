@@ -79,3 +79,24 @@ def test_batch(fd, oracle):
         en, ea, ev, eidx = oracle.lsd_map(frames[b])
         assert np.array_equal(res[b][3], eidx)
         assert np.array_equal(res[b][1].view(np.uint32), ea.view(np.uint32))
+
+
+def test_device_path_matches_host(fd, oracle):
+    """lsd_map on torch device frames (maps written whole by the kernel, no memsets) equals the host path."""
+    torch = pytest.importorskip("torch")
+    frames = np.stack([oracle.make_frame("checker", 60 + i, 120, 200, 64) for i in range(2)]
+                      + [oracle.make_frame("noise", 70, 120, 200)])
+    host = fd.lsd_map(frames)
+    dev = torch.from_numpy(frames).cuda()
+    out = (torch.full((3, 119, 199), 7.0, device="cuda"), torch.full((3, 119, 199), 7.0, device="cuda"),
+           torch.full((3, 119, 199), 7, dtype=torch.uint8, device="cuda"),
+           torch.empty((3, 119 * 199), dtype=torch.int32, device="cuda"), torch.empty((3,), dtype=torch.int64, device="cuda"))
+    n, a, v, idx, cnt = fd.lsd_map(dev, out=out)
+    torch.cuda.synchronize()
+    for b in range(3):
+        hn, ha, hv, hidx = host[b]
+        assert np.array_equal(n[b].cpu().numpy().view(np.uint32), hn.view(np.uint32))
+        assert np.array_equal(a[b].cpu().numpy().view(np.uint32), ha.view(np.uint32))
+        assert np.array_equal(v[b].cpu().numpy(), hv)
+        assert int(cnt[b]) == len(hidx)
+        assert np.array_equal(idx[b, :len(hidx)].cpu().numpy(), hidx)

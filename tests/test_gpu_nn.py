@@ -1,0 +1,87 @@
+"""GPU parity of the SuperPoint post-processing (fd_nn_select / fd_nn_descriptors)
+against the CPU oracle (nn_feature_point_detector.cpp:59-73, 128-155, 163-193), and the random-weight
+SuperPoint network end to end (network outputs checked through the oracle on the same tensors).
+
+Bar: bit-exact features (multimap order: response descending, ties by raster index descending) and
+descriptor values. The network's weights are seeded random (no trained model offline): its
+keypoints are not comparable with the reference's ("parity unpinned" for the network itself).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sp():
+    import feature_detector_amd as fd
+    from feature_detector_amd import superpoint
+
+    fd.load()
+    return superpoint
+
+
+def features(xy, cnt, b):
+    xy = xy if isinstance(xy, np.ndarray) else xy.cpu().numpy()
+    n = int(cnt[b]) if isinstance(cnt, np.ndarray) else int(cnt[b].item())
+    return xy[b, :n]
+
+
+@pytest.mark.parametrize("border,dist,maxf,thr", [(3, 15, 240, 0.1), (0, 4, 300, 0.5), (5, 0, 50, 0.3),
+                                                  (3, 15, 1, 0.1), (3, 40, 240, 0.2), (2, 1, 5000, 0.05)])
+def test_nn_select_matches_oracle(sp, oracle, border, dist, maxf, thr):
+    rng = np.random.default_rng(dist * 7 + maxf)
+    heat = np.stack([(np.round(rng.random((120, 160)) * 32) / 32).astype(np.float32),  # many ties
+                     rng.random((120, 160)).astype(np.float32),
+                     np.zeros((120, 160), np.float32)])
+    o = sp.Options(kInvalidBoundary=border, kMinFeatureDistance=dist, kMaxNumberOfDetectedFeatures=maxf,
+                   kMinResponse=thr)
+    xy, cnt = sp.nn_select(heat, o)
+    for b in range(3):
+        exp = oracle.nn_select(heat[b], border, dist, maxf, thr)
+        assert np.array_equal(features(xy, cnt, b), exp), b
+
+
+def test_nn_select_priors(sp, oracle):
+    rng = np.random.default_rng(11)
+    heat = rng.random((2, 96, 128)).astype(np.float32)
+    prior = [np.array([(10.5, 20.7), (100.0, 50.0), (-4.0, 3.0)], np.float32), np.zeros((0, 2), np.float32)]
+    o = sp.Options(kMaxNumberOfDetectedFeatures=40)
+    xy, cnt = sp.nn_select(heat, o, prior)
+    for b in range(2):
+        exp = oracle.nn_select(heat[b], 3, 15, 40, 0.1, prior[b] if len(prior[b]) else None)
+        assert np.array_equal(features(xy, cnt, b), exp)
+
+
+def test_nn_descriptors_matches_oracle(sp, oracle):
+    rng = np.random.default_rng(3)
+    m = rng.standard_normal((2, 256, 15, 20)).astype(np.float32)
+    xy = np.stack([rng.uniform(-10, 170, (33, 2)), rng.uniform(0, 160, (33, 2))]).astype(np.float32)
+    xy[0, :5] = np.round(xy[0, :5])
+    counts = np.array([33, 20], np.int32)
+    got = sp.nn_descriptors(m, xy, counts)
+    for b in range(2):
+        exp = oracle.nn_descriptors(m[b], xy[b, :counts[b]])
+        assert np.array_equal(got[b, :counts[b]].view(np.uint32), exp.view(np.uint32))
+        assert not got[b, counts[b]:].any()
+
+
+def test_superpoint_end_to_end_device(sp, oracle):
+    """Random-weight SuperPoint on device frames: GPU selection + descriptors equal the oracle's
+    post-processing of the very same network outputs."""
+    torch = pytest.importorskip("torch")
+    det = sp.SuperPointDetector(sp.Options(kComputeDescriptors=True, kMaxImageRows=240, kMaxImageCols=320))
+    assert det.Initialize()
+    frames = torch.from_numpy(np.stack([oracle.make_frame("noise", 900 + i, 240, 320) for i in range(3)])).cuda()
+    heat, desc = det.InferenceSession(frames)
+    xy, cnt, d = det.DetectGoodFeaturesWithDescriptor(frames)
+    torch.cuda.synchronize()
+    heat_h, desc_h = heat.float().cpu().numpy(), desc.float().cpu().numpy()
+    cnt_h = cnt.cpu().numpy()
+    assert cnt_h.min() > 0
+    for b in range(3):
+        exp = oracle.nn_select(heat_h[b], 3, 15, 240, 0.1)
+        got = features(xy, cnt, b)
+        assert np.array_equal(got, exp)
+        ed = oracle.nn_descriptors(desc_h[b], got)
+        assert np.array_equal(d[b, :cnt_h[b]].cpu().numpy().view(np.uint32), ed.view(np.uint32))
