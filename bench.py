@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
+MFMA_PEAK_TFLOPS_FP16 = 2500.0  # dense BF16/FP16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
 # HBM traffic per launch measured with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) and
 # corrected by the calibrated gfx950 factor (tools/gpu_traffic.sh, tools/calib/fetch_calib.hip).
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic.json")
@@ -75,6 +76,7 @@ def parse():
     p.add_argument("--no-north-star", action="store_true")
     p.add_argument("--no-config3", action="store_true", help="skip the FAST + BRIEF (configs[2]) leg")
     p.add_argument("--no-lsd", action="store_true", help="skip the LSD map (configs[3]) leg")
+    p.add_argument("--no-superpoint", action="store_true", help="skip the SuperPoint (configs[4]) leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
@@ -307,6 +309,59 @@ def run_end_to_end(torch, fd, args, seconds=3.0):
             "frames": n, "note": "host numpy frame -> H2D staging -> detect -> D2H features, synchronous per frame"}
 
 
+def conv_flops(net, rows, cols):
+    """Dense multiply-add FLOPs (2 per MAC) of every Conv2d of the network for one rows x cols frame."""
+    from torch import nn
+
+    total, scale = 0, {"1": 1, "2": 2, "3": 4, "4": 8, "P": 8, "D": 8}
+    for name, m in net.named_modules():
+        if isinstance(m, nn.Conv2d):
+            f = scale[name[4]]  # conv1a -> '1', convPa -> 'P'
+            h, w = rows // f, cols // f
+            total += 2 * h * w * m.in_channels * m.out_channels * m.kernel_size[0] * m.kernel_size[1]
+    return total
+
+
+def run_superpoint(torch, fd, dev, seed, batch=64, rows=480, cols=640, steps=10):
+    """BASELINE configs[4]: SuperPoint fp16 on 640x480, 512 frames over 8 GPUs = 64 per GPU: network
+    (PyTorch-ROCm, MIOpen convs), then GPU selection + descriptors (fd_nn_select / fd_nn_descriptors)."""
+    from feature_detector_amd import superpoint as spm
+
+    det = spm.SuperPointDetector(spm.Options(kComputeDescriptors=True, kMaxImageRows=rows, kMaxImageCols=cols),
+                                 device=dev.index or 0)
+    det.Initialize()
+    frames = make_frames(torch, "noise", batch, rows, cols, seed, dev)
+    for _ in range(2):
+        det.DetectGoodFeaturesWithDescriptor(frames)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        xy, cnt, d = det.DetectGoodFeaturesWithDescriptor(frames)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        heat, desc = det.InferenceSession(frames)
+    e1.record()
+    torch.cuda.synchronize()
+    net_ms = e0.elapsed_time(e1) / steps
+    post_ms = graph_time_ms(torch, lambda: (spm.nn_select(heat, det.options(), out=(xy, cnt)),
+                                            spm.nn_descriptors(desc, xy, cnt, out=d)), 10)
+    flops = conv_flops(det.net, rows, cols) * batch
+    return {
+        "workload": f"SuperPoint (random weights, fp16 convs) + heatmap selection (thr 0.1, dist 15, max 240) + "
+                    f"256-d descriptors, {cols}x{rows} noise, batch {batch}/GPU (BASELINE configs[4]: 512 over 8 GPUs)",
+        "ms_per_step": round(el * 1e3, 3), "frames_per_s": round(batch / el, 1),
+        "mpix_s": round(batch * rows * cols / el / 1e6, 1), "network_ms": round(net_ms, 3),
+        "postprocess_ms": round(post_ms, 4), "features_per_frame": round(float(cnt.float().mean().item()), 1),
+        "network_roofline": {"bound": "mfma", "achieved": round(flops / (net_ms * 1e-3) / 1e12, 1),
+                             "peak": MFMA_PEAK_TFLOPS_FP16, "unit": "TFLOP/s",
+                             "frac": round(flops / (net_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS_FP16, 4),
+                             "flops_per_step": flops},
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -401,6 +456,10 @@ def main():
     # ---- BASELINE configs[2]: FAST-12 + BRIEF-256, 1280x720 batch 64 (detect -> describe on device) --
     if not args.no_config3:
         out["config3_fast_brief"] = run_config3(torch, fd, dev, seed=777 + rank)
+
+    # ---- BASELINE configs[4]: SuperPoint, 640x480, 64 frames per GPU --------------------------------
+    if not args.no_superpoint:
+        out["config5_superpoint"] = run_superpoint(torch, fd, dev, seed=5151 + rank)
 
     # ---- BASELINE configs[3]: LSD map, 1920x1080 batch 256 per GPU ----------------------------------
     if not args.no_lsd:

@@ -91,7 +91,7 @@ def nn_select(heat, options: Options | None = None, prior=None, out=None, ctx: C
     rc = _lib.load().fd_nn_select(
         ctx.ptr, ctypes.c_void_p(ptr), 1 if on_dev else 0, b, r, c, ctypes.byref(opts),
         ctypes.c_void_p(pflat.ctypes.data) if pflat is not None else None,
-        ctypes.c_void_p(pcnt.ctypes.data) if pcnt is not None else None, int(stride), ctypes.c_void_p(xy_p),
+        ctypes.c_void_p(pcnt.ctypes.data) if pcnt is not None else None, ctypes.c_void_p(xy_p), int(stride),
         ctypes.c_void_p(cnt_p), 1 if on_dev else 0)
     _lib.check(ctx.ptr, rc)
     return xy, cnt

@@ -73,8 +73,12 @@ def test_superpoint_end_to_end_device(sp, oracle):
     det = sp.SuperPointDetector(sp.Options(kComputeDescriptors=True, kMaxImageRows=240, kMaxImageCols=320))
     assert det.Initialize()
     frames = torch.from_numpy(np.stack([oracle.make_frame("noise", 900 + i, 240, 320) for i in range(3)])).cuda()
+    xy2, cnt2, d2 = det.DetectGoodFeaturesWithDescriptor(frames)
+    assert tuple(xy2.shape) == (3, 241, 2) and tuple(d2.shape) == (3, 241, 256)
+    # the same post-processing on one network run (MIOpen may pick different algorithms per call)
     heat, desc = det.InferenceSession(frames)
-    xy, cnt, d = det.DetectGoodFeaturesWithDescriptor(frames)
+    xy, cnt = sp.nn_select(heat, det.options())
+    d = sp.nn_descriptors(desc, xy, cnt)
     torch.cuda.synchronize()
     heat_h, desc_h = heat.float().cpu().numpy(), desc.float().cpu().numpy()
     cnt_h = cnt.cpu().numpy()
