@@ -38,7 +38,7 @@ FD_SAMPLE_BILINEAR, FD_SAMPLE_TRUNCATE = 0, 1
 
 class fd_nn_opts(ctypes.Structure):
     _fields_ = [("invalid_boundary", ctypes.c_int32), ("min_feature_distance", ctypes.c_int32),
-                ("max_features", ctypes.c_int32), ("min_response", ctypes.c_float)]
+                ("max_features", ctypes.c_int32), ("min_response", ctypes.c_float), ("max_response", ctypes.c_float)]
 
 
 class fd_brief_opts(ctypes.Structure):

@@ -81,6 +81,7 @@ struct SelectArgs {
     uint32_t key_base;
     int key_lz;
     int tie_idx_desc;  // equal responses by descending raster index (SuperPoint) instead of ascending
+    int value_flag;    // pre_count bit 31 set by the candidate kernel -> guard flag 0x40000000 (out of key range)
     // gather kernel (k_gather, batch x gather_groups workgroups) -> first level-0 chunk per frame;
     // null pre_keys: k_select gathers it itself
     uint64_t *pre_keys;   // [batch][kSelectChunk]
@@ -140,6 +141,8 @@ struct HeatArgs {
     uint32_t *hist0;
     uint32_t key_base;
     int key_lz;
+    float vmax;           // values above it set bit 31 of value_flag[f] (the key map assumes <= vmax)
+    uint32_t *value_flag;  // [batch], the selection control block's pre_count words (gather disabled)
 };
 
 // Bilinear descriptor sampling from the 1/8-resolution descriptor map.

@@ -57,6 +57,7 @@ __global__ __launch_bounds__(kHeatBlock) void k_heat_candidates(HeatArgs a) {
                 dr[pos] = v[j];
                 di[pos] = static_cast<uint32_t>(p);
             }
+            if (v[j] > a.vmax) atomicOr(&a.value_flag[f], 0x80000000u);  // outside the key map: the call fails
             const uint32_t bin = ((float_key(v[j]) - a.key_base) << a.key_lz) >> 20;
             atomicAdd(&a.hist0[static_cast<int64_t>(f) * kHistBins + bin], 1u);
         }

@@ -301,6 +301,7 @@ struct SelectCall {
     uint32_t key_base = 0;
     int key_lz = 0;
     int tie_idx_desc = 0;  // equal responses: raster index descending (SuperPoint multimap) instead of ascending
+    bool value_flag = false;  // the candidate kernel flags out-of-range values in pre_count (gather kernel off)
 };
 
 // K4 (k_gather + k_select) on the candidate lists, features into out_xy / out_counts (device, or copied
@@ -317,6 +318,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.rows = rows;
     s.cols = cols;
     s.tie_idx_desc = q.tie_idx_desc;
+    s.value_flag = q.value_flag ? 1 : 0;
     s.mask = pi.mask;
     s.mask_wpr = pi.wpr;
     s.prior_counts = pi.counts_dev;
@@ -350,6 +352,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     const bool big = static_cast<int64_t>(rows) * cols >= (1 << 20);
     s.gather_groups = big ? std::max(1, std::min(64, 256 / std::max(batch, 1))) : 1;
     if (const char *e = std::getenv("FD_GATHER_GROUPS")) s.gather_groups = std::max(1, std::atoi(e));  // A/B
+    if (q.value_flag) s.gather_groups = 1;  // pre_count carries the candidate kernel's flag instead
     s.pre_count = sb.pre_count;
     s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
@@ -381,6 +384,9 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dcnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         for (int b = 0; b < batch; ++b) {
+            if (static_cast<uint32_t>(out_counts[b]) & 0x40000000u)
+                return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": a value above the declared maximum "
+                                               "(fd_nn_opts::max_response)");
             if (static_cast<uint32_t>(out_counts[b]) & 0xFE000000u)
                 return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (flags 0x" +
                                                [](uint32_t v) { char t[16]; std::snprintf(t, sizeof t, "%x", v); return std::string(t); }(
@@ -929,7 +935,16 @@ int fd_nn_select(fd_ctx *c, const float *heatmap, int heatmap_on_device, int bat
     h.list_cap = cap;
     h.list_count = sb.list_count;
     h.hist0 = sb.hist0;
-    key_map(FD_HARRIS, opts->min_response, nullptr, 0, h.key_base, h.key_lz);  // responses in (thr, +inf]
+    // responses in (thr, max_response] (probabilities: max 1) or (thr, +inf]
+    key_map(FD_HARRIS, opts->min_response, nullptr, 0, h.key_base, h.key_lz);
+    h.vmax = std::numeric_limits<float>::infinity();
+    const bool bounded = std::isfinite(opts->max_response) && opts->max_response > opts->min_response;
+    if (bounded) {
+        h.vmax = opts->max_response;
+        const uint32_t kmax = host_float_key(opts->max_response) + 1u;
+        h.key_lz = kmax > h.key_base ? __builtin_clz(kmax - h.key_base) : 0;
+    }
+    h.value_flag = sb.pre_count;
     c->sel_dirty = true;  // until k_select is enqueued: it resets the control block
     FD_HIP_TRY(c, fdk::launch_heat_candidates(h, c->stream));
     SelectCall sc{};
@@ -942,6 +957,7 @@ int fd_nn_select(fd_ctx *c, const float *heatmap, int heatmap_on_device, int bat
     sc.key_base = h.key_base;
     sc.key_lz = h.key_lz;
     sc.tie_idx_desc = 1;
+    sc.value_flag = true;
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, heatmap_on_device);
 }
 

@@ -236,6 +236,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         s_acc = 0;
         prefix[0] = 0;
         atomicExch(&a.out_counts[f], 0);  // (atomic: the guard flags below are atomicOr'ed)
+        if (a.value_flag && (__hip_atomic_load(&a.pre_count[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 31))
+            atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x40000000u);  // candidate outside the key map
     }
     if (n == 0) {  // RETURN_TRUE_IF(candidates_.empty()) (:55)
         if (tid == 0) a.out_counts[f] = 0;

@@ -40,20 +40,23 @@ class Options:
     kComputeDescriptors: bool = False
 
 
-def _opts(o: Options) -> fd_nn_opts:
+def _opts(o: Options, max_response: float = 1.0) -> fd_nn_opts:
     return fd_nn_opts(int(o.kInvalidBoundary), int(o.kMinFeatureDistance), int(o.kMaxNumberOfDetectedFeatures),
-                      float(o.kMinResponse))
+                      float(o.kMinResponse), float(max_response))
 
 
-def nn_select(heat, options: Options | None = None, prior=None, out=None, ctx: Context | None = None):
+def nn_select(heat, options: Options | None = None, prior=None, out=None, ctx: Context | None = None,
+              max_response: float = 1.0):
     """fd_nn_select on heatmaps [B, H, W] float32 (numpy, or a torch device tensor -> device outputs).
 
+    max_response: declared upper bound of the heatmap (1.0: softmax probabilities); float('inf') for
+    arbitrary maps (coarser selection keys). A value above it fails the call.
     Returns (xy [B, max+1, 2] float32, counts [B] int32): new features per frame, selection order.
     prior: None or a list (per frame) of (n_i, 2) float arrays of (x, y), host memory.
     """
     o = options or Options()
     ctx = ctx or default_context()
-    opts = _opts(o)
+    opts = _opts(o, max_response)
     on_dev = _is_torch_device_tensor(heat)
     if on_dev:
         import torch

@@ -171,6 +171,9 @@ typedef struct fd_nn_opts {
     int32_t min_feature_distance; /* kMinFeatureDistance, default 15 */
     int32_t max_features;         /* kMaxNumberOfDetectedFeatures, default 240 (counts prior features) */
     float min_response;           /* kMinResponse, default 0.1 */
+    float max_response;           /* upper bound of the heatmap values: 1.0 for SuperPoint's softmax
+                                     probabilities (finer selection keys); a larger value fails the call
+                                     (FD_ERR_INVALID). <= min_response or non-finite: no bound assumed */
 } fd_nn_opts;
 
 /*

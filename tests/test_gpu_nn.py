@@ -89,3 +89,27 @@ def test_superpoint_end_to_end_device(sp, oracle):
         assert np.array_equal(got, exp)
         ed = oracle.nn_descriptors(desc_h[b], got)
         assert np.array_equal(d[b, :cnt_h[b]].cpu().numpy().view(np.uint32), ed.view(np.uint32))
+
+
+def test_nn_select_key_range(sp, oracle):
+    """Probabilities (max_response 1, fine keys) and an unbounded map give the same features; a value
+    above the declared maximum fails the call instead of being misordered."""
+    import feature_detector_amd as fd
+
+    rng = np.random.default_rng(21)
+    heat = (rng.random((2, 100, 140)) ** 3).astype(np.float32)
+    o = sp.Options(kMaxNumberOfDetectedFeatures=120, kMinFeatureDistance=6)
+    a, ca = sp.nn_select(heat, o)
+    b, cb = sp.nn_select(heat, o, max_response=float("inf"))
+    assert np.array_equal(ca, cb) and np.array_equal(a, b)
+    for f in range(2):
+        assert np.array_equal(features(a, ca, f), oracle.nn_select(heat[f], 3, 6, 120, 0.1))
+    bad = heat.copy()
+    bad[1, 50, 70] = 1.5
+    with pytest.raises(fd.FdError):
+        sp.nn_select(bad, o)
+    c, cc = sp.nn_select(bad, o, max_response=float("inf"))
+    assert np.array_equal(features(c, cc, 1), oracle.nn_select(bad[1], 3, 6, 120, 0.1))
+    # the failed call left the control block clean for the next one
+    d, cd = sp.nn_select(heat, o)
+    assert np.array_equal(cd, ca) and np.array_equal(d, a)
