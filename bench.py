@@ -242,6 +242,30 @@ def run_config3(torch, fd, dev, seed, batch=64, rows=720, cols=1280, need=200, d
     }
 
 
+class phase:
+    """roctx range around one leg of the bench (torch.cuda.nvtx on ROCm): rocprofv3 --marker-trace
+    records it, and tools/rocpd_summary.py --phases attributes each kernel to the leg it ran in."""
+
+    def __init__(self, torch, name):
+        self.torch, self.name = torch, name
+
+    def __enter__(self):
+        self.torch.cuda.synchronize()
+        try:
+            self.torch.cuda.nvtx.range_push("fdbench:" + self.name)
+        except Exception:
+            pass
+        return self
+
+    def __exit__(self, *exc):
+        self.torch.cuda.synchronize()
+        try:
+            self.torch.cuda.nvtx.range_pop()
+        except Exception:
+            pass
+        return False
+
+
 def graph_time_ms(torch, fn, reps):
     """Average time of fn() replayed `reps` times from one captured hipGraph (HIP events)."""
     fn()
@@ -385,16 +409,18 @@ def main():
 
     # ---- headline workload (per rank: its own frames; weak scaling) -------------------------------
     barrier = dist.barrier if world > 1 else None
-    secs, done, pool, _ = run_config(torch, fd, dev, args.detector, args.rows, args.cols, args.batch, args.pool,
-                                     args.need, args.dist, args.pattern, args.steps, args.warmup,
-                                     not args.no_graph, seed=1234 + 1000003 * rank, barrier=barrier)
+    with phase(torch, "headline"):
+        secs, done, pool, _ = run_config(torch, fd, dev, args.detector, args.rows, args.cols, args.batch, args.pool,
+                                         args.need, args.dist, args.pattern, args.steps, args.warmup,
+                                         not args.no_graph, seed=1234 + 1000003 * rank, barrier=barrier)
     secs_max = max_over_ranks(secs, dist if world > 1 else None, dev if backend == "nccl" else None)
     px_step = args.batch * args.rows * args.cols
     value = world * done * px_step / secs_max / 1e6  # Mpix/s, all ranks
     ms_per_step = secs_max / done * 1e3
 
     # ---- per-kernel timing for the roofline (rank-local, same stream) -----------------------------
-    k_ms = kernel_time_ms(torch, fd, pool, args.detector, THR[args.detector])
+    with phase(torch, "roofline_kernel"):
+        k_ms = kernel_time_ms(torch, fd, pool, args.detector, THR[args.detector])
     k_bytes = px_step  # algorithmic: 1 B/px frame read
     kernels = {"corner_or_fast_ms": k_ms, "step_ms": ms_per_step}
     # the remainder of a step is the per-frame selection (one workgroup per frame)
@@ -435,9 +461,11 @@ def main():
     # ---- north-star shape: Shi-Tomasi 1920x1080 batch 256 (kernel roofline) -----------------------
     if not args.no_north_star:
         ns_batch = 256
-        s2, d2, pool2, _ = run_config(torch, fd, dev, "shi_tomasi", 1080, 1920, ns_batch, 2, 200, 20, "noise",
-                                      10, 2, False, seed=99 + rank)
-        kms = kernel_time_ms(torch, fd, pool2, "shi_tomasi", 40.0, reps=10)
+        with phase(torch, "north_star"):
+            s2, d2, pool2, _ = run_config(torch, fd, dev, "shi_tomasi", 1080, 1920, ns_batch, 2, 200, 20, "noise",
+                                          10, 2, False, seed=99 + rank)
+        with phase(torch, "north_star_kernel"):
+            kms = kernel_time_ms(torch, fd, pool2, "shi_tomasi", 40.0, reps=10)
         kb = ns_batch * 1080 * 1920
         ach = kb / (kms * 1e-3) / 1e9
         out["north_star"] = {
@@ -455,18 +483,23 @@ def main():
 
     # ---- BASELINE configs[2]: FAST-12 + BRIEF-256, 1280x720 batch 64 (detect -> describe on device) --
     if not args.no_config3:
-        out["config3_fast_brief"] = run_config3(torch, fd, dev, seed=777 + rank)
+        with phase(torch, "config3_fast_brief"):
+            out["config3_fast_brief"] = run_config3(torch, fd, dev, seed=777 + rank)
 
     # ---- BASELINE configs[4]: SuperPoint, 640x480, 64 frames per GPU --------------------------------
     if not args.no_superpoint:
-        out["config5_superpoint"] = run_superpoint(torch, fd, dev, seed=5151 + rank)
+        with phase(torch, "config5_superpoint"):
+            out["config5_superpoint"] = run_superpoint(torch, fd, dev, seed=5151 + rank)
 
     # ---- BASELINE configs[3]: LSD map, 1920x1080 batch 256 per GPU ----------------------------------
     if not args.no_lsd:
-        out["config4_lsd_map"] = run_lsd(torch, fd, dev, seed=4242 + rank)
-    out["device_copy_gbs"] = copy_bandwidth(torch, dev)
+        with phase(torch, "config4_lsd_map"):
+            out["config4_lsd_map"] = run_lsd(torch, fd, dev, seed=4242 + rank)
+    with phase(torch, "device_copy"):
+        out["device_copy_gbs"] = copy_bandwidth(torch, dev)
     if world == 1:
-        out["end_to_end_host_frames"] = run_end_to_end(torch, fd, args)
+        with phase(torch, "end_to_end"):
+            out["end_to_end_host_frames"] = run_end_to_end(torch, fd, args)
 
     # ---- CPU baseline: the oracle (single thread), bounded sample, rank 0 at N=1 ------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
