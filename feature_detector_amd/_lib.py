@@ -84,7 +84,7 @@ def load() -> ctypes.CDLL:
         "fd_lsd_map": (i32, [P, P, i32, i32, i32, i32, f32, P, P, P, P, i64, P, i32]),
         "fd_brief_compute": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_brief_opts), P, P, i32, P, P, i32]),
         "fd_nn_select": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_nn_opts), P, P, P, i32, P, i32]),
-        "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
+        "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

@@ -147,8 +147,9 @@ struct HeatArgs {
 
 // Bilinear descriptor sampling from the 1/8-resolution descriptor map.
 struct NnDescArgs {
-    const float *map;  // [batch][channels][map_rows][map_cols]
+    const float *map;  // [batch][channels][map_rows][map_cols], or [batch][map_rows][map_cols][channels] (nhwc)
     int batch, channels, map_rows, map_cols;
+    int nhwc;
     const float *xy;        // [batch][stride][2]
     const int32_t *counts;  // [batch] or null (= stride)
     int stride;

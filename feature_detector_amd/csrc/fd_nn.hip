@@ -16,51 +16,83 @@
 namespace fdk {
 namespace {
 
-constexpr int kHeatPerThread = 4;
 constexpr int kHeatBlock = 256;
+constexpr int kHeatRounds = 64;  // pixels per thread: a workgroup covers 16,384 consecutive pixels
+constexpr int kHeatUnroll = 4;   // loads in flight per thread
 
-// One workgroup = kHeatPerThread * 256 consecutive pixels of one frame (coalesced f32 loads).
+constexpr int kHeatStage = 1024;  // candidates a wave stages in LDS before appending them to the list
+
+// One workgroup = kHeatRounds * 256 consecutive pixels of one frame (coalesced f32 loads). Heatmap
+// values cluster in few bins and a frame has many candidates, so neither the list append nor the
+// level-0 histogram may use one global atomic per candidate (same-address atomics serialise): each
+// wave stages its candidates in LDS and appends them with one atomic per flush, and the workgroup's
+// histogram is accumulated in LDS and flushed once (one atomic per non-empty bin).
 __global__ __launch_bounds__(kHeatBlock) void k_heat_candidates(HeatArgs a) {
+    __shared__ uint32_t hist[kHistBins];
+    __shared__ float st_r[kHeatBlock / kWave][kHeatStage];
+    __shared__ uint32_t st_i[kHeatBlock / kWave][kHeatStage];
     const int f = blockIdx.y;
+    const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+    for (int b = tid; b < kHistBins; b += kHeatBlock) hist[b] = 0;
+    __syncthreads();
     const int64_t npx = static_cast<int64_t>(a.rows) * a.cols;
     const float *h = a.heat + static_cast<int64_t>(f) * npx;
-    const int64_t p0 = static_cast<int64_t>(blockIdx.x) * (kHeatPerThread * kHeatBlock) + threadIdx.x;
-    float v[kHeatPerThread];
-#pragma unroll
-    for (int j = 0; j < kHeatPerThread; ++j) {
-        const int64_t p = p0 + j * kHeatBlock;
-        v[j] = p < npx ? h[p] : 0.0f;
-    }
+    const int64_t blk0 = static_cast<int64_t>(blockIdx.x) * (kHeatRounds * kHeatBlock);
     const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * a.rows * a.mask_wpr : nullptr;
     float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
     uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
-#pragma unroll
-    for (int j = 0; j < kHeatPerThread; ++j) {
-        const int64_t p = p0 + j * kHeatBlock;
-        bool ok = p < npx && v[j] > a.thr;  // :133-135 (NaN never passes)
-        int r = 0, c = 0;
-        if (ok) {
-            r = static_cast<int>(p / a.cols);
-            c = static_cast<int>(p - static_cast<int64_t>(r) * a.cols);
-            // CreateMask (:61-68): the kInvalidBoundary outermost rows/columns are 0; prior boxes (:69-71)
-            ok = r >= a.border && r < a.rows - a.border && c >= a.border && c < a.cols - a.border;
-            if (ok && fmask) ok = (fmask[static_cast<int64_t>(r) * a.mask_wpr + (c >> 5)] >> (c & 31)) & 1u;
-        }
-        const uint64_t m = ballot(ok);
-        if (m == 0) continue;
+    int staged = 0;  // wave-uniform
+    auto flush = [&]() {
         uint32_t base = 0;
-        if (lane_id() == 0) base = atomicAdd(&a.list_count[f], static_cast<uint32_t>(popc64(m)));
+        if (lane == 0) base = atomicAdd(&a.list_count[f], static_cast<uint32_t>(staged));
         base = __builtin_amdgcn_readfirstlane(base);
-        if (ok) {
-            const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(base)));
-            if (pos < a.list_cap) {
-                dr[pos] = v[j];
-                di[pos] = static_cast<uint32_t>(p);
+        for (int k = lane; k < staged; k += kWave) {
+            const uint64_t pos = static_cast<uint64_t>(base) + k;
+            if (pos < static_cast<uint64_t>(a.list_cap)) {
+                dr[pos] = st_r[w][k];
+                di[pos] = st_i[w][k];
             }
-            if (v[j] > a.vmax) atomicOr(&a.value_flag[f], 0x80000000u);  // outside the key map: the call fails
-            const uint32_t bin = ((float_key(v[j]) - a.key_base) << a.key_lz) >> 20;
-            atomicAdd(&a.hist0[static_cast<int64_t>(f) * kHistBins + bin], 1u);
         }
+        staged = 0;
+    };
+    bool over = false;
+    for (int r0 = 0; r0 < kHeatRounds; r0 += kHeatUnroll) {
+        float v[kHeatUnroll];
+#pragma unroll
+        for (int j = 0; j < kHeatUnroll; ++j) {
+            const int64_t p = blk0 + static_cast<int64_t>(r0 + j) * kHeatBlock + tid;
+            v[j] = p < npx ? h[p] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < kHeatUnroll; ++j) {
+            const int64_t p = blk0 + static_cast<int64_t>(r0 + j) * kHeatBlock + tid;
+            bool ok = p < npx && v[j] > a.thr;  // :133-135 (NaN never passes)
+            if (ok) {
+                const int r = static_cast<int>(p / a.cols);
+                const int c = static_cast<int>(p - static_cast<int64_t>(r) * a.cols);
+                // CreateMask (:61-68): the kInvalidBoundary outermost rows/columns are 0; prior boxes (:69-71)
+                ok = r >= a.border && r < a.rows - a.border && c >= a.border && c < a.cols - a.border;
+                if (ok && fmask) ok = (fmask[static_cast<int64_t>(r) * a.mask_wpr + (c >> 5)] >> (c & 31)) & 1u;
+            }
+            const uint64_t m = ballot(ok);
+            if (m == 0) continue;
+            if (ok) {
+                const int k = mbcnt64(m, staged);
+                st_r[w][k] = v[j];
+                st_i[w][k] = static_cast<uint32_t>(p);
+                over = over || v[j] > a.vmax;
+                atomicAdd(&hist[((float_key(v[j]) - a.key_base) << a.key_lz) >> 20], 1u);
+            }
+            staged += popc64(m);
+            if (staged > kHeatStage - kWave) flush();
+        }
+    }
+    if (staged) flush();
+    if (__syncthreads_or(over) && tid == 0) atomicOr(&a.value_flag[f], 0x80000000u);  // outside the key map
+    uint32_t *gh = a.hist0 + static_cast<int64_t>(f) * kHistBins;
+    for (int b = tid; b < kHistBins; b += kHeatBlock) {
+        const uint32_t n = hist[b];
+        if (n) atomicAdd(&gh[b], n);
     }
 }
 
@@ -88,11 +120,16 @@ __global__ __launch_bounds__(256) void k_nn_desc(NnDescArgs a) {
     const int64_t plane = static_cast<int64_t>(a.map_rows) * a.map_cols;
     const float *m = a.map + static_cast<int64_t>(f) * a.channels * plane;
     float *o = a.out + slot * a.channels;
+    // element (channel j, row, col): NCHW j * plane + row * cols + col; NHWC (row * cols + col) * C + j
+    const int64_t sj = a.nhwc ? 1 : plane;
+    const int64_t sp = a.nhwc ? a.channels : 1;
+    const int64_t p00 = (static_cast<int64_t>(int_row) * a.map_cols + int_col) * sp;
+    const int64_t dc = sp, dr = static_cast<int64_t>(a.map_cols) * sp;
     for (int j = lane_id(); j < a.channels; j += kWave) {
         float d = 0.0f;
         if (inside) {
-            const float *mp = m + j * plane + static_cast<int64_t>(int_row) * a.map_cols + int_col;
-            d = w0 * mp[0] + w1 * mp[1] + w2 * mp[a.map_cols] + w3 * mp[a.map_cols + 1];  // :188-189
+            const float *mp = m + j * sj + p00;
+            d = w0 * mp[0] + w1 * mp[dc] + w2 * mp[dr] + w3 * mp[dr + dc];  // :188-189
         }
         o[j] = d;
     }
@@ -107,7 +144,9 @@ hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-int heat_blocks_per_frame(int64_t npx) { return static_cast<int>((npx + kHeatPerThread * kHeatBlock - 1) / (kHeatPerThread * kHeatBlock)); }
+int heat_blocks_per_frame(int64_t npx) {
+    return static_cast<int>((npx + kHeatRounds * kHeatBlock - 1) / (kHeatRounds * kHeatBlock));
+}
 
 hipError_t launch_nn_desc(const NnDescArgs &a, hipStream_t s) {
     const int64_t waves = static_cast<int64_t>(a.batch) * a.stride;

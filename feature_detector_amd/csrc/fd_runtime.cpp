@@ -961,8 +961,8 @@ int fd_nn_select(fd_ctx *c, const float *heatmap, int heatmap_on_device, int bat
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, heatmap_on_device);
 }
 
-int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int batch, int channels, int map_rows,
-                      int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
+int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int map_layout, int batch, int channels,
+                      int map_rows, int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
                       int io_on_device) {
     if (!c) return FD_ERR_INVALID;
     if (!map || !xy || !out) return fail(c, FD_ERR_INVALID, "bad arguments");
@@ -972,7 +972,9 @@ int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int batch,
     if (stride == 0) return FD_OK;
     const size_t mapn = static_cast<size_t>(batch) * channels * map_rows * map_cols;
     const size_t slots = static_cast<size_t>(batch) * stride;
+    if (map_layout != FD_MAP_NCHW && map_layout != FD_MAP_NHWC) return fail(c, FD_ERR_INVALID, "unknown map layout");
     fdk::NnDescArgs a{};
+    a.nhwc = map_layout == FD_MAP_NHWC;
     a.batch = batch;
     a.channels = channels;
     a.map_rows = map_rows;

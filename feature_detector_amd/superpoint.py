@@ -108,15 +108,20 @@ def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = No
     if _is_torch_device_tensor(desc_map):
         import torch
 
-        m = desc_map.to(torch.float32).contiguous()
+        m = desc_map.to(torch.float32)
         b, ch, h, w = (int(v) for v in m.shape)
+        # a channels-last map (the network's output) is read in place; anything else as NCHW
+        if m.is_contiguous(memory_format=torch.channels_last) and not m.is_contiguous():
+            layout = 1
+        else:
+            m, layout = m.contiguous(), 0
         xy_t = xy.to(torch.float32).contiguous()
         s = int(xy_t.shape[1])
         cnt_t = None if counts is None else counts.to(torch.int32).contiguous()
         res = out if out is not None else torch.zeros((b, s, ch), dtype=torch.float32, device=m.device)
         _bind_stream(ctx, True)
         rc = _lib.load().fd_nn_descriptors(
-            ctx.ptr, ctypes.c_void_p(m.data_ptr()), 1, b, ch, h, w, ctypes.c_void_p(xy_t.data_ptr()),
+            ctx.ptr, ctypes.c_void_p(m.data_ptr()), 1, layout, b, ch, h, w, ctypes.c_void_p(xy_t.data_ptr()),
             ctypes.c_void_p(cnt_t.data_ptr()) if cnt_t is not None else None, s, ctypes.c_void_p(res.data_ptr()), 1)
         _lib.check(ctx.ptr, rc)
         return res
@@ -128,7 +133,7 @@ def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = No
     res = np.zeros((b, s, ch), np.float32)
     _bind_stream(ctx, False)
     rc = _lib.load().fd_nn_descriptors(
-        ctx.ptr, ctypes.c_void_p(m.ctypes.data), 0, b, ch, h, w, ctypes.c_void_p(xy_h.ctypes.data),
+        ctx.ptr, ctypes.c_void_p(m.ctypes.data), 0, 0, b, ch, h, w, ctypes.c_void_p(xy_h.ctypes.data),
         ctypes.c_void_p(cnt_h.ctypes.data) if cnt_h is not None else None, s, ctypes.c_void_p(res.ctypes.data), 0)
     _lib.check(ctx.ptr, rc)
     return res

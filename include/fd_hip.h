@@ -192,12 +192,15 @@ int fd_nn_select(fd_ctx *ctx, const float *heatmap, int heatmap_on_device, int b
 /*
  * fd_nn_descriptors -- ExtractDescriptorsForSelectedFeatures (nn_feature_point_detector.cpp:163-193):
  * per feature (x, y) in xy [batch][stride][2] (counts as fd_brief_compute), bilinear samples at
- * (y / 8, x / 8) of each of the `channels` planes of map [batch][channels][map_rows][map_cols]
- * (zero outside [0, map_rows-1) x [0, map_cols-1)), into out [batch][stride][channels].
+ * (y / 8, x / 8) of each of the `channels` planes of the descriptor map (zero outside
+ * [0, map_rows-1) x [0, map_cols-1)), into out [batch][stride][channels]. map_layout
+ * FD_MAP_NCHW: [batch][channels][map_rows][map_cols] (the reference's per-channel matrices);
+ * FD_MAP_NHWC: [batch][map_rows][map_cols][channels] (channels-last network output, read in place).
  * xy, counts and out are all device pointers when io_on_device, host pointers otherwise.
  */
-int fd_nn_descriptors(fd_ctx *ctx, const float *map, int map_on_device, int batch, int channels, int map_rows,
-                      int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
+enum fd_map_layout { FD_MAP_NCHW = 0, FD_MAP_NHWC = 1 };
+int fd_nn_descriptors(fd_ctx *ctx, const float *map, int map_on_device, int map_layout, int batch, int channels,
+                      int map_rows, int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
                       int io_on_device);
 
 /* ---- build info --------------------------------------------------------------------------------- */

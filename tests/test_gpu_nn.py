@@ -113,3 +113,22 @@ def test_nn_select_key_range(sp, oracle):
     # the failed call left the control block clean for the next one
     d, cd = sp.nn_select(heat, o)
     assert np.array_equal(cd, ca) and np.array_equal(d, a)
+
+
+def test_nn_descriptors_channels_last_in_place(sp, oracle):
+    """A channels-last device map (the network's layout) is read in place (FD_MAP_NHWC) and gives the
+    same values as the reference's per-channel planes."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(8)
+    m = rng.standard_normal((2, 256, 12, 16)).astype(np.float32)
+    xy = rng.uniform(-4, 130, (2, 40, 2)).astype(np.float32)
+    cnt = torch.tensor([40, 17], dtype=torch.int32, device="cuda")
+    md = torch.from_numpy(m).cuda()
+    xyd = torch.from_numpy(xy).cuda()
+    a = sp.nn_descriptors(md, xyd, cnt)
+    b = sp.nn_descriptors(md.contiguous(memory_format=torch.channels_last), xyd, cnt)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    for f, n in ((0, 40), (1, 17)):
+        exp = oracle.nn_descriptors(m[f], xy[f, :n])
+        assert np.array_equal(b[f, :n].cpu().numpy().view(np.uint32), exp.view(np.uint32))
