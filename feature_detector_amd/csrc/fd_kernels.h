@@ -107,6 +107,8 @@ struct LsdArgs {
     float min_norm;
     float *norm, *angle;
     uint8_t *valid;
+    uint32_t *rowbits;  // [batch][cols-1][chunks][words]: valid rows of each (column, chunk), bit r - r0
+    int words;          // ceil(chunk_h / 32)
     int32_t *col_cnt;   // [batch][cols-1][chunks]
     int32_t *col_base;  // same shape, exclusive scan in column-major order
     int32_t *idx;

@@ -104,14 +104,20 @@ __device__ __forceinline__ float fd_atan2f(float y, float x) {
 }
 
 __device__ __forceinline__ void lsd_tile(const LsdArgs &a, int &f, int &strip, int &chunk) {
-    int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    // wave-uniform (readfirstlane): row/column bounds derived from it stay in SGPRs, and the
+    // per-row bound checks are scalar branches (no exec masking around the DPP moves)
+    int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * 4 + (threadIdx.x >> 6)));
     strip = w % a.strips;
     w /= a.strips;
     chunk = w % a.chunks;
     f = w / a.chunks;
 }
 
-// Pass 1: maps + per (column, row-chunk) valid counts. Lane = one column, walking chunk_h rows.
+// Pass 1: maps + per (column, row-chunk) valid counts and valid-row bitmasks. Lane = one column,
+// walking chunk_h rows in groups of kLsdGroup; the next group's pixel loads are issued before the
+// current group is computed (ping-pong register sets, so no copy on the back edge waits for them).
+constexpr int kLsdGroup = 4;
+
 __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
     int f, strip, chunk;
     lsd_tile(a, f, strip, chunk);
@@ -125,14 +131,8 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
     const bool colw = col <= cols - 2;  // the map has columns [0, cols-2]; outside the scan they are 0
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
     const int64_t mbase = static_cast<int64_t>(f) * (rows - 1) * mc;
+    uint32_t *bits_out = a.rowbits + ((static_cast<int64_t>(f) * mc + col) * a.chunks + chunk) * a.words;
 
-    // I(r, col) and I(r, col+1): col+1 comes from the next lane (lane 63 loads it itself).
-    auto load_pair = [&](int r, uint32_t &p0, uint32_t &p1) {
-        p0 = buf_load_u8(rs, r * cols + col);
-        uint32_t nb = from_right(p0);
-        if (lane == 63) nb = buf_load_u8(rs, r * cols + col + 1);
-        p1 = nb;
-    };
     // Map rows 0 and rows-2 lie outside the scan (:71): written as zeros by the first / last chunk, so
     // every map entry is written exactly once and the host needs no memset.
     auto zero_row = [&](int r) {
@@ -144,29 +144,65 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
     };
     if (chunk == 0) zero_row(0);
     if (r1 == rows - 2) zero_row(rows - 2);
-    uint32_t t0, t1;
-    load_pair(r0, t0, t1);
+
+    // I(r, col) for this lane; lane 63 also loads I(r, col + 1) (the others take it from lane + 1).
+    // Rows past the frame read 0 (buffer range check) and are never used.
+    auto ld = [&](int r, uint32_t &p, uint32_t &e) {
+        p = buf_load_u8(rs, r * cols + col);
+        e = lane == kWave - 1 ? buf_load_u8(rs, r * cols + col + 1) : 0u;
+    };
+    // (the DPP move runs on every lane: under a partial exec mask lane 62 would read a disabled lane 63)
+    auto right = [&](uint32_t p, uint32_t e) {
+        const uint32_t x = from_right(p);
+        return lane == kWave - 1 ? e : x;
+    };
     int cnt = 0;
-    for (int r = r0; r < r1; ++r) {
-        uint32_t b0, b1;
-        load_pair(r + 1, b0, b1);
-        const int ad = static_cast<int>(b1) - static_cast<int>(t0);
-        const int bc = static_cast<int>(t1) - static_cast<int>(b0);
-        const float gx = static_cast<float>(ad + bc) / 2.0f;
-        const float gy = static_cast<float>(ad - bc) / 2.0f;
-        const float nrm = __builtin_sqrtf((gx * gx) + (gy * gy));
-        const bool v = colv && nrm > a.min_norm;
-        float ang = 0.0f;
-        if (v) ang = fd_atan2f(gx, -gy);
-        if (colw) {
-            const int64_t i = mbase + static_cast<int64_t>(r) * mc + col;
-            if (a.norm) a.norm[i] = colv ? nrm : 0.0f;
-            if (a.angle) a.angle[i] = ang;
-            a.valid[i] = v ? 1 : 0;
+    uint32_t word = 0;
+    // one group: rows r .. r+kLsdGroup-1 from pixel rows r .. r+kLsdGroup (P/E[0..kLsdGroup])
+    auto group = [&](int r, const uint32_t (&P)[kLsdGroup + 1], const uint32_t (&E)[kLsdGroup + 1]) {
+#pragma unroll
+        for (int i = 0; i < kLsdGroup; ++i) {
+            const int rr = r + i;
+            if (rr >= r1) break;  // uniform
+            const uint32_t t0 = P[i], t1 = right(P[i], E[i]);
+            const uint32_t b0 = P[i + 1], b1 = right(P[i + 1], E[i + 1]);
+            const int ad = static_cast<int>(b1) - static_cast<int>(t0);  // :76-79
+            const int bc = static_cast<int>(t1) - static_cast<int>(b0);
+            const float gx = static_cast<float>(ad + bc) / 2.0f;  // :80-81
+            const float gy = static_cast<float>(ad - bc) / 2.0f;
+            const float nrm = __builtin_sqrtf((gx * gx) + (gy * gy));  // :82
+            const bool v = colv && nrm > a.min_norm;                  // :83
+            float ang = 0.0f;
+            if (v) ang = fd_atan2f(gx, -gy);  // :85
+            if (colw) {
+                const int64_t idx = mbase + static_cast<int64_t>(rr) * mc + col;
+                if (a.norm) a.norm[idx] = colv ? nrm : 0.0f;
+                if (a.angle) a.angle[idx] = ang;
+                a.valid[idx] = v ? 1 : 0;
+            }
+            cnt += v ? 1 : 0;
+            word |= static_cast<uint32_t>(v) << ((rr - r0) & 31);
         }
-        cnt += v ? 1 : 0;
-        t0 = b0;
-        t1 = b1;
+        // rows r0 + 32k .. r0 + 32k + 31 share a bitmask word (kLsdGroup divides 32)
+        const int done = r + kLsdGroup - r0;
+        if ((done & 31) == 0 || r + kLsdGroup >= r1) {
+            if (colv) bits_out[(done - 1) >> 5] = word;
+            word = 0;
+        }
+    };
+    static_assert(32 % kLsdGroup == 0, "bitmask words hold whole groups");
+    uint32_t A[kLsdGroup + 1], AE[kLsdGroup + 1], B[kLsdGroup + 1], BE[kLsdGroup + 1];
+#pragma unroll
+    for (int i = 0; i <= kLsdGroup; ++i) ld(r0 + i, A[i], AE[i]);
+    for (int r = r0; r < r1; r += 2 * kLsdGroup) {
+        // B: rows r+G .. r+2G (its first row is A's last: reloaded, a cache hit, to keep sets disjoint)
+#pragma unroll
+        for (int i = 0; i <= kLsdGroup; ++i) ld(r + kLsdGroup + i, B[i], BE[i]);
+        group(r, A, AE);
+        if (r + kLsdGroup >= r1) break;
+#pragma unroll
+        for (int i = 0; i <= kLsdGroup; ++i) ld(r + 2 * kLsdGroup + i, A[i], AE[i]);
+        group(r + kLsdGroup, B, BE);
     }
     if (colv) a.col_cnt[(static_cast<int64_t>(f) * mc + col) * a.chunks + chunk] = cnt;
 }
@@ -206,7 +242,8 @@ __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
     if (tid == 0) a.counts[f] = carry;
 }
 
-// Pass 3: scatter valid map indices in scan order.
+// Pass 3: scatter valid map indices in scan order, from the per-(column, chunk) row bitmasks of
+// pass 1 (a few words per lane instead of re-reading the valid map row by row).
 __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     int f, strip, chunk;
     lsd_tile(a, f, strip, chunk);
@@ -217,13 +254,17 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     if (!(col >= 1 && col <= cols - 3)) return;
     const int r0 = 1 + chunk * a.chunk_h;
     const int r1 = min(r0 + a.chunk_h, rows - 2);
-    const int64_t mbase = static_cast<int64_t>(f) * (rows - 1) * mc;
-    int64_t pos = a.col_base[(static_cast<int64_t>(f) * mc + col) * a.chunks + chunk];
+    const int64_t cc = (static_cast<int64_t>(f) * mc + col) * a.chunks + chunk;
+    int64_t pos = a.col_base[cc];
+    const uint32_t *bits = a.rowbits + cc * a.words;
     int32_t *out = a.idx + static_cast<int64_t>(f) * a.idx_cap;
-    for (int r = r0; r < r1; ++r) {
-        const int64_t i = static_cast<int64_t>(r) * mc + col;
-        if (a.valid[mbase + i]) {
-            if (pos < a.idx_cap) out[pos] = static_cast<int32_t>(i);
+    const int nw = (r1 - r0 + 31) >> 5;
+    for (int w = 0; w < nw; ++w) {
+        uint32_t m = bits[w];
+        while (m) {
+            const int rr = r0 + 32 * w + __builtin_ctz(m);
+            m &= m - 1u;
+            if (pos < a.idx_cap) out[pos] = static_cast<int32_t>(static_cast<int64_t>(rr) * mc + col);
             ++pos;
         }
     }

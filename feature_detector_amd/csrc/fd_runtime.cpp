@@ -39,7 +39,7 @@ struct fd_ctx {
     DevBuf selctl, pre_keys;
     bool sel_dirty = true;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
-    DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts;
+    DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts, l_bits;
     DevBuf b_uv, b_counts, b_bits, b_valid;
     DevBuf n_heat, n_map, n_xy, n_counts, n_out;
     DevBuf dbg;
@@ -436,7 +436,7 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->out_counts, &c->grid,     &c->dbg,
                       &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
-                      &c->l_idx,    &c->l_counts, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
+                      &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out};
     for (DevBuf *b : bufs) release(*b);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -803,6 +803,9 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         const size_t ncnt = static_cast<size_t>(batch) * mc * a.chunks;
         FD_HIP_TRY(c, ensure(c->l_cnt, sizeof(int32_t) * ncnt));
         FD_HIP_TRY(c, ensure(c->l_base, sizeof(int32_t) * ncnt));
+        a.words = (a.chunk_h + 31) / 32;
+        FD_HIP_TRY(c, ensure(c->l_bits, sizeof(uint32_t) * ncnt * a.words));
+        a.rowbits = as<uint32_t>(c->l_bits);
         a.col_cnt = as<int32_t>(c->l_cnt);
         a.col_base = as<int32_t>(c->l_base);
         a.idx = di;
