@@ -76,4 +76,24 @@ __device__ __forceinline__ uint32_t float_key(float f) {
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Correctly rounded f32 sqrt of two values that are each 0 or >= 2^-60, in 4.5 issue slots per value
+// (one transcendental + four packed ops): y = rsq(x) (v_rsq_f32, ~1 ulp), s0 = x*y, one Newton step
+// s = s0 + (x - s0*s0) * y/2 with the residual exact (fma) and the correction rounded once (fma).
+// Not correctly rounded by construction (the correction's error, ~2^-20 ulp, exceeds the 2^-29 ulp by
+// which a float's square root can approach a rounding midpoint), so it is verified exhaustively: every
+// float from 2^-60 up, and 0, against the IEEE sqrt (tools/calib/sqrt_exhaustive.hip, run by
+// tests/test_gpu_points.py). The Shi-Tomasi radicand d*d + 4b*b is 0 or >= 2^-54 (b is 0 or |b| >= 1/9,
+// a != c differ by at least ulp(1/9) = 2^-27). The tiny addend keeps rsq(0) finite (s0 = 0*y = 0,
+// s = 0) and leaves every x >= 2^-54 unchanged.
+__device__ __forceinline__ f2 sqrt_rn_rsq2(f2 x) {
+    const f2 xt = x + 0x1p-110f;
+    const f2 y = {__builtin_amdgcn_rsqf(xt.x), __builtin_amdgcn_rsqf(xt.y)};
+    const f2 s0 = x * y;
+    const f2 e = __builtin_elementwise_fma(-s0, s0, x);
+    const f2 h = y * 0.5f;
+    return __builtin_elementwise_fma(e, h, s0);
+}
+
 }  // namespace fdk

@@ -144,24 +144,7 @@ __device__ __forceinline__ void hist_flush(const uint32_t *h, uint32_t *g) {
 // Two pixels' float math at a time: <2 x float> arithmetic compiles to v_pk_mul_f32 / v_pk_add_f32 /
 // v_pk_fma_f32, which round each lane exactly like the scalar op (the kernel is VALU-issue bound, and
 // a packed op retires two pixels' worth of one reference operation per issue slot).
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-// Correctly rounded f32 sqrt of two values that are each 0 or normal: v_sqrt_f32 (within 1 ulp)
-// followed by the two fma residual corrections of the compiler's own IEEE expansion, minus its
-// denormal pre-scaling and inf/nan class fix-up. The Shi-Tomasi radicand d*d + 4b*b is either 0 or
-// >= 2^-54: b is 0 or |b| >= 1/9, and a != c differ by at least ulp(1/9) = 2^-27. For x == 0 the
-// s-1ulp candidate is a NaN whose residual compares false and the s+1ulp residual is -0, so 0 results.
-__device__ __forceinline__ f2 sqrt_rn_normal2(f2 x) {
-    const f2 s = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
-    const f2 sdn = {__int_as_float(__float_as_int(s.x) - 1), __int_as_float(__float_as_int(s.y) - 1)};
-    const f2 sup = {__int_as_float(__float_as_int(s.x) + 1), __int_as_float(__float_as_int(s.y) + 1)};
-    const f2 rdn = __builtin_elementwise_fma(-sdn, s, x);
-    const f2 rup = __builtin_elementwise_fma(-sup, s, x);
-    f2 r;
-    r.x = rup.x > 0.0f ? sup.x : (rdn.x <= 0.0f ? sdn.x : s.x);
-    r.y = rup.y > 0.0f ? sup.y : (rdn.y <= 0.0f ? sdn.y : s.y);
-    return r;
-}
+// sqrt_rn_rsq2 (correctly rounded sqrt on the reciprocal square root) lives in fd_device.h.
 
 // Stored responses of two pixels (responses_ semantics: 0 unless written), from exact integer tensor
 // sums. Same operations in the same order as the reference; only the issue is paired.
@@ -175,34 +158,42 @@ constexpr uint32_t kBiasSq = 0xB3000000u;  // 9 * kBiasSq == 0x4B000000 (mod 2^3
 constexpr uint32_t kBiasXy = 0x41400000u;  // 9 * kBiasXy == 0x4B400000 (mod 2^32)
 static_assert(9u * kBiasSq == 0x4B000000u && 9u * kBiasXy == 0x4B400000u, "bias");
 
-template <int KIND>
+// G1 (detect mode with thr >= 0): only the pre-check gates the stored value, so a pixel whose
+// response is <= thr keeps its response instead of 0. The NMS that reads these values tests
+// x > max(thr, neighbours): with thr >= 0 a kept response <= thr acts exactly like the reference's 0
+// there (as a centre it fails x > thr, as a neighbour max(thr, r) == thr == max(thr, 0)), and every
+// emitted candidate has x > thr, i.e. the reference's stored value. Saves a compare per pixel.
+template <int KIND, bool G1>
 __device__ __forceinline__ f2 corner_response2(uint32_t sxx0, uint32_t sxx1, uint32_t syy0, uint32_t syy1,
                                                uint32_t sxy0, uint32_t sxy1, float thr) {
     const f2 fxx = f2{__uint_as_float(sxx0), __uint_as_float(sxx1)} - 8388608.0f;
     const f2 fyy = f2{__uint_as_float(syy0), __uint_as_float(syy1)} - 8388608.0f;
     const f2 fxy = f2{__uint_as_float(sxy0), __uint_as_float(sxy1)} - 12582912.0f;
-    f2 res;
+    f2 res, gate, r;
     if constexpr (KIND == 0) {  // Harris, feature_point_harris_detector.cpp:95-103
         const f2 trace = fxx + fyy;
-        const f2 gate = ((trace * trace) * 0.21f) * kInvCnt2;
-        const f2 r = (((fxx * fyy) - (fxy * fxy)) - ((kHarrisAlpha * trace) * trace)) * kInvCnt2;
-        res.x = (gate.x > thr && r.x > thr) ? r.x : 0.0f;
-        res.y = (gate.y > thr && r.y > thr) ? r.y : 0.0f;
+        gate = ((trace * trace) * 0.21f) * kInvCnt2;
+        r = (((fxx * fyy) - (fxy * fxy)) - ((kHarrisAlpha * trace) * trace)) * kInvCnt2;
     } else {  // Shi-Tomasi, feature_point_shi_tomas_detector.cpp:94-103
         const f2 a = fxx * kInvCnt;
         const f2 c = fyy * kInvCnt;
-        const f2 ac = a + c;
+        gate = a + c;
         const f2 b = fxy * kInvCnt;
         const f2 d = a - c;
-        const f2 common = sqrt_rn_normal2((d * d) + ((4.0f * b) * b));
-        const f2 r = (ac + common) * 0.5f;
-        res.x = (ac.x > thr && r.x > thr) ? r.x : 0.0f;
-        res.y = (ac.y > thr && r.y > thr) ? r.y : 0.0f;
+        const f2 common = sqrt_rn_rsq2((d * d) + ((4.0f * b) * b));
+        r = (gate + common) * 0.5f;
+    }
+    if constexpr (G1) {
+        res.x = gate.x > thr ? r.x : 0.0f;
+        res.y = gate.y > thr ? r.y : 0.0f;
+    } else {
+        res.x = (gate.x > thr && r.x > thr) ? r.x : 0.0f;
+        res.y = (gate.y > thr && r.y > thr) ? r.y : 0.0f;
     }
     return res;
 }
 
-template <int KIND, bool RASTER, bool MASKED, bool ALIGNED>
+template <int KIND, bool RASTER, bool MASKED, bool ALIGNED, bool G1>
 __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, int tx, Sink &sk);
 
 // ---------------------------------------------------------------------------------------------------
@@ -210,7 +201,7 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
 // c0 = tx*kTileW + 4(l-1) .. c0+3 and walks the rows keeping 3-row sliding windows in registers:
 // pixels (+ DPP halo dwords), horizontal tensor sums, responses.
 // ---------------------------------------------------------------------------------------------------
-template <int KIND, bool RASTER, bool MASKED, bool ALIGNED>
+template <int KIND, bool RASTER, bool MASKED, bool ALIGNED, bool G1>
 __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
     __shared__ DetectLds lds_all[1];
     int f, ty, tx;
@@ -221,14 +212,14 @@ __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
         sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0};
         if (a.hist0) hist_clear(lds_all[0].hist);
     }
-    if (active) corner_tile<KIND, RASTER, MASKED, ALIGNED>(a, f, ty, tx, sk);
+    if (active) corner_tile<KIND, RASTER, MASKED, ALIGNED, G1>(a, f, ty, tx, sk);
     if constexpr (!RASTER) {
         if (active) sink_flush(sk, a, f);
         if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
     }
 }
 
-template <int KIND, bool RASTER, bool MASKED, bool ALIGNED>
+template <int KIND, bool RASTER, bool MASKED, bool ALIGNED, bool G1>
 __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, int tx, Sink &sk) {
     const int lane = lane_id();
     const int rows = a.rows, cols = a.cols;
@@ -315,8 +306,8 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
                 syy[m] = add3u(hyy[s][m], hyy[su][m], hyy[sc][m]);
                 sxy[m] = add3u(hxy[s][m], hxy[su][m], hxy[sc][m]);
             }
-            const f2 r01 = corner_response2<KIND>(sxx[0], sxx[1], syy[0], syy[1], sxy[0], sxy[1], a.thr);
-            const f2 r23 = corner_response2<KIND>(sxx[2], sxx[3], syy[2], syy[3], sxy[2], sxy[3], a.thr);
+            const f2 r01 = corner_response2<KIND, G1>(sxx[0], sxx[1], syy[0], syy[1], sxy[0], sxy[1], a.thr);
+            const f2 r23 = corner_response2<KIND, G1>(sxx[2], sxx[3], syy[2], syy[3], sxy[2], sxy[3], a.thr);
             const float r[4] = {r01.x, r01.y, r23.x, r23.y};
             if (!MASKED && rowv && tile_interior) {  // wave-uniform: no per-pixel masking needed
 #pragma unroll
@@ -666,10 +657,17 @@ static inline int blocks_for_waves(const PointsArgs &a) {
 hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s) {
     const dim3 grid(blocks_for_waves(a)), block(256);
     const bool masked = a.mask != nullptr, aligned = a.aligned4 != 0;
-#define FD_CORNER(K, RS, M)                                                                  \
-    do {                                                                                     \
-        if (aligned) hipLaunchKernelGGL((k_corner<K, RS, M, true>), grid, block, 0, s, a);  \
-        else hipLaunchKernelGGL((k_corner<K, RS, M, false>), grid, block, 0, s, a);         \
+    const bool g1 = !raster && a.thr >= 0.0f;  // single-gate stores (see corner_response2)
+#define FD_CORNER_A(K, RS, M, G)                                                                \
+    do {                                                                                        \
+        if (aligned) hipLaunchKernelGGL((k_corner<K, RS, M, true, G>), grid, block, 0, s, a);  \
+        else hipLaunchKernelGGL((k_corner<K, RS, M, false, G>), grid, block, 0, s, a);         \
+    } while (0)
+#define FD_CORNER(K, RS, M)                                      \
+    do {                                                         \
+        if (RS) FD_CORNER_A(K, RS, M, false);                    \
+        else if (g1) FD_CORNER_A(K, false, M, true);             \
+        else FD_CORNER_A(K, false, M, false);                    \
     } while (0)
     if (kind == 0) {
         if (raster) { if (masked) FD_CORNER(0, true, true); else FD_CORNER(0, true, false); }
@@ -679,6 +677,7 @@ hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t
         else { if (masked) FD_CORNER(1, false, true); else FD_CORNER(1, false, false); }
     }
 #undef FD_CORNER
+#undef FD_CORNER_A
     return hipGetLastError();
 }
 

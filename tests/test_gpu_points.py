@@ -252,3 +252,15 @@ def test_point_response_and_append(fd, oracle, name):
         assert np.array_equal(gi[0::2], gi[1::2])
     with pytest.raises(ValueError):
         fd.point_response(name, dev, THR[name], append=True)
+
+
+def test_sqrt_rsq_exhaustive():
+    # The Shi-Tomasi kernel's sqrt (fd_device.h sqrt_rn_rsq2: v_rsq_f32 + one Newton step) equals the
+    # correctly rounded sqrt on every float of its domain ({0} U [2^-60, FLT_MAX], ~1.6e9 values).
+    import os
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "calib", "sqrt_exhaustive")
+    assert os.path.exists(exe), "build tools/calib first (__graft_entry__.build())"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and " 0 mismatches" in out.stdout, out.stdout + out.stderr

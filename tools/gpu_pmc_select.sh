@@ -1,7 +1,14 @@
+# SQ / SQC counters of k_select at the headline shape (Harris 640x480 batch 1), one pass per group.
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmcs
-timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d gpurun_out/pmcs/a -o a -- python3 tools/k1_batch1.py detect > gpurun_out/pmcs/a.log 2>&1
-timeout -k 10 200 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmcs/b -o b -- python3 tools/k1_batch1.py detect > gpurun_out/pmcs/b.log 2>&1
+run() {
+  timeout -s KILL 90 rocprofv3 --pmc $2 --output-format csv -d gpurun_out/pmcs/$1 -o $1 -- python3 tools/k1_batch1.py detect > gpurun_out/pmcs/$1.log 2>&1
+  f=$(find gpurun_out/pmcs/$1 -name '*counter_collection.csv' | head -1)
+  for c in $2; do python3 tools/pmc_summary.py "$f" $c | grep -i select || true; done
+}
+run a "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
+run b "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_IFETCH SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH"
+run c "SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_MISSES_DUPLICATE"
 echo ok

@@ -11,7 +11,7 @@ for r in csv.DictReader(open(path)):
     if r["Counter_Name"] != ctr:
         continue
     per[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
-    names[int(r["Dispatch_Id"])] = r["Kernel_Name"].split("(")[0][-60:]
+    names[int(r["Dispatch_Id"])] = r["Kernel_Name"].replace("(anonymous namespace)", "").split("(")[0][-60:]
 agg = collections.defaultdict(list)
 for d, v in per.items():
     agg[names[d]].append(v)
