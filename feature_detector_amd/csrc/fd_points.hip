@@ -166,21 +166,25 @@ static_assert(9u * kBiasSq == 0x4B000000u && 9u * kBiasXy == 0x4B400000u, "bias"
 template <int KIND, bool G1>
 __device__ __forceinline__ f2 corner_response2(uint32_t sxx0, uint32_t sxx1, uint32_t syy0, uint32_t syy1,
                                                uint32_t sxy0, uint32_t sxy1, float thr) {
-    const f2 fxx = f2{__uint_as_float(sxx0), __uint_as_float(sxx1)} - 8388608.0f;
-    const f2 fyy = f2{__uint_as_float(syy0), __uint_as_float(syy1)} - 8388608.0f;
+    const f2 bxx = f2{__uint_as_float(sxx0), __uint_as_float(sxx1)};  // 2^23 + Sxx, exactly
+    const f2 byy = f2{__uint_as_float(syy0), __uint_as_float(syy1)};
     const f2 fxy = f2{__uint_as_float(sxy0), __uint_as_float(sxy1)} - 12582912.0f;
     f2 res, gate, r;
     if constexpr (KIND == 0) {  // Harris, feature_point_harris_detector.cpp:95-103
+        const f2 fxx = bxx - 8388608.0f, fyy = byy - 8388608.0f;
         const f2 trace = fxx + fyy;
         gate = ((trace * trace) * 0.21f) * kInvCnt2;
         r = (((fxx * fyy) - (fxy * fxy)) - ((kHarrisAlpha * trace) * trace)) * kInvCnt2;
     } else {  // Shi-Tomasi, feature_point_shi_tomas_detector.cpp:94-103
-        const f2 a = fxx * kInvCnt;
-        const f2 c = fyy * kInvCnt;
+        // a = fl(Sxx * k) as one fma on the biased sum: bxx*k - 2^23*k is (bxx - 2^23)*k = Sxx*k
+        // exactly before the fma's single rounding (2^23*k is exact: a power-of-two multiple of k).
+        const f2 a = __builtin_elementwise_fma(bxx, f2{kInvCnt, kInvCnt}, f2{-8388608.0f * kInvCnt, -8388608.0f * kInvCnt});
+        const f2 c = __builtin_elementwise_fma(byy, f2{kInvCnt, kInvCnt}, f2{-8388608.0f * kInvCnt, -8388608.0f * kInvCnt});
         gate = a + c;
         const f2 b = fxy * kInvCnt;
         const f2 d = a - c;
-        const f2 common = sqrt_rn_rsq2((d * d) + ((4.0f * b) * b));
+        // (4b)*b = 4*fl(b*b) exactly, so dd + fl(fl(4b)*b) is one fma of b*b with 4
+        const f2 common = sqrt_rn_rsq2(__builtin_elementwise_fma(b * b, f2{4.0f, 4.0f}, d * d));
         r = (gate + common) * 0.5f;
     }
     if constexpr (G1) {
