@@ -15,6 +15,7 @@
 // host reports as an error instead of a hang or an out-of-bounds access.
 #include "fd_device.h"
 #include "fd_kernels.h"
+#include "fd_gather.h"
 
 namespace fdk {
 
@@ -54,12 +55,12 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 // injective on the candidates' response range; see SelectArgs::key_base), then ~idx so that equal
 // responses order by ascending raster index.
 __device__ __forceinline__ uint32_t map_key32(float resp, const SelectArgs &a) {
-    return (float_key(resp) - a.key_base) << a.key_lz;
+    return sel_key32(resp, a.key_base, a.key_lz);
 }
 // (tie_idx_desc: idx itself, so that equal responses order by descending raster index, the order in
 // which SuperPoint's std::multimap is walked from crbegin, nn_feature_point_detector.cpp:144.)
 __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const SelectArgs &a) {
-    return (static_cast<uint64_t>(map_key32(resp, a)) << 32) | static_cast<uint64_t>(a.tie_idx_desc ? idx : ~idx);
+    return sel_key64(resp, idx, a.key_base, a.key_lz, a.tie_idx_desc);
 }
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
@@ -679,101 +680,14 @@ __device__ __forceinline__ void finish_frame(const SelectArgs &a, const int f) {
 // their slice of the list to pre_keys. k_select, the next kernel, reads them: the kernel boundary is
 // the visibility point, so no hand-off happens inside either kernel.
 __global__ __launch_bounds__(1024) void k_gather(SelectArgs a) {
-    __shared__ uint32_t S[kHistBins + 1];
-    __shared__ uint32_t wtot[16];
+    __shared__ GatherLds L;
     const int G = a.gather_groups;
     const int f = blockIdx.x / G, g = blockIdx.x % G;
-    const int tid = threadIdx.x, nthr = blockDim.x, lane = lane_id(), wave = tid >> 6;
-    const int64_t n = min(static_cast<int64_t>(a.list_count[f]), a.list_cap);
-    const int64_t s0 = n * g / G, s1 = n * (g + 1) / G;
-    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
-    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
-    // this slice's responses, in flight during the histogram scan (slices <= kRegGather * nthr)
-    float rr[kRegGather];
-    const bool fits = s1 - s0 <= static_cast<int64_t>(kRegGather) * nthr;
-#pragma unroll
-    for (int k = 0; k < kRegGather; ++k)
-        rr[k] = (fits && s1 > s0) ? lresp[min(s0 + tid + static_cast<int64_t>(k) * nthr, s1 - 1)] : 0.0f;
-    const uint32_t *h0 = a.hist0 + static_cast<int64_t>(f) * kHistBins;
-    for (int b = tid; b < kHistBins; b += nthr) S[b] = h0[b];
-    __syncthreads();
-    {  // in-place suffix sums (4 bins per thread)
-        const int b0 = tid * 4;
-        uint32_t v[4], sacc = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sacc += (v[q] = S[b0 + q]);
-        uint32_t incl = sacc;
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint32_t t = __shfl_down(incl, o);
-            if (lane + o < kWave) incl += t;
-        }
-        if (lane == 0) wtot[wave] = incl;
-        __syncthreads();
-        uint32_t after = 0;
-        for (int q = wave + 1; q < nthr / kWave; ++q) after += wtot[q];
-        uint32_t run = incl - sacc + after;
-#pragma unroll
-        for (int q = 3; q >= 0; --q) {
-            run += v[q];
-            S[b0 + q] = run;
-        }
-        if (tid == 0) S[kHistBins] = 0;
-        __syncthreads();
-    }
-    int lo = 0, hi = kHistBins;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (S[mid] <= static_cast<uint32_t>(kSelectChunk)) hi = mid; else lo = mid + 1;
-    }
-    if (lo >= kHistBins || S[lo] == 0) return;  // top bin alone exceeds a chunk (k_select descends)
-    const uint32_t k32lo = static_cast<uint32_t>(lo) << 20;
-    uint64_t *pk = a.pre_keys + static_cast<int64_t>(f) * kSelectChunk;
-    __shared__ uint32_t wg_base;
-    // One reservation per workgroup and round: hits counted per thread (bit mask), placed by a block
-    // prefix, then a single atomic on the frame's counter.
-    auto emit = [&](const float (&r)[kRegGather], int64_t base) {
-        uint32_t hm = 0;
-#pragma unroll
-        for (int k = 0; k < kRegGather; ++k) {
-            const int64_t i = base + tid + static_cast<int64_t>(k) * nthr;
-            hm |= static_cast<uint32_t>(i < s1 && map_key32(r[k], a) >= k32lo) << k;
-        }
-        const uint32_t cntt = __popc(hm);
-        uint32_t incl = cntt;
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
-        }
-        if (lane == kWave - 1) wtot[wave] = incl;
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        for (int q = 0; q < nthr / kWave; ++q) {
-            const uint32_t wq = wtot[q];
-            before += q < wave ? wq : 0u;
-            total += wq;
-        }
-        if (tid == 0) wg_base = total ? atomicAdd(&a.pre_count[f], total) : 0u;
-        __syncthreads();
-        uint32_t pos = wg_base + before + incl - cntt;
-        while (hm) {
-            const int k = __builtin_ctz(hm);
-            hm &= hm - 1u;
-            const int64_t i = base + tid + static_cast<int64_t>(k) * nthr;
-            if (pos < static_cast<uint32_t>(kSelectChunk)) pk[pos] = make_key(r[k], lidx[i], a);
-            ++pos;
-        }
-        __syncthreads();  // wtot / wg_base reuse
-    };
-    if (fits) {
-        emit(rr, s0);
-    } else {
-        for (int64_t base = s0; base < s1; base += static_cast<int64_t>(kRegGather) * nthr) {
-            float r2[kRegGather];
-#pragma unroll
-            for (int k = 0; k < kRegGather; ++k) r2[k] = lresp[min(base + tid + static_cast<int64_t>(k) * nthr, s1 - 1)];
-            emit(r2, base);
-        }
-    }
+    const GatherView v{a.list_resp + static_cast<int64_t>(f) * a.list_cap, a.list_idx + static_cast<int64_t>(f) * a.list_cap,
+                       min(static_cast<int64_t>(a.list_count[f]), a.list_cap), a.hist0 + static_cast<int64_t>(f) * kHistBins,
+                       a.key_base, a.key_lz, a.tie_idx_desc, a.pre_keys + static_cast<int64_t>(f) * kSelectChunk,
+                       a.pre_count + f};
+    gather_first_chunk<1024>(v, g, G, L);
 }
 
 __global__ __launch_bounds__(kSelectThreads) void k_select(SelectArgs a) {
