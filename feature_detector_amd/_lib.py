@@ -6,7 +6,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libfdhip.so")
+LIB_PATH = os.environ.get("FD_LIB_PATH") or os.path.join(LIB_DIR, "libfdhip.so")  # (override: A/B of builds)
 CSRC = os.path.join(HERE, "csrc")
 
 FD_OK, FD_ERR_INVALID, FD_ERR_HIP, FD_ERR_CAPACITY = 0, 1, 2, 3

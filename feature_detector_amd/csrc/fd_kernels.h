@@ -104,6 +104,8 @@ struct LsdArgs {
     const uint8_t *frames;
     int batch, rows, cols;
     int strips, chunks, chunk_h;
+    int strips4;   // k_lsd_map strips of 256 columns (4 per lane); strips: 64-column strips (scatter)
+    int aligned4;  // cols % 4 == 0 and 4-byte aligned frames: whole-dword row loads
     float min_norm;
     float *norm, *angle;
     uint8_t *valid;

@@ -113,81 +113,194 @@ __device__ __forceinline__ void lsd_tile(const LsdArgs &a, int &f, int &strip, i
     f = w / a.chunks;
 }
 
-// Pass 1: maps + per (column, row-chunk) valid counts and valid-row bitmasks. Lane = one column,
-// walking chunk_h rows in groups of kLsdGroup; the next group's pixel loads are issued before the
-// current group is computed (ping-pong register sets, so no copy on the back edge waits for them).
 constexpr int kLsdGroup = 4;
 
-__global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
-    int f, strip, chunk;
-    lsd_tile(a, f, strip, chunk);
-    if (f >= a.batch) return;
+// Pass 1: maps + per (column, row-chunk) valid counts and valid-row bitmasks. A wave owns a strip of
+// 256 map columns (4 per lane, read as one dword per lane and row; the fifth column comes from the
+// right neighbour lane by DPP, lane 63 loads it) and walks chunk_h rows. Every map entry is written
+// exactly once per call (dword-per-lane stores of 4 columns); the angle map first gets 0 for the whole
+// row, then the valid pixels' angles: their (gx, gy) are queued in LDS and atan2f runs on full waves
+// of 64 queued pixels (on ~3 % of the pixels of a structured frame a per-row branch would run the
+// whole atan2f for most rows, VALU-bound; compacted it is a small fraction of the row work).
+constexpr int kLsdQueue = 64 + 256;  // queued valid pixels per wave: < 64 left + one row (256 columns)
+
+struct LsdQueue {
+    uint32_t sd[4][kLsdQueue];   // (s = ad + bc, d = ad - bc) as two int16
+    uint32_t idx[4][kLsdQueue];  // map index in the frame
+};
+
+template <bool ALIGNED>
+__device__ __forceinline__ uint32_t lsd_load4(__amdgpu_buffer_rsrc_t r, int32_t off) {
+    if constexpr (ALIGNED) return buf_load_u32(r, off);
+    return buf_load_u8(r, off) | (buf_load_u8(r, off + 1) << 8) | (buf_load_u8(r, off + 2) << 16) |
+           (buf_load_u8(r, off + 3) << 24);
+}
+
+// atan2f(gx, -gy) (:85) of the queued pixels, 64 at a time while at least `keep_below` remain (0 at
+// the end: all), written into the angle map. One out-of-line copy: the atan2f body (correctly rounded
+// divisions included) is large, and a copy per unrolled row would not fit the instruction cache.
+__device__ __noinline__ int lsd_drain(const uint32_t *qsd, const uint32_t *qidx, int qn, int keep_below, float *amap) {
     const int lane = lane_id();
+    while (qn >= keep_below && qn > 0) {
+        const int take = min(qn, kWave);
+        if (lane < take) {
+            const uint32_t e = qsd[qn - take + lane];
+            const int sv = static_cast<int16_t>(e & 0xFFFFu), dv = static_cast<int16_t>(e >> 16);
+            const float gx = static_cast<float>(sv) / 2.0f;  // :80-81
+            const float gy = static_cast<float>(dv) / 2.0f;
+            amap[qidx[qn - take + lane]] = fd_atan2f(gx, -gy);
+        }
+        qn -= take;
+    }
+    return qn;
+}
+
+// INTERIOR: every column of the strip is scanned ([1, cols-3]) and present in the map: no per-column
+// masks, and the maps are written with buffer stores at 32-bit offsets (no 64-bit address math).
+template <bool ALIGNED, bool INTERIOR>
+__device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, const int strip, const int chunk,
+                                             LsdQueue &Q) {
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    uint32_t *const qsd = Q.sd[wv];
+    uint32_t *const qidx = Q.idx[wv];
     const int rows = a.rows, cols = a.cols, mc = cols - 1;
-    const int col = strip * kWave + lane;
+    const int c0 = strip * 256 + 4 * lane;
     const int r0 = 1 + chunk * a.chunk_h;
     const int r1 = min(r0 + a.chunk_h, rows - 2);  // rows [r0, r1) within [1, rows-3]
-    const bool colv = col >= 1 && col <= cols - 3;
-    const bool colw = col <= cols - 2;  // the map has columns [0, cols-2]; outside the scan they are 0
+    bool colv[4], colw[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        colv[m] = c0 + m >= 1 && c0 + m <= cols - 3;  // scanned columns (:72)
+        colw[m] = c0 + m <= cols - 2;                 // map columns [0, cols-2]
+    }
+    const bool full = c0 + 3 <= cols - 2;  // all four map columns exist: one store per map
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
     const int64_t mbase = static_cast<int64_t>(f) * (rows - 1) * mc;
-    uint32_t *bits_out = a.rowbits + ((static_cast<int64_t>(f) * mc + col) * a.chunks + chunk) * a.words;
+    float *const amap = a.angle ? a.angle + mbase : nullptr;
+    const uint32_t mbytes = static_cast<uint32_t>(rows - 1) * static_cast<uint32_t>(mc);
+    const auto rn = make_rsrc(a.norm ? a.norm + mbase : nullptr, a.norm ? 4 * mbytes : 0u);
+    const auto ra = make_rsrc(amap, amap ? 4 * mbytes : 0u);
+    const auto rv = make_rsrc(a.valid + mbase, mbytes);
 
-    // Map rows 0 and rows-2 lie outside the scan (:71): written as zeros by the first / last chunk, so
-    // every map entry is written exactly once and the host needs no memset.
-    auto zero_row = [&](int r) {
-        if (!colw) return;
-        const int64_t i = mbase + static_cast<int64_t>(r) * mc + col;
-        if (a.norm) a.norm[i] = 0.0f;
-        if (a.angle) a.angle[i] = 0.0f;
-        a.valid[i] = 0;
+    auto put = [&](int r, const float (&nv)[4], const float (&av)[4], uint32_t vb) {
+        if constexpr (INTERIOR) {
+            // (null maps: a zero-range resource drops the stores)
+            const int o = r * mc + c0;  // < 2^31: checked on the host
+            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u4{__float_as_uint(nv[0]), __float_as_uint(nv[1]), __float_as_uint(nv[2]), __float_as_uint(nv[3])}, rn,
+                4 * o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u4{__float_as_uint(av[0]), __float_as_uint(av[1]), __float_as_uint(av[2]), __float_as_uint(av[3])}, ra,
+                4 * o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(vb, rv, o, 0, 0);
+            return;
+        }
+        const int64_t i = mbase + static_cast<int64_t>(r) * mc + c0;
+        if (full) {
+            struct alignas(4) F4 { float x, y, z, w; };
+            if (a.norm) *reinterpret_cast<F4 *>(a.norm + i) = F4{nv[0], nv[1], nv[2], nv[3]};
+            if (a.angle) *reinterpret_cast<F4 *>(a.angle + i) = F4{av[0], av[1], av[2], av[3]};
+            typedef uint32_t u32a1 __attribute__((aligned(1)));
+            *reinterpret_cast<u32a1 *>(a.valid + i) = vb;
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                if (colw[m]) {
+                    if (a.norm) a.norm[i + m] = nv[m];
+                    if (a.angle) a.angle[i + m] = av[m];
+                    a.valid[i + m] = static_cast<uint8_t>(vb >> (8 * m));
+                }
+        }
     };
-    if (chunk == 0) zero_row(0);
-    if (r1 == rows - 2) zero_row(rows - 2);
-
-    // I(r, col) for this lane; lane 63 also loads I(r, col + 1) (the others take it from lane + 1).
-    // Rows past the frame read 0 (buffer range check) and are never used.
+    // Map rows 0 and rows-2 lie outside the scan (:71): zeros, written by the first / last chunk.
+    {
+        const float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (chunk == 0) put(0, z, z, 0u);
+        if (r1 == rows - 2) put(rows - 2, z, z, 0u);
+    }
+    // I(r, c0 .. c0+3) and I(r, c0+4): lane 63 loads the next dword (the others take byte 0 of the
+    // right lane's dword). Rows/columns past the frame read 0 and only feed unscanned entries.
     auto ld = [&](int r, uint32_t &p, uint32_t &e) {
-        p = buf_load_u8(rs, r * cols + col);
-        e = lane == kWave - 1 ? buf_load_u8(rs, r * cols + col + 1) : 0u;
+        p = lsd_load4<ALIGNED>(rs, r * cols + c0);
+        e = lane == kWave - 1 ? buf_load_u8(rs, r * cols + c0 + 4) : 0u;
     };
-    // (the DPP move runs on every lane: under a partial exec mask lane 62 would read a disabled lane 63)
-    auto right = [&](uint32_t p, uint32_t e) {
-        const uint32_t x = from_right(p);
+    auto fifth = [&](uint32_t p, uint32_t e) {  // DPP on every lane (lane 62 reads lane 63)
+        const uint32_t x = from_right(p) & 0xFFu;
         return lane == kWave - 1 ? e : x;
     };
-    int cnt = 0;
-    uint32_t word = 0;
+    int cnt[4] = {0, 0, 0, 0};
+    uint32_t word[4] = {0, 0, 0, 0};
+    int qn = 0;  // wave-uniform queue length
+    auto row = [&](int rr, uint32_t t, uint32_t te, uint32_t b, uint32_t be) {
+        const uint32_t t4 = fifth(t, te), b4 = fifth(b, be);
+        float nv[4], av[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        int sv[4], dv[4];
+        bool vv[4];
+        uint32_t vb = 0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int tm = (t >> (8 * m)) & 0xFF, bm = (b >> (8 * m)) & 0xFF;
+            const int tn = m < 3 ? ((t >> (8 * m + 8)) & 0xFF) : static_cast<int>(t4);
+            const int bn = m < 3 ? ((b >> (8 * m + 8)) & 0xFF) : static_cast<int>(b4);
+            const int ad = bn - tm, bc = tn - bm;  // :76-79
+            sv[m] = ad + bc;
+            dv[m] = ad - bc;
+            // gx^2 + gy^2 = (s^2 + d^2) / 4 exactly (half-integers), so the reference's correctly
+            // rounded sqrt (:82) is sqrt_rn(s^2 + d^2) / 2 (an exact power-of-two scaling)
+            nv[m] = static_cast<float>(static_cast<uint32_t>(sv[m] * sv[m] + dv[m] * dv[m]));
+        }
+        const f2 q01 = sqrt_rn_rsq2(f2{nv[0], nv[1]}) * 0.5f, q23 = sqrt_rn_rsq2(f2{nv[2], nv[3]}) * 0.5f;
+        nv[0] = q01.x, nv[1] = q01.y, nv[2] = q23.x, nv[3] = q23.y;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            vv[m] = (INTERIOR || colv[m]) && nv[m] > a.min_norm;  // :83
+            if (!INTERIOR && !colv[m]) nv[m] = 0.0f;
+            vb |= static_cast<uint32_t>(vv[m]) << (8 * m);
+            cnt[m] += vv[m] ? 1 : 0;
+            word[m] |= static_cast<uint32_t>(vv[m]) << ((rr - r0) & 31);
+        }
+        put(rr, nv, av, vb);
+        if (amap) {  // queue the valid pixels' (s, d) and map index
+            const uint64_t b0 = ballot(vv[0]), b1 = ballot(vv[1]), b2 = ballot(vv[2]), b3 = ballot(vv[3]);
+            const int tot = popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
+            if (tot) {
+                int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, qn))));
+                const uint32_t i0 = static_cast<uint32_t>(rr) * static_cast<uint32_t>(mc) + static_cast<uint32_t>(c0);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if (vv[m]) {
+                        qsd[pos] = (static_cast<uint32_t>(sv[m]) & 0xFFFFu) | (static_cast<uint32_t>(dv[m]) << 16);
+                        qidx[pos] = i0 + m;
+                        ++pos;
+                    }
+                qn += tot;
+                if (qn >= kWave) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    qn = __builtin_amdgcn_readfirstlane(lsd_drain(qsd, qidx, qn, kWave, amap));
+                }
+            }
+        }
+    };
     // one group: rows r .. r+kLsdGroup-1 from pixel rows r .. r+kLsdGroup (P/E[0..kLsdGroup])
     auto group = [&](int r, const uint32_t (&P)[kLsdGroup + 1], const uint32_t (&E)[kLsdGroup + 1]) {
 #pragma unroll
         for (int i = 0; i < kLsdGroup; ++i) {
-            const int rr = r + i;
-            if (rr >= r1) break;  // uniform
-            const uint32_t t0 = P[i], t1 = right(P[i], E[i]);
-            const uint32_t b0 = P[i + 1], b1 = right(P[i + 1], E[i + 1]);
-            const int ad = static_cast<int>(b1) - static_cast<int>(t0);  // :76-79
-            const int bc = static_cast<int>(t1) - static_cast<int>(b0);
-            const float gx = static_cast<float>(ad + bc) / 2.0f;  // :80-81
-            const float gy = static_cast<float>(ad - bc) / 2.0f;
-            const float nrm = __builtin_sqrtf((gx * gx) + (gy * gy));  // :82
-            const bool v = colv && nrm > a.min_norm;                  // :83
-            float ang = 0.0f;
-            if (v) ang = fd_atan2f(gx, -gy);  // :85
-            if (colw) {
-                const int64_t idx = mbase + static_cast<int64_t>(rr) * mc + col;
-                if (a.norm) a.norm[idx] = colv ? nrm : 0.0f;
-                if (a.angle) a.angle[idx] = ang;
-                a.valid[idx] = v ? 1 : 0;
-            }
-            cnt += v ? 1 : 0;
-            word |= static_cast<uint32_t>(v) << ((rr - r0) & 31);
+            if (r + i >= r1) break;  // uniform
+            row(r + i, P[i], E[i], P[i + 1], E[i + 1]);
         }
         // rows r0 + 32k .. r0 + 32k + 31 share a bitmask word (kLsdGroup divides 32)
         const int done = r + kLsdGroup - r0;
         if ((done & 31) == 0 || r + kLsdGroup >= r1) {
-            if (colv) bits_out[(done - 1) >> 5] = word;
-            word = 0;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                if (INTERIOR || colv[m])
+                    a.rowbits[((static_cast<int64_t>(f) * mc + c0 + m) * a.chunks + chunk) * a.words + ((done - 1) >> 5)] =
+                        word[m];
+                word[m] = 0;
+            }
         }
     };
     static_assert(32 % kLsdGroup == 0, "bitmask words hold whole groups");
@@ -204,7 +317,28 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
         for (int i = 0; i <= kLsdGroup; ++i) ld(r + 2 * kLsdGroup + i, A[i], AE[i]);
         group(r + kLsdGroup, B, BE);
     }
-    if (colv) a.col_cnt[(static_cast<int64_t>(f) * mc + col) * a.chunks + chunk] = cnt;
+    if (amap && qn > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        lsd_drain(qsd, qidx, qn, 0, amap);
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        if (INTERIOR || colv[m]) a.col_cnt[(static_cast<int64_t>(f) * mc + c0 + m) * a.chunks + chunk] = cnt[m];
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
+    __shared__ LsdQueue Q;
+    int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int strip = w % a.strips4;
+    w /= a.strips4;
+    const int chunk = w % a.chunks;
+    const int f = w / a.chunks;
+    if (f >= a.batch) return;
+    if (strip * 256 >= 1 && strip * 256 + 255 <= a.cols - 3) lsd_map_tile<ALIGNED, true>(a, f, strip, chunk, Q);
+    else lsd_map_tile<ALIGNED, false>(a, f, strip, chunk, Q);
 }
 
 // Pass 2: per-frame exclusive scan of the counts in column-major order (col outer, chunk inner).
@@ -275,7 +409,10 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s) {
     const int64_t waves = static_cast<int64_t>(a.batch) * a.chunks * a.strips;
     const dim3 grid(static_cast<unsigned>((waves + 3) / 4)), block(256);
-    hipLaunchKernelGGL(k_lsd_map, grid, block, 0, s, a);
+    const int64_t mwaves = static_cast<int64_t>(a.batch) * a.chunks * a.strips4;
+    const dim3 mgrid(static_cast<unsigned>((mwaves + 3) / 4));
+    if (a.aligned4) hipLaunchKernelGGL(k_lsd_map<true>, mgrid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_lsd_map<false>, mgrid, block, 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lsd_scan, dim3(a.batch), dim3(1024), 0, s, a);

@@ -740,6 +740,8 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
     int rc = check_shape(c, FD_HARRIS, batch, rows, cols, false);
     if (rc) return rc;
     if (rows < 2 || cols < 2) return fail(c, FD_ERR_INVALID, "LSD needs rows >= 2 and cols >= 2");  // :14
+    if (static_cast<int64_t>(rows - 1) * (cols - 1) >= (int64_t(1) << 29))  // 32-bit byte offsets into a frame's maps
+        return fail(c, FD_ERR_INVALID, "LSD frame too large ((rows-1)*(cols-1) must be < 2^29)");
     if (!valid_counts || idx_cap < 0 || (idx_cap > 0 && !valid_idx))
         return fail(c, FD_ERR_INVALID, "bad output arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
@@ -791,8 +793,11 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         a.rows = rows;
         a.cols = cols;
         a.strips = (cols - 1 + 63) / 64;  // map columns [0, cols-2]
-        const int64_t target = 8192;
-        int64_t ch = (static_cast<int64_t>(batch) * a.strips * work_rows) / target;
+        a.strips4 = (cols - 1 + 255) / 256;
+        a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
+        int64_t target = 16384;  // waves of the map kernel
+        if (const char *e = std::getenv("FD_LSD_WAVES")) target = std::max<int64_t>(64, std::atoll(e));  // A/B
+        int64_t ch = (static_cast<int64_t>(batch) * a.strips4 * work_rows) / target;
         ch = std::max<int64_t>(16, std::min<int64_t>(ch, 256));
         a.chunk_h = static_cast<int>(ch);
         a.chunks = (work_rows + a.chunk_h - 1) / a.chunk_h;
