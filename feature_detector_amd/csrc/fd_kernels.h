@@ -56,6 +56,11 @@ struct PointsArgs {
     // masked FAST: k = row_base[f][r] + word_pref[f][r][w] + popcount within the word
     const int32_t *row_base;
     const int32_t *word_pref;
+    // Sorted-segment mode (small launches, detect mode with hist0): [batch][blocks_per_frame] (base,
+    // count) of each workgroup's bin-sorted list segment; seg_bad[f] set when a tile overflowed its
+    // staging (the frame's list is then unsorted). Null = off.
+    uint2 *segdesc;
+    uint32_t *seg_bad;
 };
 
 struct SelectArgs {
@@ -87,6 +92,9 @@ struct SelectArgs {
     uint64_t *pre_keys;   // [batch][kSelectChunk]
     uint32_t *pre_count;  // [batch], reset by k_select
     int gather_groups;
+    const uint2 *segdesc;   // the candidate kernel's sorted segments (PointsArgs::segdesc) or null
+    uint32_t *seg_bad;      // [batch], reset by k_select
+    int nseg;               // segments per frame
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 

@@ -52,6 +52,7 @@ struct Sink {
     uint32_t *idx;
     uint32_t *hist;  // LDS level-0 histogram of the workgroup's frame, or null
     int n;           // staged entries (wave-uniform)
+    uint32_t *ovf;   // LDS flag: a wave of the workgroup flushed before the end (sorted-segment mode)
 };
 
 __device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f) {
@@ -103,7 +104,14 @@ __device__ __forceinline__ void emit_row(Sink &sk, const PointsArgs &a, int f, i
             if (fl[m]) dst[pos++] = Cand{v[m], id0 + m};
     } else {
         if (tot == 0) return;
-        if (sk.n + tot > kStage) sink_flush(sk, a, f);
+        if (sk.n + tot > kStage) {
+            // (sorted-segment mode: this frame's list is no longer one sorted segment per workgroup)
+            if (a.segdesc && lane_id() == 0) {
+                atomicOr(&a.seg_bad[f], 1u);
+                *sk.ovf = 1u;
+            }
+            sink_flush(sk, a, f);
+        }
         int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, sk.n))));
 #pragma unroll
         for (int m = 0; m < 4; ++m)
@@ -139,6 +147,67 @@ __device__ __forceinline__ void hist_flush(const uint32_t *h, uint32_t *g) {
         const uint32_t v = h[b];
         if (v) atomicAdd(&g[b], v);
     }
+}
+
+// Sorted-segment flush (PointsArgs::segdesc; small launches whose tiles never overflow the staging):
+// the workgroup's candidates, all still staged in LDS, go to the frame's list as one contiguous
+// segment ordered by level-0 bin, descending (a counting sort on the workgroup's LDS histogram), and
+// the segment is described in segdesc[f][g]. k_select then reads only each segment's prefix at or
+// above its first-chunk cut (a few entries per workgroup) instead of scanning the whole list.
+__device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, bool active, DetectLds &L,
+                                          uint32_t (&wtot)[4], uint32_t &wg_base) {
+    const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+    __syncthreads();
+    if (*sk.ovf) {  // part of the workgroup's list is already out unsorted: plain flush (frame marked)
+        if (active) sink_flush(sk, a, f);
+        hist_flush(L.hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+        return;
+    }
+    const int n = active ? sk.n : 0;
+    auto bin_of = [&](float r) { return ((float_key(r) - a.key_base) << a.key_lz) >> 20; };
+    for (int i = lane; i < n; i += kWave) atomicAdd(&L.hist[bin_of(sk.resp[i])], 1u);
+    hist_flush(L.hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);  // (leads with a barrier)
+    __syncthreads();
+    // in place: hist[b] = entries of bins above b (exclusive scan in descending bin order)
+    constexpr int kPer = kHistBins / 256;
+    uint32_t v[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) sum += (v[k] = L.hist[kHistBins - 1 - (tid * kPer + k)]);
+    uint32_t incl = sum;
+    for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == kWave - 1) wtot[wv] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum, total = 0;
+    for (int q = 0; q < 4; ++q) {
+        run += q < wv ? wtot[q] : 0u;
+        total += wtot[q];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        L.hist[kHistBins - 1 - (tid * kPer + k)] = run;
+        run += v[k];
+    }
+    if (tid == 0) {
+        wg_base = total ? atomicAdd(&a.list_count[f], total) : 0u;
+        const int g = static_cast<int>(blockIdx.x) % a.blocks_per_frame;
+        a.segdesc[static_cast<int64_t>(f) * a.blocks_per_frame + g] = make_uint2(wg_base, total);
+    }
+    __syncthreads();
+    float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    const int64_t base = wg_base;
+    for (int i = lane; i < n; i += kWave) {
+        const float r = sk.resp[i];
+        const int64_t pos = base + atomicAdd(&L.hist[bin_of(r)], 1u);
+        if (pos < a.list_cap) {
+            dr[pos] = r;
+            di[pos] = sk.idx[i];
+        }
+    }
+    sk.n = 0;
 }
 
 // Two pixels' float math at a time: <2 x float> arithmetic compiles to v_pk_mul_f32 / v_pk_add_f32 /
@@ -210,16 +279,24 @@ __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
     __shared__ DetectLds lds_all[1];
     int f, ty, tx;
     const bool active = decode_tile(a, f, ty, tx);
-    Sink sk{nullptr, nullptr, nullptr, 0};
+    __shared__ uint32_t seg_ovf;
+    Sink sk{nullptr, nullptr, nullptr, 0, &seg_ovf};
     if constexpr (!RASTER) {
         const int wv = threadIdx.x >> 6;
-        sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0};
+        sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0, &seg_ovf};
+        if (threadIdx.x == 0) seg_ovf = 0;
         if (a.hist0) hist_clear(lds_all[0].hist);
+        else __syncthreads();
     }
     if (active) corner_tile<KIND, RASTER, MASKED, ALIGNED, G1>(a, f, ty, tx, sk);
     if constexpr (!RASTER) {
-        if (active) sink_flush(sk, a, f);
-        if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+        if (a.segdesc) {
+            __shared__ uint32_t seg_wtot[4], seg_base;
+            seg_flush(sk, a, f, active, lds_all[0], seg_wtot, seg_base);
+        } else {
+            if (active) sink_flush(sk, a, f);
+            if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+        }
     }
 }
 
@@ -419,16 +496,24 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
     __syncthreads();
     int f, ty, tx;
     const bool active = decode_tile(a, f, ty, tx);
-    Sink sk{nullptr, nullptr, nullptr, 0};
+    __shared__ uint32_t seg_ovf;
+    Sink sk{nullptr, nullptr, nullptr, 0, &seg_ovf};
     if constexpr (!RASTER) {
         const int wv = threadIdx.x >> 6;
-        sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0};
+        sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0, &seg_ovf};
+        if (threadIdx.x == 0) seg_ovf = 0;
         if (a.hist0) hist_clear(lds_all[0].hist);
+        else __syncthreads();
     }
     if (active) fast_tile<RASTER, MASKED, ALIGNED>(a, off, seg_k, seg_o, seg_inc, f, ty, tx, sk);
     if constexpr (!RASTER) {
-        if (active) sink_flush(sk, a, f);
-        if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+        if (a.segdesc) {
+            __shared__ uint32_t seg_wtot[4], seg_base;
+            seg_flush(sk, a, f, active, lds_all[0], seg_wtot, seg_base);
+        } else {
+            if (active) sink_flush(sk, a, f);
+            if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+        }
     }
 }
 

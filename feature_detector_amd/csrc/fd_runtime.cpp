@@ -36,7 +36,7 @@ struct fd_ctx {
     // selection control block: [batch][kHistBins] level-0 histograms, then list_count per frame.
     // Zero between calls: k_select resets what a call used. sel_dirty marks a call whose kernels may
     // not have run to the end (the next call clears the block first).
-    DevBuf selctl, pre_keys;
+    DevBuf selctl, pre_keys, segdesc;
     bool sel_dirty = true;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts, l_bits;
@@ -248,7 +248,7 @@ int64_t detect_list_cap(int kind, int rows, int cols) {
 }
 
 struct SelectBufs {
-    uint32_t *hist0, *list_count, *pre_count;
+    uint32_t *hist0, *list_count, *pre_count, *seg_bad;
     uint64_t *pre_keys;
 };
 
@@ -257,7 +257,7 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
     FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
     FD_HIP_TRY(c, ensure(c->pre_keys, sizeof(uint64_t) * fdk::kSelectChunk * batch));
-    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 2);
+    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 3);
     if (c->selctl.n < ctl) {
         FD_HIP_TRY(c, ensure(c->selctl, ctl));
         c->sel_dirty = true;
@@ -270,6 +270,7 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     sb.hist0 = base;
     sb.list_count = base + static_cast<size_t>(batch) * fdk::kHistBins;
     sb.pre_count = sb.list_count + batch;
+    sb.seg_bad = sb.pre_count + batch;
     sb.pre_keys = as<uint64_t>(c->pre_keys);
     return FD_OK;
 }
@@ -302,7 +303,17 @@ struct SelectCall {
     int key_lz = 0;
     int tie_idx_desc = 0;  // equal responses: raster index descending (SuperPoint multimap) instead of ascending
     bool value_flag = false;  // the candidate kernel flags out-of-range values in pre_count (gather kernel off)
+    const uint2 *segdesc = nullptr;  // sorted segments of the candidate kernel (PointsArgs::segdesc)
+    int nseg = 0;
 };
+
+// Sorted-segment lists (PointsArgs::segdesc): for launches small enough that k_select can give every
+// workgroup segment of a frame its own threads (<= kSelectThreads segments per frame) and that would
+// otherwise gather their first chunk inside k_select (no k_gather kernel). FD_SEG_LISTS=0: off (A/B).
+bool use_seg_lists(int blocks_per_frame, int rows, int cols) {
+    if (const char *e = std::getenv("FD_SEG_LISTS"); e && std::atoi(e) == 0) return false;
+    return blocks_per_frame <= 1024 && static_cast<int64_t>(rows) * cols < (1 << 20);
+}
 
 // K4 (k_gather + k_select) on the candidate lists, features into out_xy / out_counts (device, or copied
 // back to the host and checked when !outputs_on_device).
@@ -355,6 +366,11 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     if (q.value_flag) s.gather_groups = 1;  // pre_count carries the candidate kernel's flag instead
     s.pre_count = sb.pre_count;
     s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
+    s.seg_bad = sb.seg_bad;
+    if (q.segdesc && !s.pre_keys) {
+        s.segdesc = q.segdesc;
+        s.nseg = q.nseg;
+    }
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
         FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 32 * batch));
@@ -535,6 +551,12 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     a.list_cap = cap;
     a.list_count = sb.list_count;
     a.hist0 = sb.hist0;
+    const bool seg = !g.empty && use_seg_lists(g.blocks_per_frame, rows, cols);
+    if (seg) {
+        FD_HIP_TRY(c, ensure(c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
+        a.segdesc = as<uint2>(c->segdesc);
+        a.seg_bad = sb.seg_bad;
+    }
     if (kind == FD_FAST && !g.empty) {
         rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
         if (rc) return rc;
@@ -568,6 +590,8 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     sc.cap = cap;
     sc.key_base = a.key_base;
     sc.key_lz = a.key_lz;
+    sc.segdesc = a.segdesc;
+    sc.nseg = g.blocks_per_frame;
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
 }
 

@@ -222,7 +222,30 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     for (int j = 0; j < kHistPerThread; ++j) hv[j] = a.hist0[static_cast<int64_t>(f) * kHistBins + tid + j * kSelectThreads];
     float *const pre_lds = reinterpret_cast<float *>(grid_lds);
     static_assert(kRegGather * kSelectThreads <= kGridLdsCells, "first gather round fits the grid's LDS");
-    if (!a.pre_keys) {
+    // sorted-segment mode: this frame's segment descriptors instead of the list prefetch
+    const bool seg_mode = a.segdesc != nullptr;
+    uint2 sd = make_uint2(0u, 0u);
+    uint32_t seg_bad = 0;
+    // (segment sg, slot j) of this thread in the sorted-segment gather, and its first two entries,
+    // loaded now so that they land during the histogram scan
+    const int segT = seg_mode ? max(1, nthr / a.nseg) : 1;
+    const int seg_sg = tid / segT, seg_j = tid - seg_sg * segT;
+    float pre_r[2] = {0.0f, 0.0f};
+    uint32_t pre_i[2] = {0u, 0u};
+    if (seg_mode) {
+        if (seg_sg < a.nseg) sd = a.segdesc[static_cast<int64_t>(f) * a.nseg + seg_sg];
+        seg_bad = __hip_atomic_load(&a.seg_bad[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t e = static_cast<uint32_t>(k * segT + seg_j);
+            const int64_t li = min(static_cast<int64_t>(sd.x) + e, a.list_cap - 1);
+            if (seg_sg < a.nseg && e < sd.y) {
+                pre_r[k] = lresp[li];
+                pre_i[k] = lidx[li];
+            }
+        }
+    }
+    if (!a.pre_keys && !seg_mode) {
         const uint32_t last = static_cast<uint32_t>(min(a.list_cap, static_cast<int64_t>(0xFFFFFFFF))) - 1u;
 #pragma unroll
         for (int k = 0; k < kRegGather; ++k)
@@ -371,6 +394,53 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         __syncthreads();  // sup complete; gcount read by every thread before anyone reuses it
     };
 
+    // First chunk from the sorted segments (PointsArgs::segdesc): every workgroup segment of the list
+    // is ordered by level-0 bin, descending, so the keys of bins >= lo are a prefix of each segment.
+    // T threads per segment read its entries T at a time while the last one read is still >= lo.
+    auto seg_gather = [&](int lo) {
+        if (tid == 0) gcount = 0;
+        __syncthreads();
+        const uint32_t k32lo = static_cast<uint32_t>(lo) << 20;
+        for (int r = 0;; ++r) {
+            bool more = false;
+            bool hit[2] = {false, false};
+            float rv[2];
+            uint32_t iv[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t e = static_cast<uint32_t>((2 * r + k) * segT + seg_j);
+                const bool in = seg_sg < a.nseg && e < sd.y && static_cast<int64_t>(sd.x) + e < a.list_cap;
+                if (r == 0) {
+                    rv[k] = pre_r[k];
+                    iv[k] = pre_i[k];
+                } else {
+                    const int64_t li = min(static_cast<int64_t>(sd.x) + e, a.list_cap - 1);
+                    rv[k] = in ? lresp[li] : 0.0f;
+                    iv[k] = in ? lidx[li] : 0u;
+                }
+                hit[k] = in && map_key32(rv[k], a) >= k32lo;
+            }
+            more = hit[1] && seg_j == segT - 1;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint64_t m = ballot(hit[k]);
+                if (m) {
+                    uint32_t off = 0;
+                    if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
+                    off = __builtin_amdgcn_readfirstlane(off);
+                    const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
+                    if (hit[k] && pos < static_cast<uint32_t>(kSelectChunk)) sup[pos] = make_key(rv[k], iv[k], a);
+                }
+            }
+            if (!__syncthreads_or(more)) break;
+            if (r > kSelectChunk) {  // consistency guard (sorted prefixes hold <= kSelectChunk keys)
+                if (tid == 0) atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x04000000u);
+                break;
+            }
+        }
+        __syncthreads();
+    };
+
     // The first level-0 chunk (the loop's first cut: the highest bins holding <= kSelectChunk keys),
     // gathered here so that the prefetched responses die before the sort and greedy code.
     bool first_ready = false;
@@ -387,10 +457,12 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 for (int i = tid; i < static_cast<int>(want); i += nthr) sup[i] = pk[i];
                 if (tid == 0) gcount = want;
                 __syncthreads();
+            } else if (seg_mode && seg_bad == 0) {
+                seg_gather(lo_b);
             } else {
                 if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
                     atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x02000000u);
-                gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, a.pre_keys ? nullptr : pre_lds);
+                gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, (a.pre_keys || seg_mode) ? nullptr : pre_lds);
             }
             first_ready = true;
         }
@@ -672,6 +744,7 @@ __device__ __forceinline__ void finish_frame(const SelectArgs &a, const int f) {
     if (threadIdx.x == 0) {
         __hip_atomic_store(&a.list_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.pre_count) __hip_atomic_store(&a.pre_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.seg_bad) __hip_atomic_store(&a.seg_bad[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

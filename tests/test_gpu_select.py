@@ -72,3 +72,18 @@ def test_gather_kernel_groups(fd, oracle, groups, monkeypatch):
         for i in range(2):
             exp = oracle.detect(KIND[name], frames[i], 20, THR[name], 200, sort_mode=1)[0]
             np.testing.assert_array_equal(got[i], exp)
+
+
+@pytest.mark.parametrize("seg", ["0", "1"])
+def test_sorted_segment_lists_toggle(fd, oracle, seg, monkeypatch):
+    # FD_SEG_LISTS=1 (default below a megapixel): each candidate-kernel workgroup writes its list
+    # segment sorted by level-0 bin and k_select reads only the segments' prefixes for its first
+    # chunk; tiles that overflow their staging (dense FAST) mark the frame and k_select scans it
+    monkeypatch.setenv("FD_SEG_LISTS", seg)
+    for shape, bsz in (((480, 640), 1), ((240, 320), 3), ((61, 77), 2), ((700, 1000), 1)):
+        frames = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 700 + i, *shape) for i in range(bsz)])
+        for name, dist, need in (("harris", 20, 200), ("shi_tomasi", 3, 800), ("fast", 20, 200), ("harris", 0, 50)):
+            got = _detect(fd, name, frames, need, dist)
+            for i in range(bsz):
+                exp = oracle.detect(KIND[name], frames[i], dist, THR[name], need, sort_mode=1)[0]
+                np.testing.assert_array_equal(got[i], exp)
