@@ -14,6 +14,7 @@ constexpr int kSegFast = kTileW;        // FAST has no NMS
 constexpr int kSelectChunk = 2048;      // candidates sorted per greedy chunk (LDS)
 constexpr int kGridLdsCells = 16384;    // occupancy grid kept in LDS up to this many cells
 constexpr int kMaxOffsetSegs = 48;
+constexpr int kSegHead = 64;           // selection keys kept per sorted segment head (PointsArgs::seghead)
 constexpr int kHistBins = 4096;         // level-0 digit of the selection key: top 12 bits of the mapped response
 
 // A raster-mode segment entry (fd_points_candidates only).
@@ -61,6 +62,7 @@ struct PointsArgs {
     // staging (the frame's list is then unsorted). Null = off.
     uint2 *segdesc;
     uint32_t *seg_bad;
+    uint64_t *seghead;  // [batch][blocks_per_frame][kSegHead] the segments' first keys (selection keys)
 };
 
 struct SelectArgs {
@@ -93,6 +95,7 @@ struct SelectArgs {
     uint32_t *pre_count;  // [batch], reset by k_select
     int gather_groups;
     const uint2 *segdesc;   // the candidate kernel's sorted segments (PointsArgs::segdesc) or null
+    const uint64_t *seghead;  // their first kSegHead selection keys (PointsArgs::seghead)
     uint32_t *seg_bad;      // [batch], reset by k_select
     int nseg;               // segments per frame
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels

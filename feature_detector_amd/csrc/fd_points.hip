@@ -199,13 +199,19 @@ __device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, 
     float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
     uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
     const int64_t base = wg_base;
+    const int g = static_cast<int>(blockIdx.x) % a.blocks_per_frame;
+    uint64_t *head = a.seghead + (static_cast<int64_t>(f) * a.blocks_per_frame + g) * kSegHead;
     for (int i = lane; i < n; i += kWave) {
         const float r = sk.resp[i];
-        const int64_t pos = base + atomicAdd(&L.hist[bin_of(r)], 1u);
+        const uint32_t k32 = (float_key(r) - a.key_base) << a.key_lz;
+        const uint32_t lp = atomicAdd(&L.hist[k32 >> 20], 1u);
+        const int64_t pos = base + lp;
         if (pos < a.list_cap) {
             dr[pos] = r;
             di[pos] = sk.idx[i];
         }
+        // the segment's head as selection keys (k32, ~idx): k_select's first read, no list hop
+        if (lp < static_cast<uint32_t>(kSegHead)) head[lp] = (static_cast<uint64_t>(k32) << 32) | static_cast<uint64_t>(~sk.idx[i]);
     }
     sk.n = 0;
 }

@@ -36,7 +36,7 @@ struct fd_ctx {
     // selection control block: [batch][kHistBins] level-0 histograms, then list_count per frame.
     // Zero between calls: k_select resets what a call used. sel_dirty marks a call whose kernels may
     // not have run to the end (the next call clears the block first).
-    DevBuf selctl, pre_keys, segdesc;
+    DevBuf selctl, pre_keys, segdesc, seghead;
     bool sel_dirty = true;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts, l_bits;
@@ -304,6 +304,7 @@ struct SelectCall {
     int tie_idx_desc = 0;  // equal responses: raster index descending (SuperPoint multimap) instead of ascending
     bool value_flag = false;  // the candidate kernel flags out-of-range values in pre_count (gather kernel off)
     const uint2 *segdesc = nullptr;  // sorted segments of the candidate kernel (PointsArgs::segdesc)
+    const uint64_t *seghead = nullptr;
     int nseg = 0;
 };
 
@@ -369,6 +370,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.seg_bad = sb.seg_bad;
     if (q.segdesc && !s.pre_keys) {
         s.segdesc = q.segdesc;
+        s.seghead = q.seghead;
         s.nseg = q.nseg;
     }
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
@@ -556,6 +558,8 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
         FD_HIP_TRY(c, ensure(c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
         a.segdesc = as<uint2>(c->segdesc);
         a.seg_bad = sb.seg_bad;
+        FD_HIP_TRY(c, ensure(c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
+        a.seghead = as<uint64_t>(c->seghead);
     }
     if (kind == FD_FAST && !g.empty) {
         rc = build_offsets(c, static_cast<int64_t>(rows - 6) * (cols - 6), opts->min_valid_response);
@@ -591,6 +595,7 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     sc.key_base = a.key_base;
     sc.key_lz = a.key_lz;
     sc.segdesc = a.segdesc;
+    sc.seghead = a.seghead;
     sc.nseg = g.blocks_per_frame;
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
 }

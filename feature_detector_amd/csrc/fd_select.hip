@@ -65,9 +65,10 @@ __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const Sel
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
 constexpr int kSubChunk = 512;  // keys sorted per greedy sub-chunk
-constexpr int kSelectThreads = 1024;  // k_select workgroup size (launch_select)
-constexpr int kHistPerThread = kHistBins / kSelectThreads;
-static_assert(kHistBins % kSelectThreads == 0, "histogram bins per thread");
+// k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
+// with 256 threads (4x the items per wave) the headline frame's selection measured 1.3x slower.
+constexpr int kSelectThreads = 1024;
+constexpr int kSegPer = 2;  // sorted-segment entries per thread and round
 constexpr int kRegGather = 16;  // list responses per thread and round in the level-0 gather
 
 // One wave scans a sorted chunk in order (SelectGoodFeatures, feature_point_detector.cpp:62-72), a
@@ -174,11 +175,15 @@ struct alignas(16) SelectLds {
     int resume[kLevels];
     uint32_t wtot[16];
     uint32_t gcount;
+    uint32_t seg_more[2];
     int s_done, s_acc;
     uint64_t st[32];  // diagnostic phase clocks (a.stamps only); 16..31 free for ad-hoc probes
 };
 
+template <int NT>
 __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, SelectLds &L) {
+    constexpr int kHistPerThread = kHistBins / NT;
+    static_assert(kHistBins % NT == 0 && NT <= kSelectThreads, "histogram bins per thread");
     uint32_t(&suf0)[kHistBins + 1] = L.suf0;
     uint32_t(&sufl)[kLevels - 1][257] = L.sufl;
     uint64_t(&sup)[kSelectChunk] = L.sup;
@@ -219,9 +224,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // into the occupancy grid's space, which is initialised only after this first round is consumed.
     uint32_t hv[kHistPerThread];
 #pragma unroll
-    for (int j = 0; j < kHistPerThread; ++j) hv[j] = a.hist0[static_cast<int64_t>(f) * kHistBins + tid + j * kSelectThreads];
+    for (int j = 0; j < kHistPerThread; ++j) hv[j] = a.hist0[static_cast<int64_t>(f) * kHistBins + tid + j * NT];
     float *const pre_lds = reinterpret_cast<float *>(grid_lds);
-    static_assert(kRegGather * kSelectThreads <= kGridLdsCells, "first gather round fits the grid's LDS");
+    static_assert(kRegGather * NT <= kGridLdsCells, "first gather round fits the grid's LDS");
     // sorted-segment mode: this frame's segment descriptors instead of the list prefetch
     const bool seg_mode = a.segdesc != nullptr;
     uint2 sd = make_uint2(0u, 0u);
@@ -230,19 +235,18 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // loaded now so that they land during the histogram scan
     const int segT = seg_mode ? max(1, nthr / a.nseg) : 1;
     const int seg_sg = tid / segT, seg_j = tid - seg_sg * segT;
-    float pre_r[2] = {0.0f, 0.0f};
-    uint32_t pre_i[2] = {0u, 0u};
+    uint64_t pre_key[kSegPer] = {};
     if (seg_mode) {
-        if (seg_sg < a.nseg) sd = a.segdesc[static_cast<int64_t>(f) * a.nseg + seg_sg];
+        // unconditional (clamped) loads, so that nothing waits for them before their use
+        const int sgc = min(seg_sg, a.nseg - 1);
+        sd = a.segdesc[static_cast<int64_t>(f) * a.nseg + sgc];
         seg_bad = __hip_atomic_load(&a.seg_bad[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the first two entries of this thread, from the segment heads (entries past kSegHead or past
+        // the segment's count are masked in seg_gather; the list is read there for them)
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t e = static_cast<uint32_t>(k * segT + seg_j);
-            const int64_t li = min(static_cast<int64_t>(sd.x) + e, a.list_cap - 1);
-            if (seg_sg < a.nseg && e < sd.y) {
-                pre_r[k] = lresp[li];
-                pre_i[k] = lidx[li];
-            }
+        for (int k = 0; k < kSegPer; ++k) {
+            const int e = min(k * segT + seg_j, kSegHead - 1);
+            pre_key[k] = a.seghead[(static_cast<int64_t>(f) * a.nseg + sgc) * kSegHead + e];
         }
     }
     if (!a.pre_keys && !seg_mode) {
@@ -270,15 +274,11 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
 
     // In-place suffix sums of S[0..nb) by the whole block; S[nb] = 0.
     auto suffix = [&](uint32_t *S, int nb) {
-        const int ch = (nb + nthr - 1) / nthr;  // contiguous bins per thread (<= 4)
+        const int ch = (nb + nthr - 1) / nthr;  // contiguous bins per thread
         const int b0 = min(tid * ch, nb), b1 = min(b0 + ch, nb);
-        uint32_t v[4] = {0, 0, 0, 0};
         uint32_t sacc = 0;
-        for (int b = b0; b < b1; ++b) {
-            v[b - b0] = S[b];
-            sacc += v[b - b0];
-        }
-        // suffix over threads: wave-level, then across the 16 waves
+        for (int b = b0; b < b1; ++b) sacc += S[b];
+        // suffix over threads: wave-level, then across the waves
         uint32_t incl = sacc;
         for (int o = 1; o < kWave; o <<= 1) {
             const uint32_t t = __shfl_down(incl, o);
@@ -289,8 +289,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         uint32_t after = 0;
         for (int q = wave + 1; q < nthr / kWave; ++q) after += wtot[q];
         uint32_t run = incl - sacc + after;
-        for (int b = b1 - 1; b >= b0; --b) {
-            run += v[b - b0];
+        for (int b = b1 - 1; b >= b0; --b) {  // (a thread's own bins: read before written)
+            run += S[b];
             S[b] = run;
         }
         if (tid == 0) S[nb] = 0;
@@ -323,7 +323,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     };
     auto suf = [&](int lvl) -> uint32_t * { return lvl == 0 ? suf0 : sufl[lvl - 1]; };
 
-    for (int j = 0; j < kHistPerThread; ++j) suf0[tid + j * kSelectThreads] = hv[j];
+    for (int j = 0; j < kHistPerThread; ++j) suf0[tid + j * NT] = hv[j];
     __syncthreads();
     FD_STAMP(1);
     suffix(suf0, kHistBins);
@@ -398,41 +398,58 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // is ordered by level-0 bin, descending, so the keys of bins >= lo are a prefix of each segment.
     // T threads per segment read its entries T at a time while the last one read is still >= lo.
     auto seg_gather = [&](int lo) {
-        if (tid == 0) gcount = 0;
+        if (tid == 0) {
+            gcount = 0;
+            L.seg_more[0] = 0;
+            L.seg_more[1] = 0;
+        }
         __syncthreads();
+        FD_STAMP(25);
         const uint32_t k32lo = static_cast<uint32_t>(lo) << 20;
         for (int r = 0;; ++r) {
             bool more = false;
-            bool hit[2] = {false, false};
-            float rv[2];
-            uint32_t iv[2];
+            bool hit[kSegPer] = {};
+            uint64_t kv[kSegPer];
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t e = static_cast<uint32_t>((2 * r + k) * segT + seg_j);
+            for (int k = 0; k < kSegPer; ++k) {
+                const uint32_t e = static_cast<uint32_t>((kSegPer * r + k) * segT + seg_j);
                 const bool in = seg_sg < a.nseg && e < sd.y && static_cast<int64_t>(sd.x) + e < a.list_cap;
-                if (r == 0) {
-                    rv[k] = pre_r[k];
-                    iv[k] = pre_i[k];
+                if (r == 0 && e < static_cast<uint32_t>(kSegHead)) {
+                    kv[k] = pre_key[k];
                 } else {
                     const int64_t li = min(static_cast<int64_t>(sd.x) + e, a.list_cap - 1);
-                    rv[k] = in ? lresp[li] : 0.0f;
-                    iv[k] = in ? lidx[li] : 0u;
+                    kv[k] = in ? make_key(lresp[li], lidx[li], a) : 0ull;
                 }
-                hit[k] = in && map_key32(rv[k], a) >= k32lo;
+                hit[k] = in && static_cast<uint32_t>(kv[k] >> 32) >= k32lo;
             }
-            more = hit[1] && seg_j == segT - 1;
+            more = hit[kSegPer - 1] && seg_j == segT - 1;
+            // one LDS reservation per wave and round for all kSegPer slots
+            uint64_t bm[kSegPer];
+            uint32_t wtotal = 0;
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint64_t m = ballot(hit[k]);
-                if (m) {
-                    uint32_t off = 0;
-                    if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
-                    off = __builtin_amdgcn_readfirstlane(off);
-                    const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
-                    if (hit[k] && pos < static_cast<uint32_t>(kSelectChunk)) sup[pos] = make_key(rv[k], iv[k], a);
+            for (int k = 0; k < kSegPer; ++k) {
+                bm[k] = ballot(hit[k]);
+                wtotal += popc64(bm[k]);
+            }
+            if (wtotal) {
+                uint32_t off = 0;
+                if (lane == 0) off = atomicAdd(&gcount, wtotal);
+                off = __builtin_amdgcn_readfirstlane(off);
+#pragma unroll
+                for (int k = 0; k < kSegPer; ++k) {
+                    const uint32_t pos = static_cast<uint32_t>(mbcnt64(bm[k], static_cast<int>(off)));
+                    if (hit[k] && pos < static_cast<uint32_t>(kSelectChunk)) sup[pos] = kv[k];
+                    off += popc64(bm[k]);
                 }
             }
-            if (!__syncthreads_or(more)) break;
+            FD_STAMP(23);
+            // one barrier per round: waves whose last slot still hits raise this round's flag
+            // (alternating words: the one cleared here was last read before the previous barrier)
+            if (tid == 0) L.seg_more[(r + 1) & 1] = 0;
+            if (ballot(more) != 0ull && lane == 0) L.seg_more[r & 1] = 1;
+            __syncthreads();
+            FD_STAMP(24);
+            if (L.seg_more[r & 1] == 0) break;
             if (r > kSelectChunk) {  // consistency guard (sorted prefixes hold <= kSelectChunk keys)
                 if (tid == 0) atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x04000000u);
                 break;
@@ -450,6 +467,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             const int mid = (lo_b + hi_b) >> 1;
             if (suf0[mid] <= static_cast<uint32_t>(kSelectChunk)) hi_b = mid; else lo_b = mid + 1;
         }
+        FD_STAMP(21);
         if (lo_b < kHistBins && suf0[lo_b] > 0) {
             const uint32_t want = suf0[lo_b];
             if (a.pre_keys && a.pre_count[f] == want) {  // k_gather's result (previous kernel)
@@ -467,6 +485,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             first_ready = true;
         }
     }
+    FD_STAMP(22);
     if (use_grid && grid_in_lds) {  // the first round's LDS-direct loads are consumed (or never used)
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load still landing in this space
         __syncthreads();
@@ -763,10 +782,11 @@ __global__ __launch_bounds__(1024) void k_gather(SelectArgs a) {
     gather_first_chunk<1024>(v, g, G, L);
 }
 
-__global__ __launch_bounds__(kSelectThreads) void k_select(SelectArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
     __shared__ SelectLds L;
     const int f = blockIdx.x;
-    select_frame(a, f, L);
+    select_frame<NT>(a, f, L);
     finish_frame(a, f);
 }
 
@@ -778,7 +798,7 @@ hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_select, dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
+    hipLaunchKernelGGL(k_select<kSelectThreads>, dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
     return hipGetLastError();
 }
 
