@@ -333,6 +333,37 @@ def run_end_to_end(torch, fd, args, seconds=3.0):
             "frames": n, "note": "host numpy frame -> H2D staging -> detect -> D2H features, synchronous per frame"}
 
 
+def run_ingest(torch, fd, args, seconds=3.0, batch=16, depth=3):
+    """PCIe-inclusive rate through the pipelined ingest (fd_ingest_*): host frames
+    written into pinned slots, uploads overlapped with detection, features copied back. Reported beside
+    `value`, never as it."""
+    frames = make_frames(torch, args.pattern, 2 * batch, args.rows, args.cols, 31338, torch.device("cuda")).cpu().numpy()
+    ing = fd.Ingest(args.detector, args.rows, args.cols, batch=batch, depth=depth, need=args.need,
+                    min_feature_distance=args.dist, min_valid_response=THR[args.detector])
+    n, k, t0 = 0, 0, None
+    while True:
+        slot = k % depth
+        if k >= depth:
+            ing.wait(slot)
+            n += batch
+        if t0 is None and k == depth:  # timing starts with the pipeline full
+            t0, n = time.perf_counter(), 0
+        if t0 is not None and time.perf_counter() - t0 >= seconds:
+            break
+        ing.frames(slot)[:] = frames[(k % 2) * batch:(k % 2 + 1) * batch]
+        ing.submit(slot)
+        k += 1
+    el = time.perf_counter() - t0
+    for j in range(k - depth + 1, k):  # drain
+        if j >= 0:
+            ing.wait(j % depth)
+    ing.close()
+    return {"mpix_s": round(n * args.rows * args.cols / el / 1e6, 1), "frames_per_s": round(n / el, 1),
+            "batch": batch, "depth": depth,
+            "note": "host numpy frames -> pinned slot (memcpy) -> H2D on a copy stream overlapped with detect -> "
+                    "D2H features; host fill included"}
+
+
 def conv_flops(net, rows, cols):
     """Dense multiply-add FLOPs (2 per MAC) of every Conv2d of the network for one rows x cols frame."""
     from torch import nn
@@ -500,6 +531,7 @@ def main():
     if world == 1:
         with phase(torch, "end_to_end"):
             out["end_to_end_host_frames"] = run_end_to_end(torch, fd, args)
+            out["end_to_end_ingest"] = run_ingest(torch, fd, args)
 
     # ---- CPU baseline: the oracle (single thread), bounded sample, rank 0 at N=1 ------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -20,6 +20,7 @@ EXPORTS = (
     "fd_points_response_append",
     "fd_lsd_map", "fd_brief_compute", "fd_nn_select", "fd_nn_descriptors",
     "fd_build_info",
+    "fd_ingest_create", "fd_ingest_destroy", "fd_ingest_frames", "fd_ingest_submit", "fd_ingest_wait",
 )
 
 
@@ -86,6 +87,11 @@ def load() -> ctypes.CDLL:
         "fd_nn_select": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_nn_opts), P, P, P, i32, P, i32]),
         "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
+        "fd_ingest_create": (i32, [P, i32, i32, i32, i32, i32, u32, i32, ctypes.POINTER(P)]),
+        "fd_ingest_destroy": (None, [P]),
+        "fd_ingest_frames": (P, [P, i32]),
+        "fd_ingest_submit": (i32, [P, i32, ctypes.POINTER(fd_point_opts)]),
+        "fd_ingest_wait": (i32, [P, i32, ctypes.POINTER(P), ctypes.POINTER(P)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -455,7 +455,8 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->seg_cnt,  &c->seg,      &c->resp_map,    &c->c_resp,       &c->c_x,     &c->c_y,
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
-                      &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out};
+                      &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
+                      &c->segdesc,  &c->seghead};
     for (DevBuf *b : bufs) release(*b);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
@@ -511,6 +512,11 @@ int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t m
     if (kind == FD_FAST) {
         rc = build_offsets(c, std::max<int64_t>(0, static_cast<int64_t>(rows - 6) * (cols - 6)), c->off_thr);
         if (rc) return rc;
+    }
+    const PointGeom g = point_geom(kind, batch, rows, cols);
+    if (!g.empty && use_seg_lists(g.blocks_per_frame, rows, cols)) {
+        FD_HIP_TRY(c, ensure(c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
+        FD_HIP_TRY(c, ensure(c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
     }
     return FD_OK;
 }

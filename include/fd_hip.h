@@ -206,6 +206,29 @@ int fd_nn_descriptors(fd_ctx *ctx, const float *map, int map_on_device, int map_
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);
 
+/* ---- ingest: pinned, pipelined host frames -> features ------------------------ */
+/*
+ * A streaming front end for DetectGoodFeatures on host frames (what the reference's callers do per
+ * frame after Visualizor2D::LoadImage, test_feature_point_detector.cpp:104-110): `depth` slots, each
+ * a pinned host buffer for `batch` frames plus device buffers. fd_ingest_submit copies a slot to the
+ * GPU on the ingest's own copy stream and queues detection (fd_points_detect) and the copy-back of
+ * the features on the context stream, so the upload of slot i+1 overlaps the detection of slot i.
+ * The host fills a slot's frames in place (fd_ingest_frames) and collects its features with
+ * fd_ingest_wait; slots are reused round-robin by the caller. One ingest per context at a time (its
+ * detections share the context workspace, serialised on the context stream).
+ */
+typedef struct fd_ingest fd_ingest;
+int fd_ingest_create(fd_ctx *ctx, int kind, int batch, int rows, int cols, int depth, uint32_t need,
+                     int32_t out_stride, fd_ingest **out);
+void fd_ingest_destroy(fd_ingest *ing);
+/* pinned host buffer of slot `slot`: batch * rows * cols bytes (GrayImage layout) */
+uint8_t *fd_ingest_frames(fd_ingest *ing, int slot);
+/* queue slot `slot` (its frames written) with these options; returns without waiting */
+int fd_ingest_submit(fd_ingest *ing, int slot, const fd_point_opts *opts);
+/* wait for slot `slot`; *xy -> batch * out_stride (x, y) pairs, *counts -> batch new-feature counts
+ * (pinned host memory owned by the ingest, valid until the slot is submitted again) */
+int fd_ingest_wait(fd_ingest *ing, int slot, const float **xy, const int32_t **counts);
+
 #ifdef __cplusplus
 }
 #endif
