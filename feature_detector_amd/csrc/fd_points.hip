@@ -348,6 +348,7 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
     for (int i0 = 0; i0 < n_in; i0 += 6) {
 #pragma unroll
         for (int t = 0; t < 6; ++t) {
+            if (i0 + t >= n_in) break;  // (uniform) short tiles: no steps past the tile's last NMS row
             const int s = t % 3, su = (t + 1) % 3, sc = (t + 2) % 3;  // 3-slot roles: rows ri, ri-2, ri-1
             const int ri = y0 - 3 + i0 + t;                            // row consumed this step
             ring[(t + 3) % 6] = load_px4<ALIGNED>(rs, (ri + 3) * cols + c0);

@@ -97,9 +97,17 @@ int choose_tile_h(int64_t batch, int tiles_x, int out_rows, int period, int max_
     if (const char *e = std::getenv("FD_TARGET_WAVES")) target_waves = std::max<int64_t>(1, std::atoll(e));  // tuning
     if (const char *e = std::getenv("FD_TILE_MULT")) max_mult = std::max(1, std::atoi(e));                   // tuning
     int64_t h = (batch * tiles_x * static_cast<int64_t>(out_rows)) / target_waves;
-    h = std::max<int64_t>(h, period);  // small batches: short tiles, more single-wave SIMDs busy
-    h = ((h + period - 1) / period) * period;
+    if (h < period && period == 6) {
+        // small launches: the tile's serial row chain is the latency; 3 rows (9 steps of the 6-row
+        // ring, the loop stops early) measured best at 640x480 batch 1 (tile_h 6/4/3/2/1: K1 11.4 /
+        // 10.3 / 10.1 / 10.2 / 13.2 us, and k_select grows with the number of segments below 3)
+        h = 3;
+    } else {
+        h = std::max<int64_t>(h, period);
+        h = ((h + period - 1) / period) * period;
+    }
     h = std::min<int64_t>(h, static_cast<int64_t>(period) * max_mult);
+    if (const char *e = std::getenv("FD_TILE_H")) h = std::max(1, std::atoi(e));  // tuning (A/B)
     return static_cast<int>(h);
 }
 
