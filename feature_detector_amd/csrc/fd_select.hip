@@ -176,6 +176,7 @@ struct alignas(16) SelectLds {
     uint32_t wtot[16];
     uint32_t gcount;
     uint32_t seg_more[2];
+    int ff_res[2];  // first_le results (alternating slots)
     int s_done, s_acc;
     uint64_t st[32];  // diagnostic phase clocks (a.stamps only); 16..31 free for ad-hoc probes
 };
@@ -295,6 +296,29 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         }
         if (tid == 0) S[nb] = 0;
         __syncthreads();
+    };
+    // Smallest x in [lo_x, hi_x) with S[x] - base <= lim, or hi_x (S non-increasing: the predicate is a
+    // step). All threads; each tests a contiguous run of bins and the one holding the step writes it:
+    // two barriers instead of a dependent chain of ~12 LDS reads. Results alternate between two slots,
+    // so a slot is rewritten only after every thread has passed the barrier that follows its read.
+    int ff_parity = 0;
+    auto first_le = [&](const uint32_t *S, int lo_x, int hi_x, uint32_t base, uint32_t lim) -> int {
+        const int slot = ff_parity;
+        ff_parity ^= 1;
+        if (tid == 0) L.ff_res[slot] = hi_x;
+        __syncthreads();
+        const int n = hi_x - lo_x;
+        const int per = (n + nthr - 1) / nthr;
+        const int x0 = lo_x + tid * per, x1 = min(x0 + per, hi_x);
+        if (x0 < x1 && !(x0 > lo_x && S[x0 - 1] - base <= lim)) {
+            for (int x = x0; x < x1; ++x)
+                if (S[x] - base <= lim) {
+                    L.ff_res[slot] = x;
+                    break;
+                }
+        }
+        __syncthreads();
+        return L.ff_res[slot];
     };
     // Histogram of digit `lvl` (>= 1) over keys in [klo, khi] (one pass over the list).
     auto build = [&](int lvl, uint64_t klo, uint64_t khi, uint32_t *S) {
@@ -462,11 +486,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // gathered here so that the prefetched responses die before the sort and greedy code.
     bool first_ready = false;
     {
-        int lo_b = 0, hi_b = kHistBins;
-        while (lo_b < hi_b) {
-            const int mid = (lo_b + hi_b) >> 1;
-            if (suf0[mid] <= static_cast<uint32_t>(kSelectChunk)) hi_b = mid; else lo_b = mid + 1;
-        }
+        const int lo_b = first_le(suf0, 0, kHistBins, 0u, static_cast<uint32_t>(kSelectChunk));
         FD_STAMP(21);
         if (lo_b < kHistBins && suf0[lo_b] > 0) {
             const uint32_t want = suf0[lo_b];
@@ -511,12 +531,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         const uint32_t base = S[hi + 1];
         const uint32_t lim = static_cast<uint32_t>(kSelectChunk);
         // smallest lo in [0, hi] with S[lo] - base <= lim (S is non-increasing in b)
-        int lo_b = 0, hi_b = hi + 1;
-        while (lo_b < hi_b) {
-            const int mid = (lo_b + hi_b) >> 1;
-            if (S[mid] - base <= lim) hi_b = mid; else lo_b = mid + 1;
-        }
-        int lo = lo_b;
+        int lo = first_le(S, 0, hi + 1, base, lim);
         const int w = lvl_width(level);
         const int rem = 64 - lvl_top(level);
         const uint64_t pre = prefix[level];
@@ -613,11 +628,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             int shi = hi;
             while (shi >= lo && !s_done) {
                 const uint32_t sbase = S[shi + 1];
-                int q0 = lo, q1 = shi + 1;
-                while (q0 < q1) {
-                    const int mid = (q0 + q1) >> 1;
-                    if (S[mid] - sbase <= static_cast<uint32_t>(kSubChunk)) q1 = mid; else q0 = mid + 1;
-                }
+                const int q0 = first_le(S, lo, shi + 1, sbase, static_cast<uint32_t>(kSubChunk));
                 const int slo = min(q0, shi);  // one bin larger than a sub-chunk is taken whole
                 const uint32_t sc = S[slo] - sbase;
                 if (sc > 0) {
