@@ -485,8 +485,10 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // The first level-0 chunk (the loop's first cut: the highest bins holding <= kSelectChunk keys),
     // gathered here so that the prefetched responses die before the sort and greedy code.
     bool first_ready = false;
+    int first_lo = -1;  // the first chunk's cut (the main loop's first search, done here already)
     {
         const int lo_b = first_le(suf0, 0, kHistBins, 0u, static_cast<uint32_t>(kSelectChunk));
+        first_lo = lo_b;
         FD_STAMP(21);
         if (lo_b < kHistBins && suf0[lo_b] > 0) {
             const uint32_t want = suf0[lo_b];
@@ -531,7 +533,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         const uint32_t base = S[hi + 1];
         const uint32_t lim = static_cast<uint32_t>(kSelectChunk);
         // smallest lo in [0, hi] with S[lo] - base <= lim (S is non-increasing in b)
-        int lo = first_le(S, 0, hi + 1, base, lim);
+        // (level 0, top of the histogram: the cut computed for the first chunk above)
+        int lo = (level == 0 && hi == kHistBins - 1 && first_lo >= 0) ? first_lo : first_le(S, 0, hi + 1, base, lim);
         const int w = lvl_width(level);
         const int rem = 64 - lvl_top(level);
         const uint64_t pre = prefix[level];
@@ -628,7 +631,10 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             int shi = hi;
             while (shi >= lo && !s_done) {
                 const uint32_t sbase = S[shi + 1];
-                const int q0 = first_le(S, lo, shi + 1, sbase, static_cast<uint32_t>(kSubChunk));
+                // (the whole remaining range fits a sub-chunk: no search)
+                const int q0 = S[lo] - sbase <= static_cast<uint32_t>(kSubChunk)
+                                   ? lo
+                                   : first_le(S, lo, shi + 1, sbase, static_cast<uint32_t>(kSubChunk));
                 const int slo = min(q0, shi);  // one bin larger than a sub-chunk is taken whole
                 const uint32_t sc = S[slo] - sbase;
                 if (sc > 0) {
