@@ -508,7 +508,8 @@ def main():
                          "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb,
                          "traffic": measured_traffic("northstar_k_corner")[0]},
             "valu_bound": ("~90% VALU busy (SQ_ACTIVE_INST_VALU vs SIMD issue capacity; " + VALU_FILE + "): "
-                           "~40 VALU lane-instr/px, so VALU issue, not HBM, bounds this kernel (DESIGN.md)"),
+                           "~37 VALU lane-instr/px (309 M wave-instructions per launch), so VALU issue, not HBM, bounds "
+                           "this kernel (DESIGN.md)"),
         }
         del pool2
 
