@@ -65,6 +65,7 @@ __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const Sel
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
 constexpr int kSubChunk = 512;  // keys sorted per greedy sub-chunk
+constexpr int kBucketMax = 64;  // largest bin of a sub-chunk ordered by bucket placement (else merge sort)
 // k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
 // with 256 threads (4x the items per wave) the headline frame's selection measured 1.3x slower.
 constexpr int kSelectThreads = 1024;
@@ -84,17 +85,30 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     const int d = a.dist;
     int acc = s_acc;
     bool done = false;
-    for (int b0 = 0; b0 < cnt && !done; b0 += kWave) {
-        const int i = b0 + lane;
+    // Software pipeline: a batch's position, cell and conflict mask are loaded during the previous
+    // batch's resolution (they are read-only here; only the grid is written).
+    auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C) {
+        const int i = b + lane;
         const bool in = i < cnt;
-        const uint32_t e = in ? pxy[i] : kEmpty;
-        bool ok = e != kEmpty;
-        const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-        int cell = gw2 + 1;
-        uint64_t C = 0;
+        e = in ? pxy[i] : kEmpty;
+        cell = gw2 + 1;
+        C = 0;
         if constexpr (GRID != 0) {
             cell = in ? static_cast<int>(pcell[i]) : gw2 + 1;
             C = in ? cmask[i] : 0ull;
+        }
+    };
+    uint32_t e_n;
+    int cell_n;
+    uint64_t C_n;
+    fetch(0, e_n, cell_n, C_n);
+    for (int b0 = 0; b0 < cnt && !done; b0 += kWave) {
+        const uint32_t e = e_n;
+        const int cell = cell_n;
+        uint64_t C = C_n;
+        bool ok = e != kEmpty;
+        const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+        if constexpr (GRID != 0) {
             uint32_t g[9];
 #pragma unroll
             for (int q = 0; q < 9; ++q) {
@@ -108,6 +122,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                 if (g[q] != kEmpty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
             }
         }
+        if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n);
         const uint64_t m = ballot(ok);
         C &= m;
         // Fixed point: a lane is decided once all of C is; accepted iff none of C was accepted.
@@ -664,10 +679,48 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     }
                     FD_STAMP(10);  // sub-chunk extract
                 {
+                    const int c = static_cast<int>(sc);
+                    // Bucket placement (every bin of the sub-chunk holds <= kBucketMax keys, the usual
+                    // case at the top of the list): a key of bin b belongs at (keys in the bins above b)
+                    // + (larger keys of its own bin). The level's suffix counts give the first term; a
+                    // bin's keys are grouped by one LDS atomic each on S[b+1] (entries not read again:
+                    // the next sub-chunk starts at S[slo]), then ranked by a scan of their group.
+                    uint64_t me = 0;
+                    uint32_t s_b = 0, s_b1 = 0;
+                    int bin = 0;
+                    bool big = c > nthr;
+                    if (!big && tid < c) {
+                        me = unsorted[tid];
+                        bin = static_cast<int>((me >> rem) & ((1ull << w) - 1ull));
+                        s_b = S[bin];
+                        s_b1 = S[bin + 1];
+                        big = s_b - s_b1 > static_cast<uint32_t>(kBucketMax);
+                    }
+                    if (!__syncthreads_or(big)) {
+                        if (tid < c) {
+                            const uint32_t slot = atomicAdd(const_cast<uint32_t *>(&S[bin + 1]), 1u) - sbase;
+                            tmp[min(slot, static_cast<uint32_t>(kSelectChunk - 1))] = me;
+                        }
+                        __syncthreads();
+                        FD_STAMP(11);  // bucket scatter
+                        if (tid < c) {
+                            const uint32_t g0 = s_b1 - sbase, gn = s_b - s_b1;
+                            uint32_t r = 0;
+                            for (uint32_t j0 = 0; j0 < gn; j0 += 8) {  // 8 loads in flight (clamped to the group)
+                                uint64_t v[8];
+#pragma unroll
+                                for (uint32_t u = 0; u < 8; ++u) v[u] = tmp[g0 + min(j0 + u, gn - 1)];
+#pragma unroll
+                                for (uint32_t u = 0; u < 8; ++u) r += (j0 + u < gn && v[u] > me) ? 1u : 0u;
+                            }
+                            place(static_cast<int>(min(g0 + r, static_cast<uint32_t>(kSelectChunk - 1))), me);
+                        }
+                        __syncthreads();
+                        FD_STAMP(13);  // bucket rank + place
+                    } else {
                     // Merge sort of unique keys, descending: rank inside runs of 64 by counting larger
                     // keys (broadcast LDS reads), then log2 merge levels where each key moves to
                     // (its offset in its run) + (number of larger keys in the sibling run, by binary search).
-                    const int c = static_cast<int>(sc);
                     const int c64 = (c + 63) & ~63;
                     for (int i = c + tid; i < c64; i += nthr) unsorted[i] = 0ull;
                     __syncthreads();
@@ -707,6 +760,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     for (int i = tid; i < c; i += nthr) place(i, src[i]);
                     __syncthreads();
                     FD_STAMP(13);  // place
+                    }
                     // conflict masks: earlier candidates of the same 64-batch within distance d. One work
                     // item per (candidate, quarter of its batch): 16 entries each, no divergent trip
                     // counts; each item writes its 16 bits of the candidate's 64-bit mask directly.
