@@ -34,6 +34,7 @@ constexpr int kLevels = 8;
 __device__ __forceinline__ int lvl_width(int l) { return l == 0 ? 12 : (l == 7 ? 4 : 8); }
 __device__ __forceinline__ int lvl_top(int l) { return l == 7 ? 64 : 12 + 8 * l; }  // bits consumed through l
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));  // packed (x, y) of a (y << 16) | x position
 
 // Diagnostic phase clocks (only when a.stamps is set), accumulated by thread 0 in LDS (L.st) and
 // written to a.stamps at the end: slot 15 keeps the last clock; FD_STAMP(k) adds the time since then
@@ -83,6 +84,8 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                                              uint32_t prior, int &s_acc, int &s_done) {
     const int lane = lane_id();
     const int d = a.dist;
+    const bool pk16 = a.rows + 3 * d < 65536 && a.cols + 3 * d < 65536;  // no wrap-around in 16-bit halves
+    const uint32_t w2 = 2u * static_cast<uint32_t>(d);
     int acc = s_acc;
     bool done = false;
     // Software pipeline: a batch's position, cell and conflict mask are loaded during the previous
@@ -116,10 +119,20 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                 if constexpr (GRID == 1) g[q] = grid[o];
                 else g[q] = __hip_atomic_load(&grid[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            if (pk16) {  // packed halves, as in the conflict masks (select_frame)
+                const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
 #pragma unroll
-            for (int q = 0; q < 9; ++q) {
-                const int gx = static_cast<int>(g[q] & 0xFFFFu), gy = static_cast<int>(g[q] >> 16);
-                if (g[q] != kEmpty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
+                for (int q = 0; q < 9; ++q) {
+                    const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
+                    const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
+                    if (g[q] != kEmpty && m <= w2) ok = false;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    const int gx = static_cast<int>(g[q] & 0xFFFFu), gy = static_cast<int>(g[q] >> 16);
+                    if (g[q] != kEmpty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
+                }
             }
         }
         if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n);
@@ -766,6 +779,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     // counts; each item writes its 16 bits of the candidate's 64-bit mask directly.
                     if (use_grid) {
                         uint16_t *cm16 = reinterpret_cast<uint16_t *>(buf);
+                        const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
+                        const uint32_t w2 = 2u * static_cast<uint32_t>(d);
                         for (int item = tid; item < 4 * c; item += nthr) {
                             const int p = item >> 2, q = item & 3;
                             const int bb = p & ~63, me = p - bb;
@@ -775,6 +790,24 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                                 const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
                                 const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb + 16 * q);  // broadcast
                                 const int lim = me - 16 * q;  // entries j < lim of this quarter are earlier
+                                if (pk16) {
+                                    // packed (x, y) halves: |ex - x| <= d  <=>  (ex - x + d) mod 2^16 <= 2d
+                                    // (no wrap-around: rows, cols + 3d < 2^16). Empty entries need no test:
+                                    // the greedy clears their bits (C &= ballot(ok)).
+                                    const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+#pragma unroll
+                                    for (int j4 = 0; j4 < 4; ++j4) {
+                                        const uint4 e4 = q4[j4];
+                                        const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                                        for (int t = 0; t < 4; ++t) {
+                                            const u16x2 dt = __builtin_bit_cast(u16x2, ev[t]) - base;
+                                            const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
+                                            bits |= (m <= w2 ? 1u : 0u) << (j4 * 4 + t);
+                                        }
+                                    }
+                                    if (lim < 16) bits &= (1u << lim) - 1u;
+                                } else
 #pragma unroll
                                 for (int j4 = 0; j4 < 4; ++j4) {
                                     const uint4 e4 = q4[j4];
