@@ -6,7 +6,7 @@
 // until `need` features exist (:67-69). Only the head of that order matters (640x480 noise: ~400
 // of ~27k candidates), so the list is never sorted whole: a radix descent over 64-bit keys (level 0
 // = the histogram the per-pixel kernel built while emitting) cuts it into chunks of
-// <= kSelectChunk keys from the top, each gathered to LDS, cut into sub-chunks that are merge-sorted
+// <= kSelectChunk keys from the top, each gathered to LDS, cut into sub-chunks that are ordered
 // and scanned in order by one wave in batches of 64 against an occupancy grid of (d+1)-sized cells
 // (<= 1 kept feature per cell).
 //
@@ -25,7 +25,7 @@ namespace {
 // Per-frame greedy selection (SelectGoodFeatures, feature_point_detector.cpp:54-88).
 // Candidates are visited in (response desc, raster index asc) order without a full sort: a radix
 // descent over the 64-bit key sk = (orderable response bits << 32) | ~idx cuts the frame's list into
-// consecutive chunks of <= kSelectChunk keys, each gathered into LDS, bitonic-sorted and scanned by
+// consecutive chunks of <= kSelectChunk keys, each gathered into LDS, ordered (bucket placement or merge sort) and scanned by
 // one wave. Accepted features live in an occupancy grid of (d+1)-sized cells: at most one accepted
 // feature per cell, so a Chebyshev-distance test needs the 3x3 neighbouring cells only.
 // ---------------------------------------------------------------------------------------------------
