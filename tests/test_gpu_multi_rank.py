@@ -74,3 +74,33 @@ def test_sharded_ranks_match_oracle(oracle, world):
     assert sorted(spans) == list(range(world))
     for p in procs:
         assert p.exitcode == 0
+
+
+def test_two_contexts_on_two_streams_match_oracle(oracle):
+    """The serving pipeline bench.py reports as headline_pipelined: consecutive frames alternate
+    between two contexts, each on its own stream, with no synchronisation between the streams."""
+    import torch
+
+    import feature_detector_amd as fd
+
+    dev = torch.device("cuda", 0)
+    frames = [oracle.make_frame("noise" if i % 2 else "checker", 300 + i, 240, 320) for i in range(8)]
+    ctxs = [fd.Context(0), fd.Context(0)]
+    streams = [torch.cuda.Stream(device=dev) for _ in ctxs]
+    dframes = [torch.from_numpy(f[None]).to(dev) for f in frames]
+    torch.cuda.synchronize()
+    outs = []
+    for i, f in enumerate(dframes):
+        k = i % 2
+        with torch.cuda.stream(streams[k]):
+            xy = torch.empty((1, 51, 2), dtype=torch.float32, device=dev)
+            cnt = torch.empty((1,), dtype=torch.int32, device=dev)
+            fd.detect_points("harris", f, need=50, min_feature_distance=20, min_valid_response=30.0,
+                             out=(xy, cnt), ctx=ctxs[k])
+            outs.append((xy, cnt))
+    torch.cuda.synchronize()
+    for f, (xy, cnt) in zip(frames, outs):
+        exp = oracle.detect(0, f, 20, 30.0, 50, sort_mode=1)[0]
+        np.testing.assert_array_equal(xy[0, : int(cnt[0])].cpu().numpy(), exp)
+    for c in ctxs:
+        c.close()
