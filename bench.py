@@ -536,10 +536,11 @@ def main():
     if args.batch == 1 and not args.no_graph:
         with phase(torch, "headline_pipelined"):
             p_ms, p_frames = run_pipelined(torch, fd, dev, args.detector, args.rows, args.cols, args.need, args.dist,
-                                           args.pattern, seed=4321 + rank)
+                                           args.pattern, seed=4321 + rank, nctx=4)
         out["headline_pipelined"] = {
-            "workload": "same batch-1 calls, consecutive frames alternating between 2 contexts/streams "
-                        "(per-pixel kernel of frame i+1 overlaps the selection of frame i); not `value`",
+            "workload": "same batch-1 calls, consecutive frames round-robin over 4 contexts/streams (up to 4 "
+                        "requests in flight: per-pixel kernels overlap other frames' single-workgroup selections; "
+                        "tools/pipe_sweep.py: 1/2/3/4/6 contexts); not `value`", "contexts": 4,
             "ms_per_frame": round(p_ms, 5), "mpix_s": round(args.rows * args.cols / (p_ms * 1e-3) / 1e6, 1),
             "frames": p_frames}
 
