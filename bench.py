@@ -194,7 +194,7 @@ def run_config(torch, fd, dev, detector, rows, cols, batch, pool, need, dist, pa
     ctx.reserve(KIND[detector], batch, rows, cols)
 
     def step(i):
-        fd.detect_points(detector, frames_pool[i % pool], need, dist, thr, out=(xy, cnt), ctx=ctx)
+        fd.detect_points(detector, frames_pool[i % pool], need, dist, thr, out=(xy, cnt), ctx=ctx, ties="raster")
 
     secs, done = timed_graph(torch, step, steps, warmup, use_graph, per_graph=pool, barrier=barrier)
     return secs, done, frames_pool, (xy, cnt)
@@ -223,7 +223,7 @@ def run_pipelined(torch, fd, dev, detector, rows, cols, need, dist, pattern, see
         for i in range(pool):
             k = i % nctx
             with torch.cuda.stream(streams[k]):
-                fd.detect_points(detector, frames_pool[i], need, dist, thr, out=outs[k], ctx=ctxs[k])
+                fd.detect_points(detector, frames_pool[i], need, dist, thr, out=outs[k], ctx=ctxs[k], ties="raster")
         for s in streams:
             main.wait_stream(s)
 
@@ -257,12 +257,12 @@ def run_config3(torch, fd, dev, seed, batch=64, rows=720, cols=1280, need=200, d
     ctx.reserve(fd.FD_FAST, batch, rows, cols)
 
     def step(i):
-        fd.detect_points("fast", pool[i % 2], need, dist, THR["fast"], out=(xy, cnt), ctx=ctx)
+        fd.detect_points("fast", pool[i % 2], need, dist, THR["fast"], out=(xy, cnt), ctx=ctx, ties="raster")
         fd.brief_compute(pool[i % 2], xy, cnt, length=256, half_patch_size=8, out=bits, ctx=ctx)
 
     secs, done = timed_graph(torch, step, steps, 2, True, per_graph=2)
     # the descriptor kernel alone: reps launches captured in one graph (keypoints from the last step)
-    fd.detect_points("fast", pool[0], need, dist, THR["fast"], out=(xy, cnt), ctx=ctx)
+    fd.detect_points("fast", pool[0], need, dist, THR["fast"], out=(xy, cnt), ctx=ctx, ties="raster")
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
@@ -368,10 +368,11 @@ def run_end_to_end(torch, fd, args, seconds=3.0):
     import numpy as np
 
     frames = make_frames(torch, args.pattern, 16, args.rows, args.cols, 31337, torch.device("cuda")).cpu().numpy()
-    fd.detect_points(args.detector, frames[0], args.need, args.dist, THR[args.detector])
+    fd.detect_points(args.detector, frames[0], args.need, args.dist, THR[args.detector], ties="raster")
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        fd.detect_points(args.detector, frames[n % len(frames)], args.need, args.dist, THR[args.detector])
+        fd.detect_points(args.detector, frames[n % len(frames)], args.need, args.dist, THR[args.detector],
+                         ties="raster")
         n += 1
     el = time.perf_counter() - t0
     return {"mpix_s": round(n * args.rows * args.cols / el / 1e6, 1), "ms_per_frame": round(el / n * 1e3, 4),

@@ -16,7 +16,7 @@ FD_HARRIS, FD_SHI_TOMASI, FD_FAST = 0, 1, 2
 EXPORTS = (
     "fd_ctx_create", "fd_ctx_destroy", "fd_last_error", "fd_ctx_set_stream", "fd_ctx_use_own_stream",
     "fd_ctx_get_stream",
-    "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_points_detect", "fd_points_candidates", "fd_points_response",
+    "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_ctx_set_tie_order", "fd_ctx_frame_status", "fd_points_detect", "fd_points_candidates", "fd_points_response",
     "fd_points_response_append",
     "fd_lsd_map", "fd_brief_compute", "fd_nn_select", "fd_nn_descriptors",
     "fd_build_info",
@@ -76,6 +76,8 @@ def load() -> ctypes.CDLL:
         "fd_ctx_synchronize": (i32, [P]),
         "fd_ctx_reserve": (i32, [P, i32, i32, i32, i32, i64]),
         "fd_ctx_stage": (i32, [P, P, i64, ctypes.POINTER(P)]),
+        "fd_ctx_set_tie_order": (i32, [P, i32]),
+        "fd_ctx_frame_status": (i32, [P, P, i32, i32]),
         "fd_points_detect": (i32, [P, i32, P, i32, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, u32, P, i32,
                                    P, i32]),
         "fd_points_candidates": (i32, [P, i32, P, i32, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, P, P, P,

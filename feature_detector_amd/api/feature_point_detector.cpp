@@ -49,6 +49,9 @@ fd_ctx *FeaturePointDetector::Context() {
         if (fd_ctx_create(device_, &ctx_) != FD_OK) {
             ctx_ = nullptr;
             error_ = "fd_ctx_create failed (no MI355X visible?)";
+        } else {
+            // the drop-in reproduces the reference's std::sort order of equal responses (:58-60)
+            (void)fd_ctx_set_tie_order(ctx_, FD_TIES_REFERENCE);
         }
     }
     return ctx_;

@@ -15,6 +15,7 @@ struct fd_ingest_slot {
     int32_t *dev_counts = nullptr;
     float *host_xy = nullptr;  // pinned
     int32_t *host_counts = nullptr;
+    uint32_t *host_status = nullptr;  // pinned: fd_ctx_frame_status of the slot's selection
     hipEvent_t uploaded = nullptr, done = nullptr;
     bool pending = false;
 };
@@ -35,6 +36,7 @@ void release(fd_ingest *g) {
         if (s.host_frames) (void)hipHostFree(s.host_frames);
         if (s.host_xy) (void)hipHostFree(s.host_xy);
         if (s.host_counts) (void)hipHostFree(s.host_counts);
+        if (s.host_status) (void)hipHostFree(s.host_status);
         if (s.dev_frames) (void)hipFree(s.dev_frames);
         if (s.dev_xy) (void)hipFree(s.dev_xy);
         if (s.dev_counts) (void)hipFree(s.dev_counts);
@@ -69,6 +71,7 @@ extern "C" int fd_ingest_create(fd_ctx *ctx, int kind, int batch, int rows, int 
         ok = ok && hipHostMalloc(reinterpret_cast<void **>(&s.host_frames), fbytes, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipHostMalloc(reinterpret_cast<void **>(&s.host_xy), xbytes, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipHostMalloc(reinterpret_cast<void **>(&s.host_counts), cbytes, hipHostMallocDefault) == hipSuccess;
+        ok = ok && hipHostMalloc(reinterpret_cast<void **>(&s.host_status), cbytes, hipHostMallocDefault) == hipSuccess;
         ok = ok && hipMalloc(reinterpret_cast<void **>(&s.dev_frames), fbytes) == hipSuccess;
         ok = ok && hipMalloc(reinterpret_cast<void **>(&s.dev_xy), xbytes) == hipSuccess;
         ok = ok && hipMalloc(reinterpret_cast<void **>(&s.dev_counts), cbytes) == hipSuccess;
@@ -114,7 +117,7 @@ extern "C" int fd_ingest_submit(fd_ingest *g, int slot, const fd_point_opts *opt
     const size_t xbytes = sizeof(float) * 2 * static_cast<size_t>(g->out_stride) * g->batch;
     if (hipMemcpyAsync(s.host_xy, s.dev_xy, xbytes, hipMemcpyDeviceToHost, cs) != hipSuccess ||
         hipMemcpyAsync(s.host_counts, s.dev_counts, sizeof(int32_t) * g->batch, hipMemcpyDeviceToHost, cs) != hipSuccess ||
-        hipEventRecord(s.done, cs) != hipSuccess)
+        fd_ctx_frame_status(g->ctx, s.host_status, g->batch, 1) != FD_OK || hipEventRecord(s.done, cs) != hipSuccess)
         return FD_ERR_HIP;
     s.pending = true;
     return FD_OK;
@@ -126,12 +129,11 @@ extern "C" int fd_ingest_wait(fd_ingest *g, int slot, const float **xy, const in
     if (!s.pending) return FD_ERR_INVALID;
     if (hipEventSynchronize(s.done) != hipSuccess) return FD_ERR_HIP;
     s.pending = false;
-    // the selection's consistency flags (bits 25-31 of a count), as fd_points_detect checks them for
-    // host outputs; and the capacity check
+    // the selection's consistency guards (the slot's status words), as fd_points_detect checks them
+    // for host outputs; and the capacity check
     for (int b = 0; b < g->batch; ++b) {
-        const uint32_t v = static_cast<uint32_t>(s.host_counts[b]);
-        if (v & 0xFE000000u) return FD_ERR_HIP;
-        if (static_cast<int32_t>(v) > g->out_stride) return FD_ERR_CAPACITY;
+        if (s.host_status[b] & FD_FRAME_GUARD) return FD_ERR_HIP;
+        if (s.host_counts[b] > g->out_stride) return FD_ERR_CAPACITY;
     }
     if (xy) *xy = s.host_xy;
     if (counts) *counts = s.host_counts;

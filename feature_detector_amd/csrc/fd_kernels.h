@@ -81,7 +81,11 @@ struct SelectArgs {
     uint32_t *grid_global;  // [batch][grid_w * grid_h] when the grid does not fit LDS (slow path)
     float *out_xy;
     int out_stride;
-    int32_t *out_counts;
+    int32_t *out_counts;  // plain feature counts (no flag bits)
+    // [batch] per-frame status (fd_hip.h FD_FRAME_*: tie in the scanned prefix, guard flags) and
+    // [batch] candidate count of the frame (kept for a tie resolution after the list count is reset)
+    uint32_t *status;
+    uint32_t *cand_n;
     // key map: 32-bit key = (float_key(response) - key_base) << key_lz; all candidates have
     // responses > min_valid_response, so key_base = float_key(min_valid_response) and key_lz spreads
     // the possible response range over the full 32 bits (finer level-0 bins).
@@ -99,6 +103,15 @@ struct SelectArgs {
     uint32_t *seg_bad;      // [batch], reset by k_select
     int nseg;               // segments per frame
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
+};
+
+// Greedy selection over candidates given in an explicit order (FD_TIES_REFERENCE: the reference's
+// std::sort permutation of a frame, computed on the host), one workgroup per listed frame.
+struct OrderedArgs {
+    const uint32_t *order;  // raster indices (row * cols + col), each frame's run in visiting order
+    const int64_t *offset;  // [n_frames] start of frame j's run in `order`
+    const uint32_t *count;  // [n_frames] its length
+    const int32_t *frame;   // [n_frames] frame index (into SelectArgs' per-frame arrays)
 };
 
 struct CompactArgs {
@@ -179,6 +192,7 @@ hipError_t launch_fast_mask_scan(const uint32_t *mask, int mask_wpr, int batch, 
 hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s);
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s);
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
+hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
 hipError_t launch_brief(const BriefArgs &a, hipStream_t s);

@@ -43,6 +43,13 @@ struct fd_ctx {
     DevBuf b_uv, b_counts, b_bits, b_valid;
     DevBuf n_heat, n_map, n_xy, n_counts, n_out;
     DevBuf dbg;
+    // per-frame status of the last selection call: [batch] FD_FRAME_* flags, then [batch] candidate
+    // counts (internal); status_batch = its frame count (0: no selection call yet)
+    DevBuf status;
+    int status_batch = 0;
+    int tie_order = FD_TIES_RASTER;
+    DevBuf ord, ord_meta;  // FD_TIES_REFERENCE: host-computed visiting orders of flagged frames
+    hipEvent_t xev = nullptr;  // orders a stream switch after the old stream's work (fd_ctx_set_stream)
     // FAST offset table cache
     int64_t off_n = -1;
     float off_thr = 0.0f;
@@ -63,9 +70,15 @@ int fail(fd_ctx *c, int code, const std::string &msg) {
             return fail((ctx), FD_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));                   \
     } while (0)
 
-hipError_t ensure(DevBuf &b, size_t bytes) {
+// Grow-only workspace. Growing while the context stream is being captured into a HIP graph would put
+// an allocation into the capture: that fails here with hipErrorStreamCaptureUnsupported (reserve the
+// shape first, fd_ctx_reserve, or run the call once before capturing).
+hipError_t ensure(fd_ctx *c, DevBuf &b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.n >= bytes) return hipSuccess;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (c && c->stream && hipStreamIsCapturing(c->stream, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+        return hipErrorStreamCaptureUnsupported;
     if (b.p) {
         hipError_t e = hipFree(b.p);
         if (e != hipSuccess) return e;
@@ -171,7 +184,7 @@ int setup_priors(fd_ctx *c, int batch, int rows, int cols, int dist, const float
         if (prior_counts[b] < 0) return fail(c, FD_ERR_INVALID, "negative prior count");
         pi.total += prior_counts[b];
     }
-    FD_HIP_TRY(c, ensure(c->prior_counts, sizeof(int32_t) * batch));
+    FD_HIP_TRY(c, ensure(c, c->prior_counts, sizeof(int32_t) * batch));
     FD_HIP_TRY(c, hipMemcpyAsync(c->prior_counts.p, prior_counts, sizeof(int32_t) * batch, hipMemcpyHostToDevice,
                                  c->stream));
     pi.counts_dev = as<int32_t>(c->prior_counts);
@@ -185,9 +198,9 @@ int setup_priors(fd_ctx *c, int batch, int rows, int cols, int dist, const float
         for (int i = 0; i < prior_counts[b]; ++i) frame_of.push_back(b);
     pi.wpr = (cols + 31) / 32;
     const size_t mbytes = sizeof(uint32_t) * static_cast<size_t>(batch) * rows * pi.wpr;
-    FD_HIP_TRY(c, ensure(c->prior_xy, sizeof(float) * 2 * pi.total));
-    FD_HIP_TRY(c, ensure(c->prior_frame, sizeof(int32_t) * pi.total));
-    FD_HIP_TRY(c, ensure(c->mask, mbytes));
+    FD_HIP_TRY(c, ensure(c, c->prior_xy, sizeof(float) * 2 * pi.total));
+    FD_HIP_TRY(c, ensure(c, c->prior_frame, sizeof(int32_t) * pi.total));
+    FD_HIP_TRY(c, ensure(c, c->mask, mbytes));
     FD_HIP_TRY(c, hipMemcpyAsync(c->prior_xy.p, prior_xy, sizeof(float) * 2 * pi.total, hipMemcpyHostToDevice,
                                  c->stream));
     FD_HIP_TRY(c, hipMemcpyAsync(c->prior_frame.p, frame_of.data(), sizeof(int32_t) * pi.total,
@@ -221,7 +234,7 @@ int stage_frames(fd_ctx *c, const uint8_t *frames, int on_device, int batch, int
         dframes = frames;
         return FD_OK;
     }
-    FD_HIP_TRY(c, ensure(c->frames, bytes));
+    FD_HIP_TRY(c, ensure(c, c->frames, bytes));
     FD_HIP_TRY(c, hipMemcpyAsync(c->frames.p, frames, bytes, hipMemcpyHostToDevice, c->stream));
     dframes = as<uint8_t>(c->frames);
     return FD_OK;
@@ -258,16 +271,17 @@ int64_t detect_list_cap(int kind, int rows, int cols) {
 struct SelectBufs {
     uint32_t *hist0, *list_count, *pre_count, *seg_bad;
     uint64_t *pre_keys;
+    uint32_t *status, *cand_n;
 };
 
 // Candidate lists and the (self-resetting) control block for `batch` frames.
 int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
-    FD_HIP_TRY(c, ensure(c->list_resp, sizeof(float) * cap * batch));
-    FD_HIP_TRY(c, ensure(c->list_idx, sizeof(uint32_t) * cap * batch));
-    FD_HIP_TRY(c, ensure(c->pre_keys, sizeof(uint64_t) * fdk::kSelectChunk * batch));
+    FD_HIP_TRY(c, ensure(c, c->list_resp, sizeof(float) * cap * batch));
+    FD_HIP_TRY(c, ensure(c, c->list_idx, sizeof(uint32_t) * cap * batch));
+    FD_HIP_TRY(c, ensure(c, c->pre_keys, sizeof(uint64_t) * fdk::kSelectChunk * batch));
     const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 3);
     if (c->selctl.n < ctl) {
-        FD_HIP_TRY(c, ensure(c->selctl, ctl));
+        FD_HIP_TRY(c, ensure(c, c->selctl, ctl));
         c->sel_dirty = true;
     }
     if (c->sel_dirty) {
@@ -280,6 +294,9 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     sb.pre_count = sb.list_count + batch;
     sb.seg_bad = sb.pre_count + batch;
     sb.pre_keys = as<uint64_t>(c->pre_keys);
+    FD_HIP_TRY(c, ensure(c, c->status, sizeof(uint32_t) * 2 * static_cast<size_t>(batch)));
+    sb.status = as<uint32_t>(c->status);
+    sb.cand_n = sb.status + batch;
     return FD_OK;
 }
 
@@ -324,6 +341,84 @@ bool use_seg_lists(int blocks_per_frame, int rows, int cols) {
     return blocks_per_frame <= 1024 && static_cast<int64_t>(rows) * cols < (1 << 20);
 }
 
+std::string hex(uint32_t v) {
+    char t[16];
+    std::snprintf(t, sizeof t, "%x", v);
+    return std::string(t);
+}
+
+// FD_TIES_REFERENCE (fd_ctx_set_tie_order): frames whose greedy scan met equal responses
+// (FD_FRAME_TIES from k_select) are selected again in the reference's own order. The reference sorts
+// its raster-ordered candidates with an unstable std::sort (feature_point_detector.cpp:58-60), whose
+// permutation of equal responses is defined only by libstdc++'s introsort run on that exact sequence:
+// the frame's candidate list (still in the workspace, unordered) is copied back, put in raster order
+// (the order ComputeCandidates pushes them, feature_point_harris_detector.cpp:120-137,
+// feature_point_fast_detector.cpp:83-98), sorted here with std::sort and the reference comparator,
+// and the resulting visiting order goes back to the GPU for the greedy pass (k_select_ordered).
+int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb) {
+    std::vector<uint32_t> st(2 * static_cast<size_t>(batch));
+    FD_HIP_TRY(c, hipMemcpyAsync(st.data(), sb.status, sizeof(uint32_t) * st.size(), hipMemcpyDeviceToHost, c->stream));
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<int32_t> frames;
+    for (int b = 0; b < batch; ++b) {
+        if (st[b] & FD_FRAME_GUARD)  // (read here anyway: reported for device outputs too)
+            return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (status 0x" + hex(st[b]) +
+                                           ", frame " + std::to_string(b) + ")");
+        if (st[b] & FD_FRAME_TIES) frames.push_back(b);
+    }
+    if (frames.empty()) return FD_OK;
+    struct Cand {
+        float resp;
+        uint32_t idx;
+    };
+    std::vector<std::vector<Cand>> lists(frames.size());
+    std::vector<std::vector<float>> resp(frames.size());
+    std::vector<std::vector<uint32_t>> idx(frames.size());
+    for (size_t j = 0; j < frames.size(); ++j) {
+        const int f = frames[j];
+        const size_t n = std::min<size_t>(st[batch + f], static_cast<size_t>(s.list_cap));
+        resp[j].resize(n);
+        idx[j].resize(n);
+        const size_t o = static_cast<size_t>(f) * static_cast<size_t>(s.list_cap);
+        FD_HIP_TRY(c, hipMemcpyAsync(resp[j].data(), s.list_resp + o, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipMemcpyAsync(idx[j].data(), s.list_idx + o, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    }
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> order;
+    std::vector<int64_t> offset(frames.size());
+    std::vector<uint32_t> count(frames.size());
+    for (size_t j = 0; j < frames.size(); ++j) {
+        std::vector<Cand> &v = lists[j];
+        v.resize(resp[j].size());
+        for (size_t i = 0; i < v.size(); ++i) v[i] = {resp[j][i], idx[j][i]};
+        // raster order (indices are unique), then the reference's sort (:58-60)
+        std::sort(v.begin(), v.end(), [](const Cand &a, const Cand &b) { return a.idx < b.idx; });
+        std::sort(v.begin(), v.end(), [](const Cand &a, const Cand &b) { return a.resp > b.resp; });
+        offset[j] = static_cast<int64_t>(order.size());
+        count[j] = static_cast<uint32_t>(v.size());
+        for (const Cand &e : v) order.push_back(e.idx);
+    }
+    const size_t nf = frames.size();
+    const size_t meta = (sizeof(int64_t) + sizeof(uint32_t) + sizeof(int32_t)) * nf;
+    FD_HIP_TRY(c, ensure(c, c->ord, sizeof(uint32_t) * std::max<size_t>(order.size(), 1)));
+    FD_HIP_TRY(c, ensure(c, c->ord_meta, meta));
+    std::vector<uint8_t> mbuf(meta);
+    std::memcpy(mbuf.data(), offset.data(), sizeof(int64_t) * nf);
+    std::memcpy(mbuf.data() + sizeof(int64_t) * nf, count.data(), sizeof(uint32_t) * nf);
+    std::memcpy(mbuf.data() + (sizeof(int64_t) + sizeof(uint32_t)) * nf, frames.data(), sizeof(int32_t) * nf);
+    FD_HIP_TRY(c, hipMemcpyAsync(c->ord.p, order.data(), sizeof(uint32_t) * order.size(), hipMemcpyHostToDevice, c->stream));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->ord_meta.p, mbuf.data(), meta, hipMemcpyHostToDevice, c->stream));
+    fdk::OrderedArgs o{};
+    o.order = as<uint32_t>(c->ord);
+    o.offset = reinterpret_cast<const int64_t *>(c->ord_meta.p);
+    o.count = reinterpret_cast<const uint32_t *>(static_cast<uint8_t *>(c->ord_meta.p) + sizeof(int64_t) * nf);
+    o.frame = reinterpret_cast<const int32_t *>(static_cast<uint8_t *>(c->ord_meta.p) +
+                                                (sizeof(int64_t) + sizeof(uint32_t)) * nf);
+    FD_HIP_TRY(c, fdk::launch_select_ordered(s, o, static_cast<int>(nf), c->stream));
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host vectors above are the copies' sources
+    return FD_OK;
+}
+
 // K4 (k_gather + k_select) on the candidate lists, features into out_xy / out_counts (device, or copied
 // back to the host and checked when !outputs_on_device).
 int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const SelectBufs &sb, float *out_xy,
@@ -349,15 +444,15 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         s.grid_h = (rows + s.dist) / (s.dist + 1);
         const int64_t cells = static_cast<int64_t>(s.grid_w + 2) * (s.grid_h + 2);  // bordered grid
         if (cells > fdk::kGridLdsCells) {
-            FD_HIP_TRY(c, ensure(c->grid, sizeof(uint32_t) * cells * batch));
+            FD_HIP_TRY(c, ensure(c, c->grid, sizeof(uint32_t) * cells * batch));
             s.grid_global = as<uint32_t>(c->grid);
         }
     }
     float *dxy = out_xy;
     int32_t *dcnt = out_counts;
     if (!outputs_on_device) {
-        FD_HIP_TRY(c, ensure(c->out_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch));
-        FD_HIP_TRY(c, ensure(c->out_counts, sizeof(int32_t) * batch));
+        FD_HIP_TRY(c, ensure(c, c->out_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch));
+        FD_HIP_TRY(c, ensure(c, c->out_counts, sizeof(int32_t) * batch));
         dxy = as<float>(c->out_xy);
         dcnt = as<int32_t>(c->out_counts);
     }
@@ -366,6 +461,8 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.out_counts = dcnt;
     s.key_base = q.key_base;
     s.key_lz = q.key_lz;
+    s.status = sb.status;
+    s.cand_n = sb.cand_n;
     // Small batches of large frames: spread the first chunk's gather over ~256 workgroups in its own
     // kernel (~9 us of fixed cost: pays off once one workgroup's pass over the list costs more, i.e.
     // from about a megapixel per frame; measured at 640x480: break-even).
@@ -383,12 +480,13 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     }
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
-        FD_HIP_TRY(c, ensure(c->dbg, sizeof(uint64_t) * 32 * batch));
+        FD_HIP_TRY(c, ensure(c, c->dbg, sizeof(uint64_t) * 32 * batch));
         FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 32 * batch, c->stream));
         s.stamps = as<uint64_t>(c->dbg);
     }
     FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
     c->sel_dirty = false;
+    c->status_batch = batch;
     if (stamps) {
         uint64_t h[32];
         FD_HIP_TRY(c, hipMemcpyAsync(h, c->dbg.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -404,19 +502,23 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         for (int i = 16; i < 32; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
         std::fprintf(stderr, "\n");
     }
+    if (c->tie_order == FD_TIES_REFERENCE && !q.tie_idx_desc) {
+        const int rc = resolve_ties(c, s, batch, sb);
+        if (rc) return rc;
+    }
     if (!outputs_on_device) {
+        std::vector<uint32_t> st(static_cast<size_t>(batch));
         FD_HIP_TRY(c, hipMemcpyAsync(out_xy, dxy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
                                      hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dcnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipMemcpyAsync(st.data(), sb.status, sizeof(uint32_t) * batch, hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         for (int b = 0; b < batch; ++b) {
-            if (static_cast<uint32_t>(out_counts[b]) & 0x40000000u)
+            if (st[b] & FD_FRAME_VALUE_RANGE)
                 return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": a value above the declared maximum "
                                                "(fd_nn_opts::max_response)");
-            if (static_cast<uint32_t>(out_counts[b]) & 0xFE000000u)
-                return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (flags 0x" +
-                                               [](uint32_t v) { char t[16]; std::snprintf(t, sizeof t, "%x", v); return std::string(t); }(
-                                                   static_cast<uint32_t>(out_counts[b]) >> 25) +
+            if (st[b] & FD_FRAME_GUARD)
+                return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (status 0x" + hex(st[b]) +
                                                ", frame " + std::to_string(b) + ")");
             if (out_counts[b] > out_stride) return fail(c, FD_ERR_CAPACITY, "out_stride smaller than the features found");
         }
@@ -464,23 +566,68 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
-                      &c->segdesc,  &c->seghead};
+                      &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta};
     for (DevBuf *b : bufs) release(*b);
+    if (c->xev) (void)hipEventDestroy(c->xev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
 
 const char *fd_last_error(const fd_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
+// The workspace is shared by every call on the context, so a new stream must not start before the
+// old one's work: the switch records an event on the old stream and makes the new one wait for it
+// (skipped when the new stream is being captured: a capture may not wait on uncaptured work, so the
+// caller orders it, e.g. with torch's stream.wait_stream before capturing).
+static int switch_stream(fd_ctx *c, hipStream_t s) {
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    if (s == c->stream) return FD_OK;
+    if (s) {
+        int dev = -1;
+        FD_HIP_TRY(c, hipStreamGetDevice(s, &dev));
+        if (dev != c->device)
+            return fail(c, FD_ERR_INVALID, "stream belongs to device " + std::to_string(dev) + ", the context to device " +
+                                               std::to_string(c->device));
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    FD_HIP_TRY(c, hipStreamIsCapturing(s, &cs));
+    hipStreamCaptureStatus cs_old = hipStreamCaptureStatusNone;
+    FD_HIP_TRY(c, hipStreamIsCapturing(c->stream, &cs_old));
+    if (cs == hipStreamCaptureStatusNone && cs_old == hipStreamCaptureStatusNone) {
+        if (!c->xev) FD_HIP_TRY(c, hipEventCreateWithFlags(&c->xev, hipEventDisableTiming));
+        FD_HIP_TRY(c, hipEventRecord(c->xev, c->stream));
+        FD_HIP_TRY(c, hipStreamWaitEvent(s, c->xev, 0));
+    }
+    c->stream = s;
+    return FD_OK;
+}
+
 int fd_ctx_set_stream(fd_ctx *c, void *s) {
     if (!c) return FD_ERR_INVALID;
-    c->stream = static_cast<hipStream_t>(s);
-    return FD_OK;
+    return switch_stream(c, static_cast<hipStream_t>(s));
 }
 
 int fd_ctx_use_own_stream(fd_ctx *c) {
     if (!c) return FD_ERR_INVALID;
-    c->stream = c->own_stream;
+    return switch_stream(c, c->own_stream);
+}
+
+int fd_ctx_set_tie_order(fd_ctx *c, int order) {
+    if (!c) return FD_ERR_INVALID;
+    if (order != FD_TIES_RASTER && order != FD_TIES_REFERENCE) return fail(c, FD_ERR_INVALID, "unknown tie order");
+    c->tie_order = order;
+    return FD_OK;
+}
+
+int fd_ctx_frame_status(fd_ctx *c, uint32_t *dst, int batch, int async) {
+    if (!c) return FD_ERR_INVALID;
+    if (!dst || batch < 0) return fail(c, FD_ERR_INVALID, "bad arguments");
+    if (batch > c->status_batch)
+        return fail(c, FD_ERR_INVALID, "the last selection call had " + std::to_string(c->status_batch) + " frames");
+    if (batch == 0) return FD_OK;
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    FD_HIP_TRY(c, hipMemcpyAsync(dst, c->status.p, sizeof(uint32_t) * batch, hipMemcpyDefault, c->stream));
+    if (!async) FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
     return FD_OK;
 }
 
@@ -496,7 +643,7 @@ int fd_ctx_synchronize(fd_ctx *c) {
 int fd_ctx_stage(fd_ctx *c, const void *host, int64_t bytes, const uint8_t **device_out) {
     if (!c || !host || bytes < 0 || !device_out) return fail(c, FD_ERR_INVALID, "bad arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
-    FD_HIP_TRY(c, ensure(c->frames, static_cast<size_t>(bytes)));
+    FD_HIP_TRY(c, ensure(c, c->frames, static_cast<size_t>(bytes)));
     FD_HIP_TRY(c, hipMemcpyAsync(c->frames.p, host, static_cast<size_t>(bytes), hipMemcpyHostToDevice, c->stream));
     FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
     *device_out = as<uint8_t>(c->frames);
@@ -511,20 +658,25 @@ int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t m
     SelectBufs sb{};
     rc = select_buffers(c, batch, cap, sb);
     if (rc) return rc;
-    FD_HIP_TRY(c, ensure(c->prior_counts, sizeof(int32_t) * batch));
+    FD_HIP_TRY(c, ensure(c, c->prior_counts, sizeof(int32_t) * batch));
     if (max_prior_total > 0) {
-        FD_HIP_TRY(c, ensure(c->prior_xy, sizeof(float) * 2 * max_prior_total));
-        FD_HIP_TRY(c, ensure(c->prior_frame, sizeof(int32_t) * max_prior_total));
-        FD_HIP_TRY(c, ensure(c->mask, sizeof(uint32_t) * static_cast<size_t>(batch) * rows * ((cols + 31) / 32)));
+        FD_HIP_TRY(c, ensure(c, c->prior_xy, sizeof(float) * 2 * max_prior_total));
+        FD_HIP_TRY(c, ensure(c, c->prior_frame, sizeof(int32_t) * max_prior_total));
+        FD_HIP_TRY(c, ensure(c, c->mask, sizeof(uint32_t) * static_cast<size_t>(batch) * rows * ((cols + 31) / 32)));
     }
     if (kind == FD_FAST) {
         rc = build_offsets(c, std::max<int64_t>(0, static_cast<int64_t>(rows - 6) * (cols - 6)), c->off_thr);
         if (rc) return rc;
+        if (max_prior_total > 0) {  // masked FAST: the mask scan's prefix tables
+            FD_HIP_TRY(c, ensure(c, c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
+            FD_HIP_TRY(c, ensure(c, c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * ((cols + 31) / 32)));
+        }
     }
+    FD_HIP_TRY(c, ensure(c, c->status, sizeof(uint32_t) * 2 * static_cast<size_t>(batch)));
     const PointGeom g = point_geom(kind, batch, rows, cols);
     if (!g.empty && use_seg_lists(g.blocks_per_frame, rows, cols)) {
-        FD_HIP_TRY(c, ensure(c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
-        FD_HIP_TRY(c, ensure(c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
+        FD_HIP_TRY(c, ensure(c, c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
+        FD_HIP_TRY(c, ensure(c, c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
     }
     return FD_OK;
 }
@@ -569,10 +721,10 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     a.hist0 = sb.hist0;
     const bool seg = !g.empty && use_seg_lists(g.blocks_per_frame, rows, cols);
     if (seg) {
-        FD_HIP_TRY(c, ensure(c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
+        FD_HIP_TRY(c, ensure(c, c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
         a.segdesc = as<uint2>(c->segdesc);
         a.seg_bad = sb.seg_bad;
-        FD_HIP_TRY(c, ensure(c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
+        FD_HIP_TRY(c, ensure(c, c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
         a.seghead = as<uint64_t>(c->seghead);
     }
     if (kind == FD_FAST && !g.empty) {
@@ -586,8 +738,8 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
         if (kind == FD_FAST) {
             if (pi.mask) {
                 if (rows > 4096) return fail(c, FD_ERR_INVALID, "FAST with prior features supports rows <= 4096");
-                FD_HIP_TRY(c, ensure(c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
-                FD_HIP_TRY(c, ensure(c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * pi.wpr));
+                FD_HIP_TRY(c, ensure(c, c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
+                FD_HIP_TRY(c, ensure(c, c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * pi.wpr));
                 FD_HIP_TRY(c, fdk::launch_fast_mask_scan(pi.mask, pi.wpr, batch, rows, cols, as<int32_t>(c->row_base),
                                                          as<int32_t>(c->word_pref), c->stream));
                 a.row_base = as<int32_t>(c->row_base);
@@ -681,15 +833,15 @@ int fd_points_candidates(fd_ctx *c, int kind, const uint8_t *frames, int frames_
     const PointGeom g = point_geom(kind, batch, rows, cols);
     const int segcap = kind == FD_FAST ? fdk::kSegFast : fdk::kSegCorner;
     const size_t nseg = static_cast<size_t>(batch) * rows * g.tiles_x;
-    FD_HIP_TRY(c, ensure(c->seg_cnt, sizeof(int32_t) * nseg));
-    FD_HIP_TRY(c, ensure(c->seg, sizeof(fdk::Cand) * nseg * segcap));
+    FD_HIP_TRY(c, ensure(c, c->seg_cnt, sizeof(int32_t) * nseg));
+    FD_HIP_TRY(c, ensure(c, c->seg, sizeof(fdk::Cand) * nseg * segcap));
     const size_t npx = static_cast<size_t>(batch) * rows * cols;
     float *dmap = nullptr;
     if (out_response_map) {
         if (outputs_on_device) {
             dmap = out_response_map;
         } else {
-            FD_HIP_TRY(c, ensure(c->resp_map, sizeof(float) * npx));
+            FD_HIP_TRY(c, ensure(c, c->resp_map, sizeof(float) * npx));
             dmap = as<float>(c->resp_map);
         }
         FD_HIP_TRY(c, hipMemsetAsync(dmap, 0, sizeof(float) * npx, c->stream));
@@ -699,10 +851,10 @@ int fd_points_candidates(fd_ctx *c, int kind, const uint8_t *frames, int frames_
     int64_t *dc = out_counts;
     const size_t ncap = static_cast<size_t>(std::max<int64_t>(cand_cap, 1)) * batch;
     if (!outputs_on_device) {
-        FD_HIP_TRY(c, ensure(c->c_resp, sizeof(float) * ncap));
-        FD_HIP_TRY(c, ensure(c->c_x, sizeof(int32_t) * ncap));
-        FD_HIP_TRY(c, ensure(c->c_y, sizeof(int32_t) * ncap));
-        FD_HIP_TRY(c, ensure(c->c_counts, sizeof(int64_t) * batch));
+        FD_HIP_TRY(c, ensure(c, c->c_resp, sizeof(float) * ncap));
+        FD_HIP_TRY(c, ensure(c, c->c_x, sizeof(int32_t) * ncap));
+        FD_HIP_TRY(c, ensure(c, c->c_y, sizeof(int32_t) * ncap));
+        FD_HIP_TRY(c, ensure(c, c->c_counts, sizeof(int64_t) * batch));
         dr = as<float>(c->c_resp);
         dx = as<int32_t>(c->c_x);
         dy = as<int32_t>(c->c_y);
@@ -732,8 +884,8 @@ int fd_points_candidates(fd_ctx *c, int kind, const uint8_t *frames, int frames_
             if (rc) return rc;
             if (pi.mask) {
                 if (rows > 4096) return fail(c, FD_ERR_INVALID, "FAST with prior features supports rows <= 4096");
-                FD_HIP_TRY(c, ensure(c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
-                FD_HIP_TRY(c, ensure(c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * pi.wpr));
+                FD_HIP_TRY(c, ensure(c, c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
+                FD_HIP_TRY(c, ensure(c, c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * pi.wpr));
                 FD_HIP_TRY(c, fdk::launch_fast_mask_scan(pi.mask, pi.wpr, batch, rows, cols, as<int32_t>(c->row_base),
                                                          as<int32_t>(c->word_pref), c->stream));
                 a.row_base = as<int32_t>(c->row_base);
@@ -801,24 +953,24 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         dv = valid;
     } else {
         if (norm) {
-            FD_HIP_TRY(c, ensure(c->l_norm, sizeof(float) * nmap));
+            FD_HIP_TRY(c, ensure(c, c->l_norm, sizeof(float) * nmap));
             dn = as<float>(c->l_norm);
         }
         if (angle) {
-            FD_HIP_TRY(c, ensure(c->l_angle, sizeof(float) * nmap));
+            FD_HIP_TRY(c, ensure(c, c->l_angle, sizeof(float) * nmap));
             da = as<float>(c->l_angle);
         }
     }
     if (dv == nullptr) {  // the valid map is needed internally for the ordered scatter
-        FD_HIP_TRY(c, ensure(c->l_valid, nmap));
+        FD_HIP_TRY(c, ensure(c, c->l_valid, nmap));
         dv = as<uint8_t>(c->l_valid);
     }
 
     int32_t *di = valid_idx;
     int64_t *dc = valid_counts;
     if (!outputs_on_device) {
-        FD_HIP_TRY(c, ensure(c->l_idx, sizeof(int32_t) * static_cast<size_t>(std::max<int64_t>(idx_cap, 1)) * batch));
-        FD_HIP_TRY(c, ensure(c->l_counts, sizeof(int64_t) * batch));
+        FD_HIP_TRY(c, ensure(c, c->l_idx, sizeof(int32_t) * static_cast<size_t>(std::max<int64_t>(idx_cap, 1)) * batch));
+        FD_HIP_TRY(c, ensure(c, c->l_counts, sizeof(int64_t) * batch));
         di = as<int32_t>(c->l_idx);
         dc = as<int64_t>(c->l_counts);
     }
@@ -849,10 +1001,10 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         a.angle = da;
         a.valid = dv;
         const size_t ncnt = static_cast<size_t>(batch) * mc * a.chunks;
-        FD_HIP_TRY(c, ensure(c->l_cnt, sizeof(int32_t) * ncnt));
-        FD_HIP_TRY(c, ensure(c->l_base, sizeof(int32_t) * ncnt));
+        FD_HIP_TRY(c, ensure(c, c->l_cnt, sizeof(int32_t) * ncnt));
+        FD_HIP_TRY(c, ensure(c, c->l_base, sizeof(int32_t) * ncnt));
         a.words = (a.chunk_h + 31) / 32;
-        FD_HIP_TRY(c, ensure(c->l_bits, sizeof(uint32_t) * ncnt * a.words));
+        FD_HIP_TRY(c, ensure(c, c->l_bits, sizeof(uint32_t) * ncnt * a.words));
         a.rowbits = as<uint32_t>(c->l_bits);
         a.col_cnt = as<int32_t>(c->l_cnt);
         a.col_base = as<int32_t>(c->l_base);
@@ -911,19 +1063,19 @@ int fd_brief_compute(fd_ctx *c, const uint8_t *frames, int frames_on_device, int
         a.out_bits = out_bits;
         a.out_valid = out_valid;
     } else {
-        FD_HIP_TRY(c, ensure(c->b_uv, sizeof(float) * 2 * slots));
-        FD_HIP_TRY(c, ensure(c->b_bits, sizeof(uint32_t) * nw * slots));
+        FD_HIP_TRY(c, ensure(c, c->b_uv, sizeof(float) * 2 * slots));
+        FD_HIP_TRY(c, ensure(c, c->b_bits, sizeof(uint32_t) * nw * slots));
         FD_HIP_TRY(c, hipMemcpyAsync(c->b_uv.p, uv, sizeof(float) * 2 * slots, hipMemcpyHostToDevice, c->stream));
         a.uv = as<float>(c->b_uv);
         a.out_bits = as<uint32_t>(c->b_bits);
         if (counts) {
-            FD_HIP_TRY(c, ensure(c->b_counts, sizeof(int32_t) * batch));
+            FD_HIP_TRY(c, ensure(c, c->b_counts, sizeof(int32_t) * batch));
             FD_HIP_TRY(c, hipMemcpyAsync(c->b_counts.p, counts, sizeof(int32_t) * batch, hipMemcpyHostToDevice,
                                          c->stream));
             a.counts = as<int32_t>(c->b_counts);
         }
         if (out_valid) {
-            FD_HIP_TRY(c, ensure(c->b_valid, slots));
+            FD_HIP_TRY(c, ensure(c, c->b_valid, slots));
             a.out_valid = as<uint8_t>(c->b_valid);
         }
     }
@@ -960,7 +1112,7 @@ int fd_nn_select(fd_ctx *c, const float *heatmap, int heatmap_on_device, int bat
     const int64_t npx = static_cast<int64_t>(rows) * cols;
     const float *dheat = heatmap;
     if (!heatmap_on_device) {
-        FD_HIP_TRY(c, ensure(c->n_heat, sizeof(float) * npx * batch));
+        FD_HIP_TRY(c, ensure(c, c->n_heat, sizeof(float) * npx * batch));
         FD_HIP_TRY(c, hipMemcpyAsync(c->n_heat.p, heatmap, sizeof(float) * npx * batch, hipMemcpyHostToDevice, c->stream));
         dheat = as<float>(c->n_heat);
     }
@@ -1033,7 +1185,7 @@ int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int map_la
     a.stride = stride;
     a.map = map;
     if (!map_on_device) {
-        FD_HIP_TRY(c, ensure(c->n_map, sizeof(float) * mapn));
+        FD_HIP_TRY(c, ensure(c, c->n_map, sizeof(float) * mapn));
         FD_HIP_TRY(c, hipMemcpyAsync(c->n_map.p, map, sizeof(float) * mapn, hipMemcpyHostToDevice, c->stream));
         a.map = as<float>(c->n_map);
     }
@@ -1042,13 +1194,13 @@ int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int map_la
         a.counts = counts;
         a.out = out;
     } else {
-        FD_HIP_TRY(c, ensure(c->n_xy, sizeof(float) * 2 * slots));
-        FD_HIP_TRY(c, ensure(c->n_out, sizeof(float) * channels * slots));
+        FD_HIP_TRY(c, ensure(c, c->n_xy, sizeof(float) * 2 * slots));
+        FD_HIP_TRY(c, ensure(c, c->n_out, sizeof(float) * channels * slots));
         FD_HIP_TRY(c, hipMemcpyAsync(c->n_xy.p, xy, sizeof(float) * 2 * slots, hipMemcpyHostToDevice, c->stream));
         a.xy = as<float>(c->n_xy);
         a.out = as<float>(c->n_out);
         if (counts) {
-            FD_HIP_TRY(c, ensure(c->n_counts, sizeof(int32_t) * batch));
+            FD_HIP_TRY(c, ensure(c, c->n_counts, sizeof(int32_t) * batch));
             FD_HIP_TRY(c, hipMemcpyAsync(c->n_counts.p, counts, sizeof(int32_t) * batch, hipMemcpyHostToDevice, c->stream));
             a.counts = as<int32_t>(c->n_counts);
         }

@@ -11,9 +11,12 @@
 // (<= 1 kept feature per cell).
 //
 // The workgroup resets its frame's counters and histogram for the next call (no memset launches).
-// Every data-dependent loop is bounded; an inconsistency trips a guard flag in out_counts that the
-// host reports as an error instead of a hang or an out-of-bounds access.
+// Every data-dependent loop is bounded; an inconsistency trips a guard flag in the frame's status word
+// (FD_FRAME_GUARD) that the host reports as an error instead of a hang or an out-of-bounds access.
+// The status word also flags frames whose scan met equal responses (FD_FRAME_TIES); with
+// FD_TIES_REFERENCE the host re-selects those in the reference's std::sort order (k_select_ordered).
 #include "fd_device.h"
+#include "fd_hip.h"
 #include "fd_kernels.h"
 #include "fd_gather.h"
 
@@ -78,16 +81,24 @@ constexpr int kRegGather = 16;  // list responses per thread and round in the le
 // resolved at once from cmask (per candidate: earlier candidates of its batch within distance d,
 // computed beforehand by the whole workgroup).
 // GRID: 0 = no distance test (d <= 0), 1 = occupancy grid in LDS, 2 = grid in global memory.
+// Tie check (pk32 != null: the chunk's 32-bit response keys in scan order): FD_FRAME_TIES is raised
+// when two adjacent candidates of the visited prefix, or the last visited one and the next, have
+// equal responses -- the only case in which the reference's unstable std::sort (:58-60) can change the
+// result. tie_prev / tie_has_prev carry the last key of the previous chunk (wave 0's LDS state).
 template <int GRID>
 __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
                                              const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
-                                             uint32_t prior, int &s_acc, int &s_done) {
+                                             uint32_t prior, int &s_acc, int &s_done, const uint32_t *pk32,
+                                             uint32_t &tie_prev, int &tie_has_prev) {
     const int lane = lane_id();
     const int d = a.dist;
     const bool pk16 = a.rows + 3 * d < 65536 && a.cols + 3 * d < 65536;  // no wrap-around in 16-bit halves
     const uint32_t w2 = 2u * static_cast<uint32_t>(d);
     int acc = s_acc;
     bool done = false;
+    uint32_t t_prev = tie_prev;
+    bool t_has = tie_has_prev != 0;
+    bool tied = false;
     // Software pipeline: a batch's position, cell and conflict mask are loaded during the previous
     // batch's resolution (they are read-only here; only the grid is written).
     auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C) {
@@ -145,7 +156,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         // 64 passes always suffice; the bound only guards against inconsistent input.
         for (int pass = 0; dec_m != ~0ull; ++pass) {
             if (pass >= kWave) {
-                if (lane == 0) atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x20000000u);
+                if (lane == 0) atomicOr(&a.status[f], 0x20000000u);
                 break;
             }
             const bool can = !mine && (C & ~dec_m) == 0;
@@ -166,6 +177,25 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
             acc_m = keep;
             done = true;
         }
+        if (pk32) {
+            // visited lanes: all of the batch, or up to the append that reached `need`; plus the next one
+            const int last = done ? 63 - __builtin_clzll(acc_m) : kWave - 1;
+            const int i = b0 + lane;
+            bool t = false;
+            if (lane <= last && i < cnt) {
+                const uint32_t k = pk32[i];
+                t = i > 0 ? k == pk32[i - 1] : (t_has && k == t_prev);
+            }
+            tied = tied || ballot(t) != 0ull;
+            if (done) {  // the candidate after the stop (wave-uniform)
+                const int nx = b0 + last + 1;
+                // the stop is the chunk's last candidate: its successor is not at hand, so assume a
+                // tie (a reference-order resolution then re-selects the frame, with the same result)
+                if (nx >= cnt || pk32[nx] == pk32[nx - 1]) tied = true;
+            }
+            t_prev = pk32[min(b0 + kWave, cnt) - 1];
+            t_has = true;
+        }
         if ((acc_m >> lane) & 1ull) {
             const int pos = mbcnt64(acc_m, acc);
             if (pos < a.out_stride) {
@@ -184,6 +214,61 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     if (lane == 0) {
         s_acc = acc;
         if (done) s_done = 1;
+        tie_prev = t_prev;
+        tie_has_prev = t_has ? 1 : 0;
+        if (tied) atomicOr(&a.status[f], FD_FRAME_TIES);
+    }
+}
+
+// Conflict masks of a chunk in scan order: bit j of cmask[p] = candidate (p & ~63) + j, earlier in p's
+// batch of 64, lies within Chebyshev distance d. One work item per (candidate, quarter of its batch):
+// 16 entries each, no divergent trip counts; each item writes its 16 bits of the 64-bit mask.
+__device__ __forceinline__ void conflict_masks(const uint32_t *pxy, int c, int d, int rows, int cols, uint64_t *cmask,
+                                               int tid, int nthr) {
+    uint16_t *cm16 = reinterpret_cast<uint16_t *>(cmask);
+    const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
+    const uint32_t w2 = 2u * static_cast<uint32_t>(d);
+    for (int item = tid; item < 4 * c; item += nthr) {
+        const int p = item >> 2, q = item & 3;
+        const int bb = p & ~63, me = p - bb;
+        const uint32_t e = pxy[p];
+        uint32_t bits = 0;
+        if (e != kEmpty && 16 * q < me) {
+            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+            const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb + 16 * q);  // broadcast
+            const int lim = me - 16 * q;  // entries j < lim of this quarter are earlier
+            if (pk16) {
+                // packed (x, y) halves: |ex - x| <= d  <=>  (ex - x + d) mod 2^16 <= 2d
+                // (no wrap-around: rows, cols + 3d < 2^16). Empty entries need no test:
+                // the greedy clears their bits (C &= ballot(ok)).
+                const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+#pragma unroll
+                for (int j4 = 0; j4 < 4; ++j4) {
+                    const uint4 e4 = q4[j4];
+                    const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const u16x2 dt = __builtin_bit_cast(u16x2, ev[t]) - base;
+                        const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
+                        bits |= (m <= w2 ? 1u : 0u) << (j4 * 4 + t);
+                    }
+                }
+                if (lim < 16) bits &= (1u << lim) - 1u;
+            } else {
+#pragma unroll
+                for (int j4 = 0; j4 < 4; ++j4) {
+                    const uint4 e4 = q4[j4];
+                    const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
+                        const bool nb = j4 * 4 + t < lim && ev[t] != kEmpty && abs(x - ex) <= d && abs(y - ey) <= d;
+                        bits |= static_cast<uint32_t>(nb) << (j4 * 4 + t);
+                    }
+                }
+            }
+        }
+        cm16[4 * p + q] = static_cast<uint16_t>(bits);
     }
 }
 
@@ -198,7 +283,10 @@ struct alignas(16) SelectLds {
     // sorted chunk, decoded: (y << 16) | x (kEmpty when a prior masks it) and occupancy-grid cell
     uint32_t pxy[kSelectChunk];
     uint32_t pcell[kSelectChunk];
+    uint32_t pk32[kSelectChunk];  // 32-bit response keys in scan order (tie check)
     uint32_t grid_lds[kGridLdsCells];
+    uint32_t tie_prev;
+    int tie_has_prev;
     uint64_t prefix[kLevels];
     int resume[kLevels];
     uint32_t wtot[16];
@@ -292,9 +380,12 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         s_done = 0;
         s_acc = 0;
         prefix[0] = 0;
-        atomicExch(&a.out_counts[f], 0);  // (atomic: the guard flags below are atomicOr'ed)
+        L.tie_prev = 0;
+        L.tie_has_prev = 0;
+        atomicExch(&a.status[f], 0u);  // (atomic: the flags below are atomicOr'ed)
+        a.cand_n[f] = static_cast<uint32_t>(n);
         if (a.value_flag && (__hip_atomic_load(&a.pre_count[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 31))
-            atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x40000000u);  // candidate outside the key map
+            atomicOr(&a.status[f], FD_FRAME_VALUE_RANGE);  // candidate outside the key map
     }
     if (n == 0) {  // RETURN_TRUE_IF(candidates_.empty()) (:55)
         if (tid == 0) a.out_counts[f] = 0;
@@ -503,7 +594,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             FD_STAMP(24);
             if (L.seg_more[r & 1] == 0) break;
             if (r > kSelectChunk) {  // consistency guard (sorted prefixes hold <= kSelectChunk keys)
-                if (tid == 0) atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x04000000u);
+                if (tid == 0) atomicOr(&a.status[f], 0x04000000u);
                 break;
             }
         }
@@ -529,7 +620,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 seg_gather(lo_b);
             } else {
                 if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
-                    atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x02000000u);
+                    atomicOr(&a.status[f], 0x02000000u);
                 gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, (a.pre_keys || seg_mode) ? nullptr : pre_lds);
             }
             first_ready = true;
@@ -548,7 +639,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     for (int64_t iter = 0;; ++iter) {
         if (s_done) break;
         if (iter > 4 * n + 64) {  // every iteration retires a bin or descends; guards inconsistent input
-            if (tid == 0) atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x10000000u);
+            if (tid == 0) atomicOr(&a.status[f], 0x10000000u);
             break;
         }
         if (hi < 0) {
@@ -567,7 +658,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         const int rem = 64 - lvl_top(level);
         const uint64_t pre = prefix[level];
         if (lo > hi && level + 1 >= kLevels) {  // keys are unique: impossible with consistent input
-            if (tid == 0) atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x08000000u);
+            if (tid == 0) atomicOr(&a.status[f], 0x08000000u);
             break;
         }
         if (lo > hi) {  // bin `hi` alone exceeds a chunk: descend into it
@@ -585,7 +676,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             FD_STAMP(7);
             build(level, klo, khi, suf(level));
             if (tid == 0 && suf(level)[0] != expect)  // consistency guard: descent histogram == parent bin
-                atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x02000000u);
+                atomicOr(&a.status[f], 0x02000000u);
             FD_STAMP(6);  // descent pass
             hi = (1 << lvl_width(level)) - 1;
             continue;
@@ -637,7 +728,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             }
             __syncthreads();
             if (tid == 0 && gcount != cnt)  // consistency guard: gathered == histogram count
-                atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x04000000u);
+                atomicOr(&a.status[f], 0x04000000u);
             FD_STAMP(3);  // gather
             const uint32_t s1 = static_cast<uint32_t>(d + 1);
             auto place = [&](int pos, uint64_t sk) {  // decode position, prior mask, grid cell
@@ -646,12 +737,13 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 if (idx >= static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols)) {  // consistency guard
                     ok = false;
                     idx = 0;
-                    atomicOr(reinterpret_cast<uint32_t *>(&a.out_counts[f]), 0x80000000u);
+                    atomicOr(&a.status[f], 0x80000000u);
                 }
                 const uint32_t y = idx / static_cast<uint32_t>(cols);
                 const uint32_t x = idx - y * static_cast<uint32_t>(cols);
                 if (fmask) ok = (fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u;
                 pxy[pos] = ok ? ((y << 16) | x) : kEmpty;
+                L.pk32[pos] = static_cast<uint32_t>(sk >> 32);
                 if (use_grid) pcell[pos] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
             };
             // Sub-chunks of <= kSubChunk keys from the top bins of the superchunk (already in LDS):
@@ -774,68 +866,25 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     __syncthreads();
                     FD_STAMP(13);  // place
                     }
-                    // conflict masks: earlier candidates of the same 64-batch within distance d. One work
-                    // item per (candidate, quarter of its batch): 16 entries each, no divergent trip
-                    // counts; each item writes its 16 bits of the candidate's 64-bit mask directly.
-                    if (use_grid) {
-                        uint16_t *cm16 = reinterpret_cast<uint16_t *>(buf);
-                        const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
-                        const uint32_t w2 = 2u * static_cast<uint32_t>(d);
-                        for (int item = tid; item < 4 * c; item += nthr) {
-                            const int p = item >> 2, q = item & 3;
-                            const int bb = p & ~63, me = p - bb;
-                            const uint32_t e = pxy[p];
-                            uint32_t bits = 0;
-                            if (e != kEmpty && 16 * q < me) {
-                                const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-                                const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb + 16 * q);  // broadcast
-                                const int lim = me - 16 * q;  // entries j < lim of this quarter are earlier
-                                if (pk16) {
-                                    // packed (x, y) halves: |ex - x| <= d  <=>  (ex - x + d) mod 2^16 <= 2d
-                                    // (no wrap-around: rows, cols + 3d < 2^16). Empty entries need no test:
-                                    // the greedy clears their bits (C &= ballot(ok)).
-                                    const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
-#pragma unroll
-                                    for (int j4 = 0; j4 < 4; ++j4) {
-                                        const uint4 e4 = q4[j4];
-                                        const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-                                        for (int t = 0; t < 4; ++t) {
-                                            const u16x2 dt = __builtin_bit_cast(u16x2, ev[t]) - base;
-                                            const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
-                                            bits |= (m <= w2 ? 1u : 0u) << (j4 * 4 + t);
-                                        }
-                                    }
-                                    if (lim < 16) bits &= (1u << lim) - 1u;
-                                } else
-#pragma unroll
-                                for (int j4 = 0; j4 < 4; ++j4) {
-                                    const uint4 e4 = q4[j4];
-                                    const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-                                    for (int t = 0; t < 4; ++t) {
-                                        const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
-                                        const bool nb = j4 * 4 + t < lim && ev[t] != kEmpty && abs(x - ex) <= d &&
-                                                        abs(y - ey) <= d;
-                                        bits |= static_cast<uint32_t>(nb) << (j4 * 4 + t);
-                                    }
-                                }
-                            }
-                            cm16[4 * p + q] = static_cast<uint16_t>(bits);
-                        }
-                    }
+                    // conflict masks: earlier candidates of the same 64-batch within distance d
+                    if (use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
                 }
                 __syncthreads();
                 FD_STAMP(14);  // conflict masks
-                // greedy scan in order by wave 0 (SelectGoodFeatures :62-72)
+                // greedy scan in order by wave 0 (SelectGoodFeatures :62-72); ties checked unless the
+                // order of equal responses is defined (SuperPoint's multimap)
                 if (tid < kWave) {
                     const int c = static_cast<int>(sc);
+                    const uint32_t *tk = a.tie_idx_desc ? nullptr : L.pk32;
                     if (!use_grid)
-                        greedy_chunk<0>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done);
+                        greedy_chunk<0>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                                        L.tie_has_prev);
                     else if (grid_in_lds)
-                        greedy_chunk<1>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done);
+                        greedy_chunk<1>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                                        L.tie_has_prev);
                     else
-                        greedy_chunk<2>(a, f, c, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done);
+                        greedy_chunk<2>(a, f, c, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                                        L.tie_has_prev);
                 }
                 __syncthreads();
                 FD_STAMP(5);  // greedy
@@ -846,10 +895,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         }
         hi = lo - 1;
     }
-    if (tid == 0) {  // keep consistency-guard flags (bits 30/31) for the host to report
-        const uint32_t flags = static_cast<uint32_t>(a.out_counts[f]) & 0xFE000000u;
-        a.out_counts[f] = static_cast<int32_t>(static_cast<uint32_t>(s_acc) | flags);
-    }
+    if (tid == 0) a.out_counts[f] = s_acc;  // (flags, if any, are in a.status[f])
     FD_STAMP(7);
     if (a.stamps && tid == 0)
         for (int i = 0; i < 32; ++i) a.stamps[static_cast<int64_t>(f) * 32 + i] = L.st[i];
@@ -894,7 +940,92 @@ __global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
     finish_frame(a, f);
 }
 
+// Greedy selection in a given order (FD_TIES_REFERENCE): the frame's candidates as raster indices in
+// the order the reference's std::sort leaves them (computed on the host for frames k_select flagged),
+// visited chunk by chunk with the same greedy as k_select (SelectGoodFeatures :62-72): decode, prior
+// mask, grid cell; conflict masks; one wave scans in batches of 64. Overwrites the frame's features.
+struct alignas(16) OrderedLds {
+    uint32_t pxy[kSelectChunk];
+    uint32_t pcell[kSelectChunk];
+    uint64_t cmask[kSelectChunk];
+    uint32_t grid_lds[kGridLdsCells];
+    int s_done, s_acc;
+    uint32_t tie_prev;
+    int tie_has_prev;
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs o) {
+    __shared__ OrderedLds L;
+    const int j = blockIdx.x, tid = threadIdx.x;
+    const int f = o.frame[j];
+    const uint32_t *ord = o.order + o.offset[j];
+    const int64_t n = o.count[j];
+    const int rows = a.rows, cols = a.cols, d = a.dist;
+    const bool use_grid = d >= 1;
+    const int gw2 = a.grid_w + 2;
+    const int cells = gw2 * (a.grid_h + 2);
+    const bool grid_in_lds = cells <= kGridLdsCells;
+    uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
+    uint32_t *const grid = grid_in_lds ? L.grid_lds : grid_g;
+    const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
+    const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
+    const uint32_t npx = static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols);
+    const uint32_t s1 = static_cast<uint32_t>(d + 1);
+    if (use_grid)
+        for (int i = tid; i < cells; i += NT) grid[i] = kEmpty;
+    if (tid == 0) {
+        L.s_done = 0;
+        L.s_acc = 0;
+        L.tie_prev = 0;
+        L.tie_has_prev = 0;
+    }
+    __syncthreads();
+    for (int64_t base = 0; base < n; base += kSelectChunk) {
+        if (L.s_done) break;
+        const int c = static_cast<int>(min(static_cast<int64_t>(kSelectChunk), n - base));
+        for (int i = tid; i < c; i += NT) {
+            uint32_t idx = ord[base + i];
+            bool ok = true;
+            if (idx >= npx) {  // consistency guard
+                ok = false;
+                idx = 0;
+                atomicOr(&a.status[f], 0x80000000u);
+            }
+            const uint32_t y = idx / static_cast<uint32_t>(cols), x = idx - y * static_cast<uint32_t>(cols);
+            if (fmask) ok = ok && ((fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u);
+            L.pxy[i] = ok ? ((y << 16) | x) : kEmpty;
+            if (use_grid) L.pcell[i] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
+        }
+        __syncthreads();
+        if (use_grid) conflict_masks(L.pxy, c, d, rows, cols, L.cmask, tid, NT);
+        __syncthreads();
+        if (tid < kWave) {
+            if (!use_grid)
+                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr,
+                                L.tie_prev, L.tie_has_prev);
+            else if (grid_in_lds)
+                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr,
+                                L.tie_prev, L.tie_has_prev);
+            else
+                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr,
+                                L.tie_prev, L.tie_has_prev);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        a.out_counts[f] = L.s_acc;
+        atomicOr(&a.status[f], FD_FRAME_RESOLVED);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s) {
+    if (n_frames <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_select_ordered<256>, dim3(static_cast<unsigned>(n_frames)), dim3(256), 0, s, a, o);
+    return hipGetLastError();
+}
 
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
     if (a.pre_keys) {

@@ -14,7 +14,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import FD_SAMPLE_BILINEAR, FD_SAMPLE_TRUNCATE, fd_brief_opts
-from .points import Context, _bind_stream, _frames, _is_torch_device_tensor, default_context
+from .points import Context, _bind_stream, _frames, _is_torch_device_tensor, _resolve_ctx
 
 SAMPLERS = {"bilinear": FD_SAMPLE_BILINEAR, "truncate": FD_SAMPLE_TRUNCATE}
 
@@ -33,7 +33,7 @@ def brief_compute(frames, uv, counts=None, length: int = 256, half_patch_size: i
     """
     smp = SAMPLERS[sampler] if isinstance(sampler, str) else int(sampler)
     fptr, f_on_dev, b, r, c, keep_f = _frames(frames)
-    ctx = ctx or default_context()
+    ctx = _resolve_ctx(ctx, frames, uv)
     nw = (int(length) + 31) // 32
     opts = fd_brief_opts(int(length), int(half_patch_size), smp)
     if _is_torch_device_tensor(uv):

@@ -7,6 +7,7 @@ runs the HIP kernels; there is no CPU path.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from dataclasses import dataclass
 
@@ -16,6 +17,9 @@ from . import _lib
 from ._lib import FD_FAST, FD_HARRIS, FD_SHI_TOMASI, fd_point_opts
 
 KINDS = {"harris": FD_HARRIS, "shi_tomasi": FD_SHI_TOMASI, "fast": FD_FAST}
+# order of equal responses in the selection (include/fd_hip.h fd_ctx_set_tie_order)
+TIES = {"raster": 0, "reference": 1}
+FRAME_TIES, FRAME_RESOLVED, FRAME_VALUE_RANGE, FRAME_GUARD = 0x1, 0x2, 0x40000000, 0xBE000000
 
 _ctx_lock = threading.Lock()
 _contexts: dict[int, "Context"] = {}
@@ -57,8 +61,28 @@ class Context:
     def reserve(self, kind: int, batch: int, rows: int, cols: int, max_prior_total: int = 0):
         _lib.check(self.ptr, _lib.load().fd_ctx_reserve(self.ptr, kind, batch, rows, cols, max_prior_total))
 
+    def set_tie_order(self, ties: str):
+        """'raster' (equal responses by raster index) or 'reference' (the reference's std::sort order)."""
+        _lib.check(self.ptr, _lib.load().fd_ctx_set_tie_order(self.ptr, TIES[ties]))
 
-def default_context(device: int = 0) -> Context:
+    def frame_status(self, batch: int, out=None):
+        """Per-frame FD_FRAME_* words of the last selection call: numpy uint32 [batch] (synchronous), or
+        copied asynchronously into `out` (a device int32 tensor [batch]) on the context stream."""
+        if out is not None:
+            _lib.check(self.ptr, _lib.load().fd_ctx_frame_status(self.ptr, ctypes.c_void_p(out.data_ptr()), batch, 1))
+            return out
+        st = np.zeros((batch,), np.uint32)
+        _lib.check(self.ptr, _lib.load().fd_ctx_frame_status(self.ptr, ctypes.c_void_p(st.ctypes.data), batch, 0))
+        return st
+
+
+def _default_device() -> int:
+    return int(os.environ.get("FD_DEVICE", "0"))
+
+
+def default_context(device: int | None = None) -> Context:
+    """The shared context of a GPU (default: $FD_DEVICE or 0), created on first use."""
+    device = _default_device() if device is None else int(device)
     with _ctx_lock:
         c = _contexts.get(device)
         if c is None:
@@ -97,11 +121,32 @@ def _frames(x):
     return ptr, on_dev, int(b), int(r), int(c), x
 
 
+def _resolve_ctx(ctx: Context | None, *inputs) -> Context:
+    """The context of a call: `ctx`, or the default context of the GPU the torch inputs live on. A
+    context on another device than its inputs is an error (its workspace and stream are per device)."""
+    dev = None
+    for x in inputs:
+        if _is_torch_device_tensor(x):
+            import torch
+
+            d = x.device.index if x.device.index is not None else torch.cuda.current_device()
+            if dev is not None and d != dev:
+                raise ValueError(f"inputs on different devices ({dev} and {d})")
+            dev = d
+    if ctx is None:
+        return default_context(dev)
+    if dev is not None and ctx.device != dev:
+        raise ValueError(f"context is on device {ctx.device} but the inputs are on device {dev}")
+    return ctx
+
+
 def _bind_stream(ctx: Context, on_device: bool):
+    """Device inputs run on torch's current stream of the context's device; host inputs on the
+    context's own stream. (The library orders a stream switch after the previous stream's work.)"""
     if on_device:
         import torch
 
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        ctx.set_stream(torch.cuda.current_stream(ctx.device).cuda_stream)
     else:
         ctx.set_stream(None)
 
@@ -123,36 +168,59 @@ def _priors(prior, batch):
 class DetectResult:
     xy: object  # [batch, stride, 2] float32 (numpy or torch)
     counts: object  # [batch] int32
+    status: object = None  # [batch] FD_FRAME_* words (numpy uint32, or a device int32 tensor), if fetched
 
     def features(self, b: int) -> np.ndarray:
         xy = self.xy if isinstance(self.xy, np.ndarray) else self.xy.cpu().numpy()
         n = int(self.counts[b]) if isinstance(self.counts, np.ndarray) else int(self.counts[b].item())
         return xy[b, :n].copy()
 
+    def frame_flags(self) -> np.ndarray:
+        """Per-frame FD_FRAME_* words as numpy uint32 (synchronises a device result)."""
+        if self.status is None:
+            raise ValueError("status was not fetched (out= without a status tensor)")
+        st = self.status if isinstance(self.status, np.ndarray) else self.status.cpu().numpy()
+        return st.astype(np.uint32)
+
+    def check(self) -> "DetectResult":
+        """Raise if a frame tripped an internal guard (device results carry no flags in their counts)."""
+        bad = np.nonzero(self.frame_flags() & np.uint32(FRAME_GUARD | FRAME_VALUE_RANGE))[0]
+        if len(bad):
+            raise _lib.FdError(_lib.FD_ERR_HIP, f"selection flags 0x{int(self.frame_flags()[bad[0]]):x} on frame {bad[0]}")
+        return self
+
 
 def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_valid_response: float = 0.1,
-                  prior=None, ctx: Context | None = None, out=None) -> DetectResult:
+                  prior=None, ctx: Context | None = None, out=None, ties: str = "reference") -> DetectResult:
     """FeaturePointDetector::DetectGoodFeatures on a batch (include/fd_hip.h fd_points_detect).
 
-    Returns the NEW features per frame (x, y), in selection order. With torch device frames the
-    outputs are device tensors (asynchronous on the current stream); `out` may pass preallocated
-    (xy, counts) tensors so that repeated calls allocate nothing (graph capture).
+    Returns the NEW features per frame (x, y), in selection order, and the per-frame status words.
+    ties="reference" (default): frames whose greedy scan meets equal responses are re-selected in the
+    reference's std::sort order, so every frame equals the reference's DetectGoodFeatures; the call
+    then synchronises once. ties="raster": equal responses by raster index (fully asynchronous,
+    graph-capturable; identical wherever no tie reaches the scan, FD_FRAME_TIES marks the others).
+    With torch device frames the outputs are device tensors (on the current stream); `out` may pass
+    preallocated (xy, counts) or (xy, counts, status) tensors so that repeated calls allocate nothing.
     """
     kind = KINDS[kind] if isinstance(kind, str) else int(kind)
     ptr, on_dev, b, r, c, keep = _frames(frames)
-    ctx = ctx or default_context()
+    ctx = _resolve_ctx(ctx, frames)
     _bind_stream(ctx, bool(on_dev))
+    ctx.set_tie_order(ties)
     opts = fd_point_opts(int(min_feature_distance), float(min_valid_response))
     pxy, pcnt, _keep2 = _priors(prior, b)
     stride = max(int(need), 1) + 1
+    status = None
     if on_dev:
         import torch
 
         if out is None:
             xy = torch.empty((b, stride, 2), dtype=torch.float32, device=frames.device)
             cnt = torch.empty((b,), dtype=torch.int32, device=frames.device)
+            status = torch.empty((b,), dtype=torch.int32, device=frames.device)
         else:
-            xy, cnt = out
+            xy, cnt = out[0], out[1]
+            status = out[2] if len(out) > 2 else None
             stride = xy.shape[1]
         xy_ptr, cnt_ptr = xy.data_ptr(), cnt.data_ptr()
     else:
@@ -166,7 +234,12 @@ def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_v
         int(need), ctypes.c_void_p(xy_ptr), stride, ctypes.c_void_p(cnt_ptr), on_dev)
     _lib.check(ctx.ptr, rc)
     del keep
-    return DetectResult(xy, cnt)
+    if on_dev:
+        if status is not None:
+            ctx.frame_status(b, out=status)
+    else:
+        status = ctx.frame_status(b)
+    return DetectResult(xy, cnt, status)
 
 
 def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx: Context | None = None,
@@ -184,7 +257,7 @@ def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx:
     ptr, on_dev, b, r, c, keep = _frames(frames)
     if not on_dev:
         raise TypeError("point_response takes device frames")
-    ctx = ctx or default_context()
+    ctx = _resolve_ctx(ctx, frames)
     _bind_stream(ctx, True)
     cap = r * c if kind == FD_FAST else r * c // 2 + 64
     if out is None:
@@ -218,7 +291,7 @@ def point_candidates(kind, frames, min_feature_distance: int = 15, min_valid_res
     ptr, on_dev, b, r, c, keep = _frames(frames)
     if on_dev:
         raise TypeError("point_candidates takes host frames")
-    ctx = ctx or default_context()
+    ctx = _resolve_ctx(ctx, frames)
     _bind_stream(ctx, False)
     opts = fd_point_opts(int(min_feature_distance), float(min_valid_response))
     pxy, pcnt, _keep2 = _priors(prior, b)
@@ -251,7 +324,7 @@ def lsd_map(frames, min_norm: float = 20.0, cap: int | None = None, ctx: Context
     `out` may pass them preallocated (graph capture); any of norm/angle/valid may be None to skip.
     """
     ptr, on_dev, b, r, c, keep = _frames(frames)
-    ctx = ctx or default_context()
+    ctx = _resolve_ctx(ctx, frames)
     mr, mc = r - 1, c - 1
     cap = mr * mc if cap is None else cap
     if on_dev:

@@ -24,7 +24,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import fd_nn_opts
-from .points import Context, _bind_stream, _is_torch_device_tensor, default_context
+from .points import Context, _bind_stream, _is_torch_device_tensor, _resolve_ctx
 
 
 @dataclass
@@ -55,7 +55,7 @@ def nn_select(heat, options: Options | None = None, prior=None, out=None, ctx: C
     prior: None or a list (per frame) of (n_i, 2) float arrays of (x, y), host memory.
     """
     o = options or Options()
-    ctx = ctx or default_context()
+    ctx = _resolve_ctx(ctx, heat)
     opts = _opts(o, max_response)
     on_dev = _is_torch_device_tensor(heat)
     if on_dev:
@@ -104,7 +104,7 @@ def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = No
     """fd_nn_descriptors: desc_map [B, C, h, w] float32, xy [B, S, 2] -> descriptors [B, S, C].
 
     Host arrays give numpy outputs; torch device tensors give device outputs (current stream)."""
-    ctx = ctx or default_context()
+    ctx = _resolve_ctx(ctx, desc_map, xy)
     if _is_torch_device_tensor(desc_map):
         import torch
 

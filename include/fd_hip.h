@@ -59,8 +59,38 @@ int fd_ctx_use_own_stream(fd_ctx *ctx);
 void *fd_ctx_get_stream(const fd_ctx *ctx);
 int fd_ctx_synchronize(fd_ctx *ctx);
 /* Pre-size device workspace for a (kind, batch, rows, cols) shape so that later calls of that shape
- * allocate nothing (required before hipGraph capture of fd_points_detect). */
+ * allocate nothing (required before hipGraph capture of fd_points_detect). Not covered: the global
+ * occupancy grid of very small min_feature_distance (cells > 16384 per frame, e.g. 640x480 with d <= 4)
+ * -- run one call of the shape before capturing. A call that would grow the workspace while its
+ * stream is being captured fails (FD_ERR_HIP, "stream capture") instead of allocating. */
 int fd_ctx_reserve(fd_ctx *ctx, int kind, int batch, int rows, int cols, int64_t max_prior_total);
+/*
+ * Order of equal responses in the selection (SelectGoodFeatures, feature_point_detector.cpp:58-60 sorts
+ * with an unstable std::sort, so equal responses have no defined order):
+ *   FD_TIES_RASTER     (default) response descending, equal responses by raster index ascending: a
+ *                      total order, fully asynchronous and graph-capturable.
+ *   FD_TIES_REFERENCE  the reference's own permutation: every frame whose greedy scan meets two equal
+ *                      responses (FD_FRAME_TIES) is re-selected in the order libstdc++'s std::sort
+ *                      leaves the raster-ordered candidates in (the sort runs on the host, the greedy
+ *                      selection again on the GPU). Frames without such a tie are identical in both
+ *                      modes. Each selection call then synchronises its stream once to read the flags.
+ * SuperPoint's fd_nn_select has a defined order (std::multimap) and ignores this setting.
+ */
+enum fd_tie_order { FD_TIES_RASTER = 0, FD_TIES_REFERENCE = 1 };
+int fd_ctx_set_tie_order(fd_ctx *ctx, int order);
+
+/*
+ * Per-frame status words of the last selection call on this context (fd_points_detect, fd_nn_select):
+ * FD_FRAME_* bits. Copies `batch` words to dst on the context stream (dst: device or host memory);
+ * with async = 0 the call waits for the copy. Device-output calls return plain counts and leave their
+ * flags here, so a caller can check them without a host round trip per call.
+ */
+#define FD_FRAME_TIES 0x00000001u       /* equal responses met in the greedy scan (order defined by the mode) */
+#define FD_FRAME_RESOLVED 0x00000002u   /* re-selected in the reference's std::sort order (FD_TIES_REFERENCE) */
+#define FD_FRAME_VALUE_RANGE 0x40000000u /* fd_nn_select: a heatmap value above fd_nn_opts::max_response */
+#define FD_FRAME_GUARD 0xBE000000u      /* internal consistency guard tripped (host-output calls fail FD_ERR_HIP) */
+int fd_ctx_frame_status(fd_ctx *ctx, uint32_t *dst, int batch, int async);
+
 /* Copy `bytes` of host memory into the context's frame staging buffer; *device_out receives its device
  * address, valid until the next call that stages frames on this context. Lets a caller run several
  * entry points on one upload (frames_on_device = 1). Synchronous. */
@@ -79,9 +109,11 @@ int fd_ctx_stage(fd_ctx *ctx, const void *host, int64_t bytes, const uint8_t **d
  *   prior_counts  batch entries (number of prior features of each frame), or NULL
  *   need          needed_feature_num (counts the prior features, checked after each append, :67-69)
  *   out_xy        batch * out_stride (x, y) float pairs: the NEW features of each frame, in order
- *   out_counts    batch int32: number of new features per frame
- * Candidate order: response descending, ties by raster index ascending (the reference's std::sort
- * is unstable; see DESIGN.md "Tie order"). out_stride must be >= min(need, candidates) + 1.
+ *   out_counts    batch int32: number of new features per frame (plain counts; per-frame flags are
+ *                 in fd_ctx_frame_status)
+ * Candidate order: response descending; equal responses as fd_ctx_set_tie_order says (default raster
+ * index ascending; FD_TIES_REFERENCE = the reference's std::sort permutation, DESIGN.md "Tie order").
+ * out_stride must be >= min(need, candidates) + 1.
  */
 int fd_points_detect(fd_ctx *ctx, int kind, const uint8_t *frames, int frames_on_device, int batch, int rows,
                      int cols, const fd_point_opts *opts, const float *prior_xy, const int32_t *prior_counts,

@@ -80,3 +80,20 @@ def oracle():
 
     O.lib()
     return O
+
+
+def make_tie_frame(oracle, rows=480, cols=640, seed=77, copies=(6, 8)):
+    """A frame whose greedy scan meets equal responses: identical 15x15 corner stamps (constant
+    surround, so every copy has bit-identical Harris / Shi-Tomasi responses) on a low-contrast noise
+    background. The reference's unstable std::sort orders the equal responses differently from raster
+    order, so the two tie orders select different feature lists (checked against the oracle)."""
+    img = oracle.make_frame("noise", seed, rows, cols) // 4
+    patch = np.full((15, 15), 100, np.uint8)
+    patch[4:8, 4:8] = 250
+    patch[7:11, 7:11] = 10
+    ys = np.linspace(10, rows - 30, copies[0]).astype(int)
+    xs = np.linspace(10, cols - 30, copies[1]).astype(int)
+    for y in ys:
+        for x in xs:
+            img[y:y + 15, x:x + 15] = patch
+    return img

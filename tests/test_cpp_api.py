@@ -78,6 +78,22 @@ def test_point_demo_matches_oracle(tmp_path, image_png, oracle, ref_counts):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["harris", "shi_tomasi"])
+def test_point_demo_tie_frame_reference_order(tmp_path, oracle, name):
+    """Equal responses in the greedy scan: the drop-in class runs FD_TIES_REFERENCE, so its features
+    are the reference's std::sort order (oracle sort_mode 0), which differs from raster order here."""
+    from conftest import make_tie_frame
+
+    img = make_tie_frame(oracle)
+    _build()
+    r = {x["test"]: x for x in _run("fd_demo_points", img, tmp_path)}[name]
+    feats, _ = oracle.detect(KIND[name], img, 20, THR[name], 200, None, sort_mode=0)
+    stable, _ = oracle.detect(KIND[name], img, 20, THR[name], 200, None, sort_mode=1)
+    got = np.array(r["features"], np.float32).reshape(-1, 2)
+    assert np.array_equal(got, feats) and not np.array_equal(got, stable)
+
+
+@pytest.mark.gpu
 def test_line_demo_reference_counts(tmp_path, image_png, oracle, ref_counts):
     _build()
     (r,) = _run("fd_demo_lines", image_png, tmp_path)

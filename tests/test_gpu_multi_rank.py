@@ -52,7 +52,7 @@ def test_sharded_ranks_match_oracle(oracle, world):
     import torch.multiprocessing as mp
 
     frames = np.stack([oracle.make_frame("noise" if i % 2 else "checker", 70 + i, 120, 160) for i in range(7)])
-    expected = [oracle.detect(0, f, 20, 30.0, 50, sort_mode=1)[0].tolist() for f in frames]
+    expected = [oracle.detect(0, f, 20, 30.0, 50, sort_mode=0)[0].tolist() for f in frames]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -100,7 +100,7 @@ def test_two_contexts_on_two_streams_match_oracle(oracle):
             outs.append((xy, cnt))
     torch.cuda.synchronize()
     for f, (xy, cnt) in zip(frames, outs):
-        exp = oracle.detect(0, f, 20, 30.0, 50, sort_mode=1)[0]
+        exp = oracle.detect(0, f, 20, 30.0, 50, sort_mode=0)[0]
         np.testing.assert_array_equal(xy[0, : int(cnt[0])].cpu().numpy(), exp)
     for c in ctxs:
         c.close()

@@ -1,9 +1,9 @@
 """GPU parity of the point-detection hot path (HIP kernels via the C ABI) against the CPU oracle.
 
 Bar: bit-exact. Candidates (response bits, x, y, raster order) and the Harris/Shi-Tomasi response
-maps must equal the oracle's; selected features must equal the oracle's with the deterministic
-(response desc, raster asc) order, and equal the reference std::sort order whenever no tie reaches
-the greedy scan (checked and reported per case).
+maps must equal the oracle's; selected features must equal the oracle's in both tie orders: the
+default "reference" order (the reference's std::sort permutation) against oracle sort_mode 0, and
+"raster" (response desc, raster asc) against the oracle's stable order (sort_mode 1).
 """
 import numpy as np
 import pytest
@@ -47,14 +47,19 @@ def assert_same_candidates(got, exp):
 
 
 def check_detect(fd, oracle, name, img, dist, thr, need, prior=None):
-    res = fd.detect_points(name, img, need, dist, thr, prior=None if prior is None else [prior])
+    pr = None if prior is None else [prior]
+    res = fd.detect_points(name, img, need, dist, thr, prior=pr)  # ties="reference"
     got = res.features(0)
-    exp_stable, cands = oracle.detect(KIND[name], img, dist, thr, need, prior, sort_mode=1)
-    assert np.array_equal(got, exp_stable)
     exp_ref, cands_ref = oracle.detect(KIND[name], img, dist, thr, need, prior, sort_mode=0)
+    assert np.array_equal(got, exp_ref)
+    raster = fd.detect_points(name, img, need, dist, thr, prior=pr, ties="raster")
+    exp_stable, _ = oracle.detect(KIND[name], img, dist, thr, need, prior, sort_mode=1)
+    assert np.array_equal(raster.features(0), exp_stable)
     if not np.array_equal(exp_ref, exp_stable):
-        # Only possible when equal responses meet inside the scanned prefix (unstable std::sort).
+        # Only possible when equal responses meet inside the scanned prefix (unstable std::sort),
+        # and then the GPU must have flagged the frame and re-selected it in the reference order.
         assert oracle.prefix_has_ties(cands_ref[0], len(cands_ref[0]))
+        assert res.frame_flags()[0] & fd.points.FRAME_RESOLVED
     return got
 
 
@@ -116,7 +121,7 @@ def test_batch_equals_single(fd, oracle):
         for b in range(len(frames)):
             single = fd.detect_points(name, frames[b], 100, 10, THR[name]).features(0)
             assert np.array_equal(res.features(b), single)
-            exp, _ = oracle.detect(KIND[name], frames[b], 10, THR[name], 100, sort_mode=1)
+            exp, _ = oracle.detect(KIND[name], frames[b], 10, THR[name], 100, sort_mode=0)
             assert np.array_equal(single, exp)
 
 
@@ -179,7 +184,7 @@ def test_1080p_against_oracle_and_golden_counts(fd, oracle, ref_counts, name):
     frames = np.stack([oracle.make_frame(p, 1234, 1080, 1920) for p in ("noise", "checker")])
     res = fd.detect_points(name, frames, 200, 20, THR[name])
     for b, p in enumerate(("noise", "checker")):
-        exp, cands = oracle.detect(KIND[name], frames[b], 20, THR[name], 200, sort_mode=1)
+        exp, cands = oracle.detect(KIND[name], frames[b], 20, THR[name], 200, sort_mode=0)
         rec = [r for r in ref_counts["synthetic_candidates"]
                if r["rows"] == 1080 and r["pattern"] == p][0]
         assert len(cands[0]) == rec[name]
@@ -205,7 +210,7 @@ def test_large_batch_properties(fd, oracle):
         np.fill_diagonal(d, 1e9)
         assert d.min() > 20
     for b in (0, 1, 37):
-        exp, _ = oracle.detect(1, host[b], 20, 40.0, 200, sort_mode=1)
+        exp, _ = oracle.detect(1, host[b], 20, 40.0, 200, sort_mode=0)
         assert np.array_equal(xy[b, :counts[b]], exp)
 
 

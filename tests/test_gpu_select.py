@@ -2,7 +2,11 @@
 oracle's restatement across the regimes of its radix descent: no distance test, tiny and huge
 cells (LDS grid and global grid), needs that finish inside the first chunk and needs that are never
 reached (every candidate visited: many chunks and descents), batches of mixed frames, and repeated
-calls of different shapes and kinds (the kernel resets its own counters and histograms)."""
+calls of different shapes and kinds (the kernel resets its own counters and histograms).
+
+Every case runs in both tie orders: "raster" (the kernel's total order, against the oracle's stable
+order) and "reference" (frames whose scan meets equal responses re-selected in std::sort's order,
+against the oracle's std::sort order)."""
 import numpy as np
 import pytest
 
@@ -20,9 +24,12 @@ def fd():
     return fd
 
 
-def _detect(fd, name, frames, need, dist):
-    res = fd.detect_points(name, frames, need, dist, THR[name])
-    return [res.features(i).copy() for i in range(frames.shape[0])]
+def _check(fd, oracle, name, frames, need, dist):
+    for ties, mode in (("raster", 1), ("reference", 0)):
+        res = fd.detect_points(name, frames, need, dist, THR[name], ties=ties)
+        for i in range(frames.shape[0]):
+            exp = oracle.detect(KIND[name], frames[i], dist, THR[name], need, sort_mode=mode)[0]
+            np.testing.assert_array_equal(res.features(i), exp, err_msg=f"{name} frame {i} ties={ties}")
 
 
 @pytest.mark.parametrize("dist,need", [(0, 50), (1, 500), (3, 200), (20, 200), (60, 100), (254, 10), (255, 10),
@@ -30,19 +37,14 @@ def _detect(fd, name, frames, need, dist):
 @pytest.mark.parametrize("name", ["harris", "shi_tomasi", "fast"])
 def test_select_regimes_against_oracle(fd, oracle, name, dist, need):
     frames = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 300 + i, 240, 320) for i in range(3)])
-    got = _detect(fd, name, frames, need, dist)
-    for i, g in enumerate(got):
-        exp = oracle.detect(KIND[name], frames[i], dist, THR[name], need, sort_mode=1)[0]
-        np.testing.assert_array_equal(g, exp)
+    _check(fd, oracle, name, frames, need, dist)
 
 
 @pytest.mark.parametrize("name", ["harris", "fast"])
 def test_batch1_720p(fd, oracle, name):
     # FAST 720p noise consumes ~5k candidates: many sub-chunks of the first chunks
     img = oracle.make_frame("noise", 77, 720, 1280)
-    got = _detect(fd, name, img[None], 200, 20)[0]
-    exp = oracle.detect(KIND[name], img, 20, THR[name], 200, sort_mode=1)[0]
-    np.testing.assert_array_equal(got, exp)
+    _check(fd, oracle, name, img[None], 200, 20)
 
 
 def test_repeated_calls_reset_state(fd, oracle):
@@ -50,16 +52,11 @@ def test_repeated_calls_reset_state(fd, oracle):
     b = oracle.make_frame("checker", 6, 333, 251)
     for _ in range(3):
         for name, img in (("harris", a), ("fast", b), ("shi_tomasi", a), ("harris", b)):
-            got = _detect(fd, name, img[None], 150, 7)[0]
-            exp = oracle.detect(KIND[name], img, 7, THR[name], 150, sort_mode=1)[0]
-            np.testing.assert_array_equal(got, exp)
+            _check(fd, oracle, name, img[None], 150, 7)
     # batch sizes changing between calls re-lay the control block; it must still read as zero
     for bsz in (4, 1, 7, 2):
         frames = np.stack([oracle.make_frame("noise", 40 + i, 120, 160) for i in range(bsz)])
-        got = _detect(fd, "harris", frames, 60, 5)
-        for i in range(bsz):
-            exp = oracle.detect(0, frames[i], 5, 30.0, 60, sort_mode=1)[0]
-            np.testing.assert_array_equal(got[i], exp)
+        _check(fd, oracle, "harris", frames, 60, 5)
 
 
 @pytest.mark.parametrize("groups", ["1", "3", "64"])
@@ -68,10 +65,7 @@ def test_gather_kernel_groups(fd, oracle, groups, monkeypatch):
     monkeypatch.setenv("FD_GATHER_GROUPS", groups)
     frames = np.stack([oracle.make_frame("noise", 90 + i, 240, 320) for i in range(2)])
     for name in ("harris", "fast"):
-        got = _detect(fd, name, frames, 200, 20)
-        for i in range(2):
-            exp = oracle.detect(KIND[name], frames[i], 20, THR[name], 200, sort_mode=1)[0]
-            np.testing.assert_array_equal(got[i], exp)
+        _check(fd, oracle, name, frames, 200, 20)
 
 
 @pytest.mark.parametrize("seg", ["0", "1"])
@@ -83,7 +77,4 @@ def test_sorted_segment_lists_toggle(fd, oracle, seg, monkeypatch):
     for shape, bsz in (((480, 640), 1), ((240, 320), 3), ((61, 77), 2), ((700, 1000), 1)):
         frames = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 700 + i, *shape) for i in range(bsz)])
         for name, dist, need in (("harris", 20, 200), ("shi_tomasi", 3, 800), ("fast", 20, 200), ("harris", 0, 50)):
-            got = _detect(fd, name, frames, need, dist)
-            for i in range(bsz):
-                exp = oracle.detect(KIND[name], frames[i], dist, THR[name], need, sort_mode=1)[0]
-                np.testing.assert_array_equal(got[i], exp)
+            _check(fd, oracle, name, frames, need, dist)
