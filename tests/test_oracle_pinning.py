@@ -1,8 +1,10 @@
-"""CPU: the oracle restatement reproduces every output of the reference recorded in the survey.
+"""CPU: the oracle restatement reproduces every output count recorded by the survey's probe.
 
-The reference ships no golden vectors; tests/golden/reference_counts.json holds the reference's own
-outputs recorded by the survey. Matching all of them exactly, for
-all four detectors and three frame sizes, pins the restatement (and the synthetic-frame generator).
+The reference ships no golden vectors; tests/golden/reference_counts.json holds the counts the
+survey's probe recorded. That probe compiled the reference against
+stand-in Slam_Utility headers, so under this project's rules these counts do NOT pin the oracle
+("parity unpinned"): they are a consistency check of the restatement and of the
+synthetic-frame generator, nothing more.
 """
 import numpy as np
 import pytest
@@ -41,9 +43,7 @@ def test_synthetic_candidate_counts(oracle, ref_counts, size, pattern):
 
 
 def test_synthetic_lsd_valid_counts(oracle, ref_counts):
-    for rec in ref_counts["synthetic_lsd_valid"]:
-        if rec["rows"] > 480:
-            continue  # 1080p rows are checked by the slow marker run below
+    for rec in ref_counts["synthetic_lsd_valid"]:  # all sizes incl. 1080p (~0.15 s in total)
         img = oracle.make_frame(rec["pattern"], 1234, rec["rows"], rec["cols"], rec["period"])
         assert len(oracle.lsd_map(img)[3]) == rec["valid"]
 
