@@ -118,18 +118,28 @@ def timed_graph(torch, fn, steps, warmup, use_graph, per_graph, barrier=None):
     for i in range(max(warmup, 1)):  # eager warmup also sizes the library workspace
         fn(i)
     torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for i in range(per_graph):
-            fn(i)
-    g.replay()
-    reps = max(1, (steps + per_graph - 1) // per_graph)
+    # Exactly `steps` steps: reps replays of a graph of per_graph steps + one graph of the remainder.
+    per_graph = max(1, min(per_graph, steps))
+    reps, rem = divmod(steps, per_graph)
+    graphs = []
+    for n in (per_graph, rem):
+        if n == 0:
+            graphs.append(None)
+            continue
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for i in range(n):
+                fn(i)
+        g.replay()  # untimed: first replay uploads the graph
+        graphs.append(g)
     fence()
     t0 = time.perf_counter()
     for _ in range(reps):
-        g.replay()
+        graphs[0].replay()
+    if graphs[1] is not None:
+        graphs[1].replay()
     fence()
-    return time.perf_counter() - t0, reps * per_graph
+    return time.perf_counter() - t0, reps * per_graph + rem
 
 
 def kernel_time_ms(torch, fd, frames_pool, kind, thr, reps=50):
@@ -463,18 +473,122 @@ def run_superpoint(torch, fd, dev, seed, batch=64, rows=480, cols=640, steps=10)
     }
 
 
-def main():
-    args = parse()
-    import torch
+def cpu_workers():
+    """Threads for the CPU pool leg: the CPUs this process may run on, capped by the lease's thread
+    budget (the GPU box exports OMP_NUM_THREADS=16: its CPU share, although nproc shows the whole
+    host). Returns (workers, visible logical CPUs, cap source)."""
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    lease = os.environ.get("OMP_NUM_THREADS")
+    if lease and lease.isdigit() and int(lease) > 0:
+        return min(visible, int(lease)), visible, f"OMP_NUM_THREADS={lease} (lease CPU share)"
+    return visible, visible, "sched_getaffinity"
+
+
+def cpu_leg(work, px_per_item, seconds, unit="Mpix/s", label="", kind="port"):
+    """Time work(i, tls) (one item = one frame, tls = per-thread state) on 1 thread, then on a pool of
+    cpu_workers() threads, each for about `seconds` of wall time (ctypes releases the GIL, so the
+    pool scales). Returns (single-thread baseline dict, pool baseline dict)."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run_for(tls, deadline, start):
+        n = 0
+        while time.perf_counter() < deadline:
+            work(start + n, tls)
+            n += 1
+        return n
+
+    tls0 = {}
+    work(0, tls0)  # warm (allocations, page faults)
+    t0 = time.perf_counter()
+    n1 = run_for(tls0, t0 + seconds, 0)
+    el1 = time.perf_counter() - t0
+    workers, visible, cap = cpu_workers()
+    barrier = threading.Barrier(workers)
+
+    def pooled(w):
+        tls = {}
+        work(w, tls)
+        barrier.wait()
+        t = time.perf_counter()
+        n = run_for(tls, t + seconds, 1000 * w)
+        return n, time.perf_counter() - t
+
+    with ThreadPoolExecutor(workers) as ex:
+        res = list(ex.map(pooled, range(workers)))
+    n2 = sum(r[0] for r in res)
+    el2 = max(r[1] for r in res)
+    host = f"host {cpu_model()}, {visible} logical CPUs visible"
+    single = {"value": round(n1 * px_per_item / el1 / 1e6, 3), "unit": unit, "cores": 1, "kind": kind,
+              "sample": f"{n1} frames in {el1:.1f} s on 1 thread: {label}; {host}"}
+    pool = {"value": round(n2 * px_per_item / el2 / 1e6, 3), "unit": unit, "cores": workers, "kind": kind,
+            "sample": f"{n2} frames in {el2:.1f} s over {workers} threads ({cap}), one detector state per "
+                      f"thread: {label}; {host}"}
+    return single, pool
+
+
+def cpu_frames(torch, dev, pattern, n, rows, cols, seed, period=16):
+    return make_frames(torch, pattern, n, rows, cols, seed, dev, period).cpu().numpy()
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without torchrun: start N rank processes (one GPU each) and wait for them.
+    The parent never touches the GPU (only the ranks do), so no GPU context is inherited or exec'd."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def launch_check(args, world, rank, local):
+    """FD_BENCH_LAUNCH_CHECK=1: the rank layout without any GPU work (the CPU tests use it with gloo):
+    every rank reports its device index; rank 0 prints one JSON line."""
     import torch.distributed as dist
 
+    ndev = int(os.environ.get("FD_BENCH_LAUNCH_CHECK_DEVICES", "0")) or world
+    dist.init_process_group("gloo")
+    objs = [None] * world
+    dist.all_gather_object(objs, {"rank": rank, "local_rank": local, "device": local % ndev, "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "requested_gpus": args.gpus, "ranks": objs}), flush=True)
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # self-launch: one rank process per GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch one rank per GPU")
+    if os.environ.get("FD_BENCH_LAUNCH_CHECK") == "1":
+        return launch_check(args, world, rank, local)
+    import torch
+    import torch.distributed as dist
+
     # Control-plane collectives only (barrier, timing max): RCCL by default; FD_BENCH_BACKEND=gloo
     # rehearses N>1 on fewer GPUs (ranks then share devices round-robin).
     backend = os.environ.get("FD_BENCH_BACKEND", "nccl")
-    dev_index = local % max(torch.cuda.device_count(), 1)
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench.py: {world} ranks but {ndev} visible GPUs (RCCL needs one GPU per rank; "
+                         "FD_BENCH_BACKEND=gloo rehearses more ranks than GPUs)")
+    dev_index = local % max(ndev, 1)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     if world > 1:
@@ -553,6 +667,11 @@ def main():
                                           10, 2, False, seed=99 + rank)
         with phase(torch, "north_star_kernel"):
             kms = kernel_time_ms(torch, fd, pool2, "shi_tomasi", 40.0, reps=10)
+        del pool2
+        with phase(torch, "north_star_kernel_checker"):
+            pool3 = [make_frames(torch, "checker", ns_batch, 1080, 1920, 199 + rank + 7919 * i, dev) for i in range(2)]
+            kms_checker = kernel_time_ms(torch, fd, pool3, "shi_tomasi", 40.0, reps=10)
+            del pool3
         kb = ns_batch * 1080 * 1920
         ach = kb / (kms * 1e-3) / 1e9
         out["north_star"] = {
@@ -560,6 +679,7 @@ def main():
             "mpix_s_per_gpu": round(d2 * kb / s2 / 1e6, 1), "ms_per_step": round(s2 / d2 * 1e3, 4),
             "kernel": "k_corner<ShiTomasi>", "kernel_ms": round(kms, 4),
             "kernel_mpix_s": round(kb / (kms * 1e-3) / 1e6, 1),
+            "kernel_ms_checker": round(kms_checker, 4),
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb,
                          "traffic": measured_traffic("northstar_k_corner")[0]},
@@ -567,7 +687,6 @@ def main():
                            "~37 VALU lane-instr/px (309 M wave-instructions per launch), so VALU issue, not HBM, bounds "
                            "this kernel (DESIGN.md)"),
         }
-        del pool2
 
     # ---- BASELINE configs[2]: FAST-12 + BRIEF-256, 1280x720 batch 64 (detect -> describe on device) --
     if not args.no_config3:
@@ -590,38 +709,60 @@ def main():
             out["end_to_end_host_frames"] = run_end_to_end(torch, fd, args)
             out["end_to_end_ingest"] = run_ingest(torch, fd, args)
 
-    # ---- CPU baseline: the oracle (single thread), bounded sample, rank 0 at N=1 ------------------
+    # ---- CPU baselines beside every leg: rank 0 at N=1, bounded samples of the same workloads ------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import oracle as O
 
         O.lib()
-        frames = make_frames(torch, args.pattern, 64, args.rows, args.cols, 4242, dev).cpu().numpy()
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < args.cpu_seconds and n < 100000:
-            O.detect(KIND[args.detector], frames[n % len(frames)], args.dist, THR[args.detector], args.need)
-            n += 1
-        el = time.perf_counter() - t0
-        out["cpu_baseline"] = {
-            "value": round(n * args.rows * args.cols / el / 1e6, 3), "unit": "Mpix/s", "cores": 1, "kind": "port",
-            "sample": f"{n} frames of the same workload ({args.detector}, {args.cols}x{args.rows}, dist {args.dist}, "
-                      f"need {args.need}) through oracle.detect (full DetectGoodFeatures restatement), "
-                      f"{el:.1f} s, 1 thread, host {os.cpu_count()} logical CPUs visible ({cpu_model()})",
-        }
-        # a pool of workers, one frame each at a time (ctypes releases the GIL)
-        from concurrent.futures import ThreadPoolExecutor
+        sec = args.cpu_seconds
+        leg = max(2.0, sec / 2.5)
 
-        workers = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
-        per_worker = max(1, n // 2)
-        t1 = time.perf_counter()
-        with ThreadPoolExecutor(workers) as ex:
-            list(ex.map(lambda i: O.detect(KIND[args.detector], frames[i % len(frames)], args.dist,
-                                           THR[args.detector], args.need), range(per_worker * workers)))
-        el2 = time.perf_counter() - t1
-        out["cpu_baseline_pool"] = {
-            "value": round(per_worker * workers * args.rows * args.cols / el2 / 1e6, 3), "unit": "Mpix/s",
-            "cores": workers, "kind": "port",
-            "sample": f"{per_worker * workers} frames over a pool of {workers} threads, {el2:.1f} s ({cpu_model()})",
-        }
+        def refflow(kind_name, frames, dist_, need_):
+            def work(i, tls):
+                det = tls.setdefault("det", O.RefFlowDetector())
+                det.detect(KIND[kind_name], frames[i % len(frames)], dist_, THR[kind_name], need_)
+            return work
+
+        frames = cpu_frames(torch, dev, args.pattern, 64, args.rows, args.cols, 4242)
+        flow = ("reference data flow (oracle/fd_oracle_refflow.cpp: float sliding sums, dense response map, "
+                "std::sort, int32 mask), g++ -O3 like the reference build")
+        out["cpu_baseline"], out["cpu_baseline_pool"] = cpu_leg(
+            refflow(args.detector, frames, args.dist, args.need), args.rows * args.cols, sec,
+            label=f"{args.detector} DetectGoodFeatures {args.cols}x{args.rows} {args.pattern}, dist {args.dist}, "
+                  f"need {args.need}; {flow}")
+        del frames
+        if "north_star" in out:
+            for pat in ("noise", "checker"):
+                fr = cpu_frames(torch, dev, pat, 8, 1080, 1920, 99)
+                b1, bp = cpu_leg(refflow("shi_tomasi", fr, 20, 200), 1080 * 1920, leg,
+                                 label=f"shi_tomasi DetectGoodFeatures 1920x1080 {pat}, dist 20, need 200; {flow}")
+                key = "" if pat == "noise" else "_checker"
+                out["north_star"]["cpu_baseline" + key], out["north_star"]["cpu_baseline_pool" + key] = b1, bp
+        if "config3_fast_brief" in out:
+            fr = cpu_frames(torch, dev, "noise", 8, 720, 1280, 777)
+
+            def fast_brief(i, tls):
+                det = tls.setdefault("det", O.RefFlowDetector())
+                img = fr[i % len(fr)]
+                kp = det.detect(KIND["fast"], img, 20, THR["fast"], 200)
+                O.brief(img, kp, 256, 8, 0)
+
+            out["config3_fast_brief"]["cpu_baseline"], out["config3_fast_brief"]["cpu_baseline_pool"] = cpu_leg(
+                fast_brief, 720 * 1280, leg,
+                label="FAST thr 10 DetectGoodFeatures (reference data flow) + BRIEF-256 per keypoint "
+                      "(oracle restatement), 1280x720 noise, dist 20, need 200")
+        if "config4_lsd_map" in out:
+            fr = cpu_frames(torch, dev, "checker", 8, 1080, 1920, 4242, period=64)
+
+            def lsd(i, tls):
+                img = fr[i % len(fr)]
+                nrm, _, _, idx = O.lsd_map(img)
+                O.lsd_sort(nrm, idx)
+
+            out["config4_lsd_map"]["cpu_baseline"], out["config4_lsd_map"]["cpu_baseline_pool"] = cpu_leg(
+                lsd, 1080 * 1920, leg,
+                label="ComputeLineLevelAngleMap restatement (maps + column-major valid list + std::sort by norm), "
+                      "1920x1080 64-px checker")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

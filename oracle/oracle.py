@@ -14,7 +14,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "liborc.so")
-SRC = os.path.join(HERE, "fd_oracle.cpp")
+SRCS = [os.path.join(HERE, f) for f in ("fd_oracle.cpp", "fd_oracle_refflow.cpp", "Makefile")]
 
 HARRIS, SHI_TOMASI, FAST = 0, 1, 2
 _P = ctypes.c_void_p
@@ -24,7 +24,7 @@ _lib = None
 def build(force: bool = False) -> str:
     """Compile the oracle with the reference build's float semantics (no -march => no FMA)."""
     os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(SRC):
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < max(map(os.path.getmtime, SRCS)):
         subprocess.check_call(["make", "-s", "-C", HERE])
     return LIB_PATH
 
@@ -52,6 +52,9 @@ def lib():
             "orc_brief": (None, [_P, i32, i32, _P, i32, i32, i32, i32, _P, _P, _P, _P]),
             "orc_nn_select": (i32, [_P, i32, i32, i32, i32, i32, f32, _P, i32, _P, i32]),
             "orc_nn_descriptors": (None, [_P, i32, i32, i32, _P, i32, _P]),
+            "orc_ref_state_new": (_P, []),
+            "orc_ref_state_free": (None, [_P]),
+            "orc_detect_refflow": (i32, [_P, i32, _P, i32, i32, i32, f32, u32, _P, i32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -132,6 +135,28 @@ def detect(kind, img, dist, thr, need, prior=None, sort_mode=0):
     n = lib().orc_detect(kind, _ptr(img), R, C, dist, thr, need, _ptr(pr), n_prior, sort_mode, _ptr(out), out_cap,
                          ctypes.byref(nout), _ptr(cr), _ptr(cx), _ptr(cy), cap)
     return out[: nout.value].copy(), (cr[:n].copy(), cx[:n].copy(), cy[:n].copy())
+
+
+class RefFlowDetector:
+    """DetectGoodFeatures in the reference's data flow (oracle/fd_oracle_refflow.cpp): float sliding
+    sums, dense response map, pair list, std::sort, int32 mask. One instance per thread, like the
+    reference's detector objects; used as the timed CPU baseline and checked against detect()."""
+
+    def __init__(self):
+        self._s = lib().orc_ref_state_new()
+
+    def detect(self, kind, img, dist, thr, need):
+        img = np.ascontiguousarray(img, np.uint8)
+        R, C = img.shape
+        cap = max(int(need), 1)
+        out = np.zeros((cap, 2), np.float32)
+        n = lib().orc_detect_refflow(self._s, kind, _ptr(img), R, C, dist, thr, need, _ptr(out), cap)
+        return out[:min(n, cap)].copy()
+
+    def __del__(self):
+        if getattr(self, "_s", None) and _lib is not None:
+            _lib.orc_ref_state_free(self._s)
+            self._s = None
 
 
 def prefix_has_ties(sorted_resp, n_scanned):
