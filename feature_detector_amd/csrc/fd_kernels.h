@@ -31,6 +31,10 @@ struct FastOffsets {
     int64_t k_start[kMaxOffsetSegs];
     double o_start[kMaxOffsetSegs];
     double inc[kMaxOffsetSegs];
+    // FAST score of a 16-bit ring mask (bit k = sample k of kFastIndice): the longest circular run of
+    // set bits, i.e. the reference's two-pass count (feature_point_fast_detector.cpp:55-78). 64 KiB,
+    // device memory owned by the context (build_offsets fills it once).
+    const uint8_t *run_lut;
 };
 
 struct PointsArgs {

@@ -20,6 +20,7 @@ namespace fdk {
 namespace {
 
 constexpr int kStage = 512;  // per-wave LDS staging of candidates (detect mode)
+constexpr int kStageFast = FD_STAGE_FAST;  // FAST: fewer flushes (each drains the wave's stores)
 constexpr float kInvCnt = 1.0f / 9.0f;                  // 1 / (3*3)  (:71)
 constexpr float kInvCnt2 = (1.0f / 9.0f) * (1.0f / 9.0f);  // harris :72
 constexpr float kHarrisAlpha = 0.04f;                  // feature_point_harris_detector.h:13
@@ -53,6 +54,8 @@ struct Sink {
     uint32_t *hist;  // LDS level-0 histogram of the workgroup's frame, or null
     int n;           // staged entries (wave-uniform)
     uint32_t *ovf;   // LDS flag: a wave of the workgroup flushed before the end (sorted-segment mode)
+    uint32_t *ehist = nullptr;  // LDS level-0 histogram counted at emit time instead of at flush (FAST)
+    int cap = kStage;           // staging capacity (entries)
 };
 
 __device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f) {
@@ -104,7 +107,7 @@ __device__ __forceinline__ void emit_row(Sink &sk, const PointsArgs &a, int f, i
             if (fl[m]) dst[pos++] = Cand{v[m], id0 + m};
     } else {
         if (tot == 0) return;
-        if (sk.n + tot > kStage) {
+        if (sk.n + tot > sk.cap) {
             // (sorted-segment mode: this frame's list is no longer one sorted segment per workgroup)
             if (a.segdesc && lane_id() == 0) {
                 atomicOr(&a.seg_bad[f], 1u);
@@ -116,6 +119,7 @@ __device__ __forceinline__ void emit_row(Sink &sk, const PointsArgs &a, int f, i
 #pragma unroll
         for (int m = 0; m < 4; ++m)
             if (fl[m]) {
+                if (sk.ehist) atomicAdd(&sk.ehist[((float_key(v[m]) - a.key_base) << a.key_lz) >> 20], 1u);
                 sk.resp[pos] = v[m];
                 sk.idx[pos] = id0 + m;
                 ++pos;
@@ -131,11 +135,13 @@ __device__ __forceinline__ uint32_t mask_bits4(const PointsArgs &a, int f, int r
 }
 
 // Workgroup-shared staging + level-0 histogram (detect mode).
-struct DetectLds {
-    float resp[4][kStage];
-    uint32_t idx[4][kStage];
+template <int S>
+struct DetectLdsT {
+    float resp[4][S];
+    uint32_t idx[4][S];
     uint32_t hist[kHistBins];
 };
+using DetectLds = DetectLdsT<kStage>;
 
 __device__ __forceinline__ void hist_clear(uint32_t *h) {
     for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) h[b] = 0;
@@ -154,7 +160,8 @@ __device__ __forceinline__ void hist_flush(const uint32_t *h, uint32_t *g) {
 // segment ordered by level-0 bin, descending (a counting sort on the workgroup's LDS histogram), and
 // the segment is described in segdesc[f][g]. k_select then reads only each segment's prefix at or
 // above its first-chunk cut (a few entries per workgroup) instead of scanning the whole list.
-__device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, bool active, DetectLds &L,
+template <class LdsT>
+__device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, bool active, LdsT &L,
                                           uint32_t (&wtot)[4], uint32_t &wg_base) {
     const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
     __syncthreads();
@@ -165,7 +172,8 @@ __device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, 
     }
     const int n = active ? sk.n : 0;
     auto bin_of = [&](float r) { return ((float_key(r) - a.key_base) << a.key_lz) >> 20; };
-    for (int i = lane; i < n; i += kWave) atomicAdd(&L.hist[bin_of(sk.resp[i])], 1u);
+    if (!sk.ehist)  // (FAST counted its candidates at emit time)
+        for (int i = lane; i < n; i += kWave) atomicAdd(&L.hist[bin_of(sk.resp[i])], 1u);
     hist_flush(L.hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);  // (leads with a barrier)
     __syncthreads();
     // in place: hist[b] = entries of bins above b (exclusive scan in descending bin order)
@@ -444,63 +452,70 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
 }
 
 // ---------------------------------------------------------------------------------------------------
-// K3: FAST-12. Same tile walk with a 7-row register window (ring radius 3).
+// K3: FAST-12
 // ---------------------------------------------------------------------------------------------------
-// Bresenham ring of radius 3 (kFastIndice, feature_point_fast_detector.cpp:7-8), as compile-time tables.
-__device__ constexpr int ring_dx(int k) {
-    constexpr int8_t t[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-    return t[k];
+// Byte-parallel (SWAR) comparisons: a lane's dword holds 4 consecutive pixels of one row, and every
+// ring sample of those 4 pixels is one dword too (the row's dword shifted by dx bytes), so one compare
+// sequence classifies 4 pixels. Only bit 7 of each byte of a result is meaningful.
+constexpr uint32_t kH = 0x80808080u;  // top bit of every byte
+constexpr uint32_t kL = 0x7F7F7F7Fu;  // low 7 bits of every byte
+constexpr uint32_t kOnes = 0x01010101u;
+
+// Per byte: x > y, from the low-7-bit difference (no borrow leaves a byte: the minuend carries the top
+// bit, the subtrahend is at most 0x80) and the top bits. yk = (y & kL) + kOnes, precomputed per pixel.
+// The final select (x7 != y7 ? x7 : z7) is one v_bitop3_b32.
+__device__ __forceinline__ uint32_t swar_gt(uint32_t x, uint32_t y, uint32_t yk) {
+    const uint32_t z = (x | kH) - yk;
+    return (x & ~y) | (~(x ^ y) & z);
 }
-__device__ constexpr int ring_dy(int k) {
-    constexpr int8_t t[16] = {-3, -3, -2, -1, 0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3};
-    return t[k];
+// Per byte: min(p + 15, 255) (bright threshold; v > 255 never holds, like v > p + 15 for p > 240).
+__device__ __forceinline__ uint32_t swar_adds15(uint32_t p) {
+    const uint32_t t = (p & kL) + 0x0F0F0F0Fu;      // low 7 bits + 15: bit 7 = carry
+    const uint32_t ov = p & t & kH;                  // p >= 128 and carry: the sum exceeds 255
+    const uint32_t ovm = (ov - (ov >> 7)) | ov;      // 0xFF where ov
+    return t | (p & kH) | ovm;
+}
+// Per byte: max(p - 15, 0) (dark threshold; v < 0 never holds, like v < p - 15 for p < 15).
+__device__ __forceinline__ uint32_t swar_subs15(uint32_t p) {
+    const uint32_t d = (p | kH) - 0x0F0F0F0Fu;       // 0x80 + (p & 0x7F) - 15 >= 0x71: no borrow
+    const uint32_t un = ~p & ~d & kH;                // p < 128 and the difference below 128: p < 15
+    const uint32_t unm = (un - (un >> 7)) | un;
+    return (d ^ (~p & kH)) & ~unm;
+}
+// The 4 pixels' samples at column offset dx of a row held as [L | P | R] (compile-time dx).
+template <int DX>
+__device__ __forceinline__ uint32_t shifted(uint32_t L, uint32_t P, uint32_t R) {
+    if constexpr (DX == 0) return P;
+    else if constexpr (DX > 0) return __builtin_amdgcn_alignbyte(R, P, DX);
+    else return __builtin_amdgcn_alignbyte(P, L, 4 + DX);
 }
 
-// Longest circular run of set bits in a 16-bit ring mask (== the reference's two-pass count,
-// feature_point_fast_detector.cpp:55-78; 16 when the whole ring is set).
-__device__ __forceinline__ int circ_run16(uint32_t b) {
-    if (b == 0xFFFFu) return 16;
-    const uint32_t x = b | (b << 16);
-    const uint32_t r2 = x & (x >> 1), r4 = r2 & (r2 >> 2), r8 = r4 & (r4 >> 4);
-    uint32_t S = 0xFFFFFFFFu, T;
-    int r = 0;
-    T = S & r8;
-    if (T) { S = T; r = 8; }
-    T = S & (r4 >> r);
-    if (T) { S = T; r += 4; }
-    T = S & (r2 >> r);
-    if (T) { S = T; r += 2; }
-    T = S & (x >> r);
-    if (T) { r += 1; }
-    return r;
-}
-
-__device__ __forceinline__ float fast_offset(int nseg, const int64_t *ks, const double *os, const double *inc,
-                                             int64_t k) {
+// FAST running offset o_k (feature_point_fast_detector.cpp:85,93) from the segment table: inside a
+// segment o_k = o_s + (k - k_s) * inc exactly (build_offsets checks it), and one fma rounds that exact
+// value once, so the float result is the reference's sum. Per-lane segment search (binary, LDS).
+__device__ __forceinline__ float fast_offset(int nseg, const int32_t *ks, const float *os, const float *inc, int32_t k) {
     int lo = 0, hi = nseg - 1;
     while (lo < hi) {  // last segment with k_start <= k
         const int mid = (lo + hi + 1) >> 1;
         if (ks[mid] <= k) lo = mid; else hi = mid - 1;
     }
-    return static_cast<float>(os[lo] + static_cast<double>(k - ks[lo]) * inc[lo]);
+    return __builtin_fmaf(static_cast<float>(k - ks[lo]), inc[lo], os[lo]);
 }
 
 template <bool RASTER, bool MASKED, bool ALIGNED>
-__device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int64_t *seg_k,
-                                          const double *seg_o, const double *seg_inc, int f, int ty, int tx, Sink &sk);
+__device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int32_t *seg_k,
+                                          const float *seg_o, const float *seg_inc, int f, int ty, int tx, Sink &sk);
 
 template <bool RASTER, bool MASKED, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
-    __shared__ DetectLds lds_all[1];
-    __shared__ int64_t seg_k[kMaxOffsetSegs];
-    __shared__ double seg_o[kMaxOffsetSegs], seg_inc[kMaxOffsetSegs];
-    if (threadIdx.x == 0)
-        for (int i = 0; i < off.nseg; ++i) {
-            seg_k[i] = off.k_start[i];
-            seg_o[i] = off.o_start[i];
-            seg_inc[i] = off.inc[i];
-        }
-    __syncthreads();
+    __shared__ DetectLdsT<kStageFast> lds_all[1];
+    __shared__ int32_t seg_k[kMaxOffsetSegs];
+    __shared__ float seg_o[kMaxOffsetSegs], seg_inc[kMaxOffsetSegs];
+    for (int i = threadIdx.x; i < off.nseg; i += blockDim.x) {
+        seg_k[i] = static_cast<int32_t>(off.k_start[i]);  // frames < 2^31 px (checked on the host)
+        seg_o[i] = static_cast<float>(off.o_start[i]);     // exact: a float of the sequence
+        seg_inc[i] = static_cast<float>(off.inc[i]);       // exact: a difference of two nearby floats
+    }
     int f, ty, tx;
     const bool active = decode_tile(a, f, ty, tx);
     __shared__ uint32_t seg_ovf;
@@ -508,9 +523,14 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
     if constexpr (!RASTER) {
         const int wv = threadIdx.x >> 6;
         sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0, &seg_ovf};
+        sk.ehist = sk.hist;  // FAST: histogram counted at emit time (measured faster than at flush)
+        sk.hist = nullptr;
+        sk.cap = kStageFast;
         if (threadIdx.x == 0) seg_ovf = 0;
-        if (a.hist0) hist_clear(lds_all[0].hist);
+        if (a.hist0) hist_clear(lds_all[0].hist);  // (includes the barrier for the segment table)
         else __syncthreads();
+    } else {
+        __syncthreads();
     }
     if (active) fast_tile<RASTER, MASKED, ALIGNED>(a, off, seg_k, seg_o, seg_inc, f, ty, tx, sk);
     if constexpr (!RASTER) {
@@ -524,20 +544,36 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
     }
 }
 
+// K3: FAST-12 (feature_point_fast_detector.cpp:11-98). Same tile walk as K1 with a 7-row register
+// window (ring radius 3). Per row step a lane classifies its 4 pixels at once:
+//  * thresholds min(p+15, 255) / max(p-15, 0) per byte; the cardinal pre-check (:20-42: samples 4, 8,
+//    12 all brighter or all darker) as 6 byte-parallel compares;
+//  * only if a lane of the wave passes: the other 13 samples, each bright/dark bit inserted into
+//    per-pixel 8-bit halves of the ring masks (bit k = sample k);
+//  * the score, the longest circular run of either mask (the reference's two-pass count, :55-78), from
+//    a 64 Ki-entry table indexed by the 16-bit mask (L2/L1-resident), for passing pixels only;
+//  * response = score + o_k (:88) with o_k from the segment table (one fma).
 template <bool RASTER, bool MASKED, bool ALIGNED>
-__device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int64_t *seg_k,
-                                          const double *seg_o, const double *seg_inc, int f, int ty, int tx, Sink &sk) {
+__device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int32_t *seg_k,
+                                          const float *seg_o, const float *seg_inc, int f, int ty, int tx, Sink &sk) {
     const int lane = lane_id();
     const int rows = a.rows, cols = a.cols;
     const int c0 = tx * kTileW + 4 * (lane - 1);
     const int y0 = 3 + ty * a.tile_h;
     const int y1 = min(y0 + a.tile_h, rows - 3);  // output rows [y0, y1) within [3, rows-4]
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
-    const int diff = 15;  // kMinPixelDiffValue (feature_point_fast_detector.h:14)
+    const auto lut = make_rsrc(off.run_lut, 65536u);
 
     bool colv[4];
+    uint32_t colmask = 0;  // bit 7 of byte m: column c0+m inside [3, cols-4], owned by an interior lane
 #pragma unroll
-    for (int m = 0; m < 4; ++m) colv[m] = lane >= 1 && lane <= 62 && c0 + m >= 3 && c0 + m <= cols - 4;
+    for (int m = 0; m < 4; ++m) {
+        colv[m] = lane >= 1 && lane <= 62 && c0 + m >= 3 && c0 + m <= cols - 4;
+        colmask |= colv[m] ? (0x80u << (8 * m)) : 0u;
+    }
+    // the tile's scan-index range per row (unmasked k = (row-3)(cols-6) + col-3) and its offset segment
+    const int cmin = max(tx * kTileW, 3), cmax = min(tx * kTileW + kTileW - 1, cols - 4);
+    int sg = 0;  // wave-uniform, advances with the rows
 
     uint32_t P[7], L[7], R[7];
 #pragma unroll
@@ -555,41 +591,74 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
             R[s] = from_right(P[s]);
             const int orow = ri - 3;  // output row; its window rows orow-3..orow+3 are slots s+1..s (mod 7)
             if (orow < y0 || orow >= y1) continue;  // wave-uniform
-#define PX(dy, j) win_byte(L[(s + 4 + (dy)) % 7], P[(s + 4 + (dy)) % 7], R[(s + 4 + (dy)) % 7], (j))
-            uint32_t mb = 0xFu;
-            if constexpr (MASKED) mb = mask_bits4(a, f, orow, c0);
-            bool pass[4];
-            int p[4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                p[m] = PX(0, m);
-                const int hi = p[m] + diff, lo = p[m] - diff;
-                const int s4 = PX(0, m + 3), s8 = PX(3, m), s12 = PX(0, m - 3);
-                // Cardinal pre-check (:20-42): samples 4, 8, 12 all brighter or all darker.
-                pass[m] = colv[m] && ((mb >> m) & 1u) &&
-                          ((s4 > hi && s8 > hi && s12 > hi) || (s4 < lo && s8 < lo && s12 < lo));
+#define ROW(dy) L[(s + 4 + (dy)) % 7], P[(s + 4 + (dy)) % 7], R[(s + 4 + (dy)) % 7]
+            const uint32_t p = P[(s + 4) % 7];
+            const uint32_t tb = swar_adds15(p), td = swar_subs15(p);
+            const uint32_t tbk = (tb & kL) + kOnes;         // bright: v > tb
+            const uint32_t tdk = (td | kH) - kOnes;          // dark: td > v, i.e. v < td
+            auto bright = [&](uint32_t v) { return swar_gt(v, tb, tbk); };
+            auto dark = [&](uint32_t v) {
+                const uint32_t z = tdk - (v & kL);
+                return (td & ~v) | (~(td ^ v) & z);
+            };
+            uint32_t live = colmask;
+            if constexpr (MASKED) {
+                const uint32_t mb = mask_bits4(a, f, orow, c0);
+                live &= ((mb & 1u) ? 0x80u : 0u) | ((mb & 2u) ? 0x8000u : 0u) | ((mb & 4u) ? 0x800000u : 0u) |
+                        ((mb & 8u) ? 0x80000000u : 0u);
             }
+            // Cardinal pre-check (:20-42): samples 4 (dx 3), 8 (dy 3), 12 (dx -3) all bright or all dark.
+            const uint32_t v4 = shifted<3>(ROW(0)), v8 = P[(s + 7) % 7], v12 = shifted<-3>(ROW(0));
+            const uint32_t b4 = bright(v4), b8 = bright(v8), b12 = bright(v12);
+            const uint32_t d4 = dark(v4), d8 = dark(v8), d12 = dark(v12);
+            const uint32_t pass = ((b4 & b8 & b12) | (d4 & d8 & d12)) & live;
             int score[4] = {0, 0, 0, 0};
-            if (ballot(pass[0] || pass[1] || pass[2] || pass[3]) != 0ull) {
+            if (ballot(pass != 0u) != 0ull) {  // wave-uniform
+                // ring masks, 8 samples per half: acc = bfi(kH, g, acc >> 1) inserts sample k at bit 7;
+                // after 8 insertions sample k of the half sits at bit k - 8*half of each byte.
+                uint32_t blo, bhi, dlo, dhi;
+                auto put = [](uint32_t &acc, uint32_t g) { acc = (g & kH) | ((acc >> 1) & kL); };
+                // kFastIndice (:7-8): k -> (dx, dy)
+                const uint32_t v0 = shifted<0>(ROW(-3)), v1 = shifted<1>(ROW(-3)), v2 = shifted<2>(ROW(-2));
+                const uint32_t v3 = shifted<3>(ROW(-1)), v5 = shifted<3>(ROW(1)), v6 = shifted<2>(ROW(2));
+                const uint32_t v7 = shifted<1>(ROW(3));
+                blo = bright(v0); dlo = dark(v0);
+                put(blo, bright(v1)); put(dlo, dark(v1));
+                put(blo, bright(v2)); put(dlo, dark(v2));
+                put(blo, bright(v3)); put(dlo, dark(v3));
+                put(blo, b4); put(dlo, d4);
+                put(blo, bright(v5)); put(dlo, dark(v5));
+                put(blo, bright(v6)); put(dlo, dark(v6));
+                put(blo, bright(v7)); put(dlo, dark(v7));
+                const uint32_t v9 = shifted<-1>(ROW(3)), v10 = shifted<-2>(ROW(2)), v11 = shifted<-3>(ROW(1));
+                const uint32_t v13 = shifted<-3>(ROW(-1)), v14 = shifted<-2>(ROW(-2)), v15 = shifted<-1>(ROW(-3));
+                bhi = b8; dhi = d8;
+                put(bhi, bright(v9)); put(dhi, dark(v9));
+                put(bhi, bright(v10)); put(dhi, dark(v10));
+                put(bhi, bright(v11)); put(dhi, dark(v11));
+                put(bhi, b12); put(dhi, d12);
+                put(bhi, bright(v13)); put(dhi, dark(v13));
+                put(bhi, bright(v14)); put(dhi, dark(v14));
+                put(bhi, bright(v15)); put(dhi, dark(v15));
 #pragma unroll
                 for (int m = 0; m < 4; ++m) {
-                    const int hi = p[m] + diff, lo = p[m] - diff;
-                    uint32_t B = 0, D = 0;
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        const int v = PX(ring_dy(k), m + ring_dx(k));
-                        B |= static_cast<uint32_t>(v > hi) << k;
-                        D |= static_cast<uint32_t>(v < lo) << k;
+                    if ((pass >> (8 * m + 7)) & 1u) {
+                        const uint32_t sel = 0x0C0C0000u | (static_cast<uint32_t>(4 + m) << 8) | static_cast<uint32_t>(m);
+                        const uint32_t ib = __builtin_amdgcn_perm(bhi, blo, sel);  // bits 0-7 | 8-15
+                        const uint32_t id = __builtin_amdgcn_perm(dhi, dlo, sel);
+                        score[m] = static_cast<int>(max(buf_load_u8(lut, static_cast<int32_t>(ib)),
+                                                        buf_load_u8(lut, static_cast<int32_t>(id))));
                     }
-                    const int sc = max(circ_run16(B), circ_run16(D));
-                    score[m] = pass[m] ? sc : 0;
                 }
             }
-#undef PX
-            // Scan index k of each pixel among mask-true pixels (the offset counter of :85-93).
-            int64_t kbase;
-            uint32_t mword = 0;
+#undef ROW
+            // Scan index k of each pixel among mask-true pixels (the offset counter of :85-93) and the
+            // response score + o_k (:88).
+            float resp[4];
+            bool fl[4];
             if constexpr (MASKED) {
+                int32_t kbase = 0;
+                uint32_t mword = 0;
                 const int64_t rb = static_cast<int64_t>(f) * rows + orow;
                 kbase = a.row_base[rb];
                 if (c0 >= 0 && c0 < cols) {
@@ -598,38 +667,45 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
                     mword = a.mask[rb * a.mask_wpr + w];
                     if (w == 0) mword &= ~7u;
                 }
-            } else {
-                kbase = static_cast<int64_t>(orow - 3) * (cols - 6) + (c0 - 3);
-            }
-            bool fl[4];
-            float v[4];
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                int64_t k;
-                if constexpr (MASKED) {
-                    k = kbase + __popc(mword & ((1u << ((c0 + m) & 31)) - 1u));  // earlier pixels in the word
+                for (int m = 0; m < 4; ++m) {
+                    const bool lv = (live >> (8 * m + 7)) & 1u;
+                    const int32_t k = kbase + __popc(mword & ((1u << ((c0 + m) & 31)) - 1u));  // earlier pixels in the word
+                    resp[m] = 0.0f;
+                    if (lv && (score[m] > 0 || k >= off.k0))
+                        resp[m] = static_cast<float>(score[m]) + fast_offset(off.nseg, seg_k, seg_o, seg_inc, k);
+                    fl[m] = lv && resp[m] > a.thr;
+                }
+            } else {
+                const int32_t krow = (orow - 3) * (cols - 6) - 3;  // k = krow + column
+                const int32_t kmin = krow + cmin, kmax = krow + cmax;
+                while (sg + 1 < off.nseg && seg_k[sg + 1] <= kmin) ++sg;  // (uniform; rows only move forward)
+                if (sg + 1 >= off.nseg || seg_k[sg + 1] > kmax) {     // the whole row step in one segment
+                    const float os = seg_o[sg], inc = seg_inc[sg];
+                    const int32_t kr = krow + c0 - seg_k[sg];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        resp[m] = static_cast<float>(score[m]) + __builtin_fmaf(static_cast<float>(kr + m), inc, os);
+                        fl[m] = colv[m] && resp[m] > a.thr;
+                    }
                 } else {
-                    k = kbase + m;
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        resp[m] = 0.0f;
+                        if (colv[m]) resp[m] = static_cast<float>(score[m]) +
+                                               fast_offset(off.nseg, seg_k, seg_o, seg_inc, krow + c0 + m);
+                        fl[m] = colv[m] && resp[m] > a.thr;
+                    }
                 }
-                const bool live = colv[m] && ((mb >> m) & 1u);
-                float resp = 0.0f;
-                bool cand = false;
-                if (live && (score[m] > 0 || k >= off.k0)) {
-                    const float o = fast_offset(off.nseg, seg_k, seg_o, seg_inc, k);
-                    resp = static_cast<float>(score[m]) + o;  // :88 ComputeResponseOfPixel(...) + offset
-                    cand = resp > a.thr;
-                }
-                fl[m] = cand;
-                v[m] = resp;
             }
             const uint64_t b[4] = {ballot(fl[0]), ballot(fl[1]), ballot(fl[2]), ballot(fl[3])};
-            emit_row<RASTER, kSegFast>(sk, a, f, tx, orow, c0, b, fl, v);
+            emit_row<RASTER, kSegFast>(sk, a, f, tx, orow, c0, b, fl, resp);
             if constexpr (RASTER) {
                 if (a.resp_map != nullptr) {
                     float *mrow = a.resp_map + (static_cast<int64_t>(f) * rows + orow) * cols;
 #pragma unroll
                     for (int m = 0; m < 4; ++m)
-                        if (fl[m]) mrow[c0 + m] = v[m];
+                        if (fl[m]) mrow[c0 + m] = resp[m];
                 }
             }
         }

@@ -49,6 +49,8 @@ struct fd_ctx {
     int status_batch = 0;
     int tie_order = FD_TIES_RASTER;
     DevBuf ord, ord_meta;  // FD_TIES_REFERENCE: host-computed visiting orders of flagged frames
+    DevBuf run_lut;        // FAST score per 16-bit ring mask (FastOffsets::run_lut), filled once
+    bool run_lut_ready = false;
     hipEvent_t xev = nullptr;  // orders a stream switch after the old stream's work (fd_ctx_set_stream)
     // FAST offset table cache
     int64_t off_n = -1;
@@ -126,7 +128,32 @@ int choose_tile_h(int64_t batch, int tiles_x, int out_rows, int period, int max_
 
 // FAST running offset o_0 = 1e-5f, o_{k+1} = fl(o_k + 1e-5f) (feature_point_fast_detector.cpp:85,93)
 // as runs of constant increment; verified exact against the recurrence before use.
+// FAST score table (FastOffsets::run_lut): for every 16-bit ring mask, the reference's two-pass count
+// (feature_point_fast_detector.cpp:55-78) of consecutive set bits, run over the mask twice without a
+// reset between the passes (so a run may wrap around), stopping once 16 is reached.
+int ensure_run_lut(fd_ctx *c) {
+    if (c->run_lut_ready) return FD_OK;
+    FD_HIP_TRY(c, ensure(c, c->run_lut, 65536));
+    std::vector<uint8_t> table(65536);
+    for (uint32_t b = 0; b < 65536; ++b) {
+        int run = 0, best = 0;
+        for (int pass = 0; pass < 2 && best < 16; ++pass)
+            for (int k = 0; k < 16; ++k) {
+                run = ((b >> k) & 1u) ? run + 1 : 0;
+                best = std::max(best, run);
+            }
+        table[b] = static_cast<uint8_t>(std::min(best, 16));
+    }
+    FD_HIP_TRY(c, hipMemcpyAsync(c->run_lut.p, table.data(), 65536, hipMemcpyHostToDevice, c->stream));
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the host table dies with this call
+    c->run_lut_ready = true;
+    return FD_OK;
+}
+
 int build_offsets(fd_ctx *c, int64_t n, float thr) {
+    int rc = ensure_run_lut(c);
+    if (rc) return rc;
+    c->off.run_lut = as<uint8_t>(c->run_lut);
     if (c->off_n == n && c->off_thr == thr) return FD_OK;
     fdk::FastOffsets o{};
     o.nseg = 0;
@@ -161,6 +188,7 @@ int build_offsets(fd_ctx *c, int64_t n, float thr) {
         const float r = static_cast<float>(o.o_start[s] + static_cast<double>(k - o.k_start[s]) * o.inc[s]);
         if (r != seq[static_cast<size_t>(k)]) return fail(c, FD_ERR_INVALID, "FAST offset table not exact");
     }
+    o.run_lut = as<uint8_t>(c->run_lut);
     c->off = o;
     c->off_n = n;
     c->off_thr = thr;
@@ -566,7 +594,7 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
-                      &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta};
+                      &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut};
     for (DevBuf *b : bufs) release(*b);
     if (c->xev) (void)hipEventDestroy(c->xev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

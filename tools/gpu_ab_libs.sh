@@ -1,0 +1,14 @@
+# A/B of library builds (FD_LIB_PATH) on one profile_kernels.py shape. usage: bash tools/gpu_ab_libs.sh <shape> lib1 lib2 ...
+set -e
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out/abl
+SHAPE=$1; shift
+for L in "$@"; do
+  n=$(basename $L .so)
+  FD_LIB_PATH=$GRAFT_REPO_ROOT/$L timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/abl/$n -o run -- python3 tools/profile_kernels.py --shape $SHAPE > /dev/null 2>&1
+  python3 -c "
+import csv,glob
+for f in glob.glob('gpurun_out/abl/$n/**/*kernel_stats.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        if r['Name'].startswith('void fdk'): print('$n', r['Name'][:50], r['Calls'], r['AverageNs'])
+"
+done
