@@ -18,7 +18,7 @@ EXPORTS = (
     "fd_ctx_get_stream",
     "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_ctx_set_tie_order", "fd_ctx_frame_status", "fd_points_detect", "fd_points_candidates", "fd_points_response",
     "fd_points_response_append",
-    "fd_lsd_map", "fd_brief_compute", "fd_nn_select", "fd_nn_descriptors",
+    "fd_lsd_map", "fd_lsd_lines", "fd_lsd_lines_state", "fd_brief_compute", "fd_nn_select", "fd_nn_descriptors",
     "fd_build_info",
     "fd_ingest_create", "fd_ingest_destroy", "fd_ingest_frames", "fd_ingest_submit", "fd_ingest_wait",
 )
@@ -40,6 +40,15 @@ FD_SAMPLE_BILINEAR, FD_SAMPLE_TRUNCATE = 0, 1
 class fd_nn_opts(ctypes.Structure):
     _fields_ = [("invalid_boundary", ctypes.c_int32), ("min_feature_distance", ctypes.c_int32),
                 ("max_features", ctypes.c_int32), ("min_response", ctypes.c_float), ("max_response", ctypes.c_float)]
+
+
+class fd_lsd_opts(ctypes.Structure):
+    _fields_ = [("min_valid_gradient_norm", ctypes.c_float), ("min_tolerance_angle_residual_rad", ctypes.c_float),
+                ("min_valid_line_length", ctypes.c_float), ("max_tolerance_inlier_ratio", ctypes.c_float)]
+
+
+# fd_lsd_rect as 12 floats: start x, y, end x, y, center x, y, length, width, angle, dir x, y, inlier ratio
+LSD_RECT_FLOATS = 12
 
 
 class fd_brief_opts(ctypes.Structure):
@@ -85,6 +94,8 @@ def load() -> ctypes.CDLL:
         "fd_points_response": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
         "fd_points_response_append": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
         "fd_lsd_map": (i32, [P, P, i32, i32, i32, i32, f32, P, P, P, P, i64, P, i32]),
+        "fd_lsd_lines": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_lsd_opts), u32, P, i32, P, i32]),
+        "fd_lsd_lines_state": (i32, [P, P, P, P, P, i64, P]),
         "fd_brief_compute": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_brief_opts), P, P, i32, P, P, i32]),
         "fd_nn_select": (i32, [P, P, i32, i32, i32, i32, ctypes.POINTER(fd_nn_opts), P, P, P, i32, P, i32]),
         "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, i32, P, P, i32, P, i32]),

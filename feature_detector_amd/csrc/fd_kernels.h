@@ -144,6 +144,12 @@ struct LsdArgs {
     int32_t *idx;
     int64_t idx_cap;
     int64_t *counts;
+    // Compact mode (fd_lsd_lines): no dense maps (norm/angle/valid null); the scatter writes, per valid
+    // pixel in scan order, its map index, norm and angle into one list for the whole batch, frame f's
+    // run starting at frame_base[f] (exclusive scan of counts, k_lsd_frames). Null = per-frame idx_cap.
+    float *lnorm;
+    float *langle;
+    int64_t *frame_base;
 };
 
 struct BriefArgs {
@@ -199,6 +205,8 @@ hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_g
 hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
+hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s);    // compact mode: map (counts, row bits) + scans
+hipError_t launch_lsd_scatter(const LsdArgs &a, hipStream_t s);  // compact mode: the lists
 hipError_t launch_brief(const BriefArgs &a, hipStream_t s);
 hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s);
 int heat_blocks_per_frame(int64_t npx);

@@ -180,7 +180,7 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     const uint32_t mbytes = static_cast<uint32_t>(rows - 1) * static_cast<uint32_t>(mc);
     const auto rn = make_rsrc(a.norm ? a.norm + mbase : nullptr, a.norm ? 4 * mbytes : 0u);
     const auto ra = make_rsrc(amap, amap ? 4 * mbytes : 0u);
-    const auto rv = make_rsrc(a.valid + mbase, mbytes);
+    const auto rv = make_rsrc(a.valid ? a.valid + mbase : nullptr, a.valid ? mbytes : 0u);
 
     auto put = [&](int r, const float (&nv)[4], const float (&av)[4], uint32_t vb) {
         if constexpr (INTERIOR) {
@@ -202,14 +202,14 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
             if (a.norm) *reinterpret_cast<F4 *>(a.norm + i) = F4{nv[0], nv[1], nv[2], nv[3]};
             if (a.angle) *reinterpret_cast<F4 *>(a.angle + i) = F4{av[0], av[1], av[2], av[3]};
             typedef uint32_t u32a1 __attribute__((aligned(1)));
-            *reinterpret_cast<u32a1 *>(a.valid + i) = vb;
+            if (a.valid) *reinterpret_cast<u32a1 *>(a.valid + i) = vb;
         } else {
 #pragma unroll
             for (int m = 0; m < 4; ++m)
                 if (colw[m]) {
                     if (a.norm) a.norm[i + m] = nv[m];
                     if (a.angle) a.angle[i + m] = av[m];
-                    a.valid[i + m] = static_cast<uint8_t>(vb >> (8 * m));
+                    if (a.valid) a.valid[i + m] = static_cast<uint8_t>(vb >> (8 * m));
                 }
         }
     };
@@ -391,8 +391,34 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     const int64_t cc = (static_cast<int64_t>(f) * mc + col) * a.chunks + chunk;
     int64_t pos = a.col_base[cc];
     const uint32_t *bits = a.rowbits + cc * a.words;
-    int32_t *out = a.idx + static_cast<int64_t>(f) * a.idx_cap;
     const int nw = (r1 - r0 + 31) >> 5;
+    if (a.frame_base) {
+        // Compact mode: the list entry carries the pixel's norm and angle, recomputed here from the
+        // four pixels (the same operations as the map pass: bit-identical), so no dense map is written.
+        const int64_t base = a.frame_base[f];
+        const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
+        for (int w = 0; w < nw; ++w) {
+            uint32_t m = bits[w];
+            while (m) {
+                const int rr = r0 + 32 * w + __builtin_ctz(m);
+                m &= m - 1u;
+                const int o = rr * cols + col;
+                const int ad = static_cast<int>(buf_load_u8(rs, o + cols + 1)) - static_cast<int>(buf_load_u8(rs, o));  // :76-77
+                const int bc = static_cast<int>(buf_load_u8(rs, o + 1)) - static_cast<int>(buf_load_u8(rs, o + cols));  // :78-79
+                const int sv = ad + bc, dv = ad - bc;
+                const float q = static_cast<float>(static_cast<uint32_t>(sv * sv + dv * dv));
+                const float nrm = sqrt_rn_rsq2(f2{q, q}).x * 0.5f;  // :82 (as in the map pass)
+                const float gx = static_cast<float>(sv) / 2.0f, gy = static_cast<float>(dv) / 2.0f;  // :80-81
+                const int64_t at = base + pos;
+                a.idx[at] = static_cast<int32_t>(static_cast<int64_t>(rr) * mc + col);
+                a.lnorm[at] = nrm;
+                a.langle[at] = fd_atan2f(gx, -gy);  // :85
+                ++pos;
+            }
+        }
+        return;
+    }
+    int32_t *out = a.idx + static_cast<int64_t>(f) * a.idx_cap;
     for (int w = 0; w < nw; ++w) {
         uint32_t m = bits[w];
         while (m) {
@@ -404,7 +430,38 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     }
 }
 
+// Compact mode: frame_base[f] = valid pixels of frames [0, f) (one workgroup; batch is small).
+__global__ __launch_bounds__(64) void k_lsd_frames(const int64_t *counts, int batch, int64_t *frame_base) {
+    if (threadIdx.x != 0) return;
+    int64_t acc = 0;
+    for (int f = 0; f < batch; ++f) {
+        frame_base[f] = acc;
+        acc += counts[f];
+    }
+    frame_base[batch] = acc;
+}
+
 }  // namespace
+
+hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s) {
+    const int64_t mwaves = static_cast<int64_t>(a.batch) * a.chunks * a.strips4;
+    const dim3 mgrid(static_cast<unsigned>((mwaves + 3) / 4)), block(256);
+    if (a.aligned4) hipLaunchKernelGGL(k_lsd_map<true>, mgrid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_lsd_map<false>, mgrid, block, 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lsd_scan, dim3(a.batch), dim3(1024), 0, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lsd_frames, dim3(1), dim3(64), 0, s, a.counts, a.batch, a.frame_base);
+    return hipGetLastError();
+}
+
+hipError_t launch_lsd_scatter(const LsdArgs &a, hipStream_t s) {
+    const int64_t waves = static_cast<int64_t>(a.batch) * a.chunks * a.strips;
+    hipLaunchKernelGGL(k_lsd_scatter, dim3(static_cast<unsigned>((waves + 3) / 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s) {
     const int64_t waves = static_cast<int64_t>(a.batch) * a.chunks * a.strips;

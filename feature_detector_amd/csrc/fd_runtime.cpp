@@ -11,14 +11,21 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fd_hip.h"
 #include "fd_kernels.h"
+#include "fd_lines.h"
 
 namespace {
 
 struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+};
+
+struct HostBuf {  // pinned host memory (hipHostMalloc), grow-only
     void *p = nullptr;
     size_t n = 0;
 };
@@ -50,6 +57,12 @@ struct fd_ctx {
     int tie_order = FD_TIES_RASTER;
     DevBuf ord, ord_meta;  // FD_TIES_REFERENCE: host-computed visiting orders of flagged frames
     DevBuf run_lut;        // FAST score per 16-bit ring mask (FastOffsets::run_lut), filled once
+    // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
+    DevBuf l_lnorm, l_langle, l_fbase;
+    HostBuf h_idx, h_norm, h_angle;
+    std::vector<int32_t> st_idx;
+    std::vector<float> st_norm, st_angle;
+    std::vector<uint8_t> st_used;
     bool run_lut_ready = false;
     hipEvent_t xev = nullptr;  // orders a stream switch after the old stream's work (fd_ctx_set_stream)
     // FAST offset table cache
@@ -92,6 +105,28 @@ hipError_t ensure(fd_ctx *c, DevBuf &b, size_t bytes) {
     if (e != hipSuccess) return e;
     b.n = want;
     return hipSuccess;
+}
+
+hipError_t ensure_host(HostBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.n >= bytes) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipHostFree(b.p);
+        if (e != hipSuccess) return e;
+        b.p = nullptr;
+        b.n = 0;
+    }
+    const size_t want = bytes + bytes / 4;  // headroom: batches vary in valid-pixel counts
+    hipError_t e = hipHostMalloc(&b.p, want, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    b.n = want;
+    return hipSuccess;
+}
+
+void release(HostBuf &b) {
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
 }
 
 void release(DevBuf &b) {
@@ -556,6 +591,34 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     return FD_OK;
 }
 
+// Shared LSD launch geometry (fd_lsd_map and fd_lsd_lines).
+void lsd_geometry(fdk::LsdArgs &a, int batch, int rows, int cols, const uint8_t *dframes) {
+    const int work_rows = rows - 3;  // rows [1, rows-3]
+    a.frames = dframes;
+    a.batch = batch;
+    a.rows = rows;
+    a.cols = cols;
+    a.strips = (cols - 1 + 63) / 64;  // map columns [0, cols-2]
+    a.strips4 = (cols - 1 + 255) / 256;
+    a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
+    int64_t target = 16384;  // waves of the map kernel
+    if (const char *e = std::getenv("FD_LSD_WAVES")) target = std::max<int64_t>(64, std::atoll(e));  // A/B
+    int64_t ch = (static_cast<int64_t>(batch) * a.strips4 * work_rows) / target;
+    ch = std::max<int64_t>(16, std::min<int64_t>(ch, 256));
+    a.chunk_h = static_cast<int>(ch);
+    a.chunks = (work_rows + a.chunk_h - 1) / a.chunk_h;
+    a.words = (a.chunk_h + 31) / 32;
+}
+
+// Host threads of the line stage: all hardware threads, capped by the process's thread budget
+// (OMP_NUM_THREADS, e.g. a lease's CPU share); FD_LINE_THREADS overrides.
+int default_line_threads() {
+    int t = static_cast<int>(std::thread::hardware_concurrency());
+    if (const char *e = std::getenv("OMP_NUM_THREADS"); e && std::atoi(e) > 0) t = std::min(t, std::atoi(e));
+    if (const char *e = std::getenv("FD_LINE_THREADS"); e && std::atoi(e) > 0) t = std::atoi(e);
+    return std::max(1, t);
+}
+
 }  // namespace
 
 extern "C" {
@@ -594,7 +657,9 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
-                      &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut};
+                      &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
+                      &c->l_lnorm,  &c->l_langle, &c->l_fbase};
+    for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle}) release(*b);
     for (DevBuf *b : bufs) release(*b);
     if (c->xev) (void)hipEventDestroy(c->xev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -1011,19 +1076,7 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         FD_HIP_TRY(c, hipMemsetAsync(dc, 0, sizeof(int64_t) * batch, c->stream));
     } else {  // k_lsd_map writes every map entry (zeros outside the scanned rows/columns)
         fdk::LsdArgs a{};
-        a.frames = dframes;
-        a.batch = batch;
-        a.rows = rows;
-        a.cols = cols;
-        a.strips = (cols - 1 + 63) / 64;  // map columns [0, cols-2]
-        a.strips4 = (cols - 1 + 255) / 256;
-        a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
-        int64_t target = 16384;  // waves of the map kernel
-        if (const char *e = std::getenv("FD_LSD_WAVES")) target = std::max<int64_t>(64, std::atoll(e));  // A/B
-        int64_t ch = (static_cast<int64_t>(batch) * a.strips4 * work_rows) / target;
-        ch = std::max<int64_t>(16, std::min<int64_t>(ch, 256));
-        a.chunk_h = static_cast<int>(ch);
-        a.chunks = (work_rows + a.chunk_h - 1) / a.chunk_h;
+        lsd_geometry(a, batch, rows, cols, dframes);
         a.min_norm = min_norm;
         a.norm = dn;
         a.angle = da;
@@ -1031,7 +1084,6 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         const size_t ncnt = static_cast<size_t>(batch) * mc * a.chunks;
         FD_HIP_TRY(c, ensure(c, c->l_cnt, sizeof(int32_t) * ncnt));
         FD_HIP_TRY(c, ensure(c, c->l_base, sizeof(int32_t) * ncnt));
-        a.words = (a.chunk_h + 31) / 32;
         FD_HIP_TRY(c, ensure(c, c->l_bits, sizeof(uint32_t) * ncnt * a.words));
         a.rowbits = as<uint32_t>(c->l_bits);
         a.col_cnt = as<int32_t>(c->l_cnt);
@@ -1053,6 +1105,105 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
             if (valid_counts[b] > idx_cap) return fail(c, FD_ERR_CAPACITY, "idx_cap smaller than the valid pixels");
     } else if (!frames_on_device) {
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    return FD_OK;
+}
+
+int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
+                 const fd_lsd_opts *opts, uint32_t needed, fd_lsd_rect *out_rects, int32_t rect_stride,
+                 int32_t *out_counts, int threads) {
+    int rc = check_shape(c, FD_HARRIS, batch, rows, cols, false);
+    if (rc) return rc;
+    if (rows < 2 || cols < 2) return fail(c, FD_ERR_INVALID, "LSD needs rows >= 2 and cols >= 2");  // :14
+    if (static_cast<int64_t>(rows - 1) * (cols - 1) >= (int64_t(1) << 29))
+        return fail(c, FD_ERR_INVALID, "LSD frame too large ((rows-1)*(cols-1) must be < 2^29)");
+    if (!opts || !out_counts || rect_stride < 0 || (rect_stride > 0 && !out_rects))
+        return fail(c, FD_ERR_INVALID, "bad output arguments");
+    if (frames == nullptr) return fail(c, FD_ERR_INVALID, "frames is NULL");
+    c->st_idx.clear();
+    c->st_norm.clear();
+    c->st_angle.clear();
+    c->st_used.clear();
+    for (int b = 0; b < batch; ++b) out_counts[b] = 0;
+    if (needed == 0) return FD_OK;  // :15
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    const uint8_t *dframes = nullptr;
+    rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
+    if (rc) return rc;
+    std::vector<int64_t> base(static_cast<size_t>(batch) + 1, 0);
+    if (rows - 3 > 0 && cols - 3 > 0) {
+        // GPU: validity counts + row bits and the scans (pass 1-2), then the compact lists (pass 3)
+        fdk::LsdArgs a{};
+        lsd_geometry(a, batch, rows, cols, dframes);
+        a.min_norm = opts->min_valid_gradient_norm;
+        const size_t ncnt = static_cast<size_t>(batch) * (cols - 1) * a.chunks;
+        FD_HIP_TRY(c, ensure(c, c->l_cnt, sizeof(int32_t) * ncnt));
+        FD_HIP_TRY(c, ensure(c, c->l_base, sizeof(int32_t) * ncnt));
+        FD_HIP_TRY(c, ensure(c, c->l_bits, sizeof(uint32_t) * ncnt * a.words));
+        FD_HIP_TRY(c, ensure(c, c->l_counts, sizeof(int64_t) * batch));
+        FD_HIP_TRY(c, ensure(c, c->l_fbase, sizeof(int64_t) * (static_cast<size_t>(batch) + 1)));
+        a.rowbits = as<uint32_t>(c->l_bits);
+        a.col_cnt = as<int32_t>(c->l_cnt);
+        a.col_base = as<int32_t>(c->l_base);
+        a.counts = as<int64_t>(c->l_counts);
+        a.frame_base = as<int64_t>(c->l_fbase);
+        FD_HIP_TRY(c, fdk::launch_lsd_count(a, c->stream));
+        FD_HIP_TRY(c, hipMemcpyAsync(base.data(), a.frame_base, sizeof(int64_t) * base.size(), hipMemcpyDeviceToHost,
+                                     c->stream));
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        const int64_t total = base[static_cast<size_t>(batch)];
+        if (total > 0) {
+            FD_HIP_TRY(c, ensure(c, c->l_idx, sizeof(int32_t) * total));
+            FD_HIP_TRY(c, ensure(c, c->l_lnorm, sizeof(float) * total));
+            FD_HIP_TRY(c, ensure(c, c->l_langle, sizeof(float) * total));
+            a.idx = as<int32_t>(c->l_idx);
+            a.idx_cap = total;
+            a.lnorm = as<float>(c->l_lnorm);
+            a.langle = as<float>(c->l_langle);
+            FD_HIP_TRY(c, fdk::launch_lsd_scatter(a, c->stream));
+            FD_HIP_TRY(c, ensure_host(c->h_idx, sizeof(int32_t) * total));
+            FD_HIP_TRY(c, ensure_host(c->h_norm, sizeof(float) * total));
+            FD_HIP_TRY(c, ensure_host(c->h_angle, sizeof(float) * total));
+            FD_HIP_TRY(c, hipMemcpyAsync(c->h_idx.p, a.idx, sizeof(int32_t) * total, hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(c->h_norm.p, a.lnorm, sizeof(float) * total, hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(c->h_angle.p, a.langle, sizeof(float) * total, hipMemcpyDeviceToHost,
+                                         c->stream));
+            FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        }
+    } else if (!frames_on_device) {
+        FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the staging copy reads the caller's buffer
+    }
+    // host: region growing + rectangles, frames over worker threads
+    std::vector<fdl::FrameList> fl(static_cast<size_t>(batch));
+    const int32_t *hidx = static_cast<const int32_t *>(c->h_idx.p);
+    const float *hn = static_cast<const float *>(c->h_norm.p), *ha = static_cast<const float *>(c->h_angle.p);
+    for (int b = 0; b < batch; ++b) {
+        const int64_t o = base[static_cast<size_t>(b)], n = base[static_cast<size_t>(b) + 1] - o;
+        fl[static_cast<size_t>(b)] = fdl::FrameList{n ? hidx + o : nullptr, n ? hn + o : nullptr, n ? ha + o : nullptr, n};
+    }
+    const int64_t n0 = fl[0].n;
+    c->st_used.assign(static_cast<size_t>(n0), 0);
+    fdl::detect_lines(rows, cols, *opts, fl.data(), batch, out_rects, rect_stride, out_counts, c->st_used.data(),
+                      threads > 0 ? threads : default_line_threads());
+    if (n0 > 0) {
+        c->st_idx.assign(fl[0].idx, fl[0].idx + n0);
+        c->st_norm.assign(fl[0].norm, fl[0].norm + n0);
+        c->st_angle.assign(fl[0].angle, fl[0].angle + n0);
+    }
+    return FD_OK;
+}
+
+int fd_lsd_lines_state(fd_ctx *c, int32_t *idx, float *norm, float *angle, uint8_t *used, int64_t cap, int64_t *n) {
+    if (!c || !n || cap < 0) return FD_ERR_INVALID;
+    const int64_t m = static_cast<int64_t>(c->st_idx.size());
+    *n = m;
+    const int64_t w = std::min(m, cap);
+    if (w > 0 && (!idx || !norm || !angle || !used)) return fail(c, FD_ERR_INVALID, "bad output arguments");
+    for (int64_t k = 0; k < w; ++k) {
+        idx[k] = c->st_idx[static_cast<size_t>(k)];
+        norm[k] = c->st_norm[static_cast<size_t>(k)];
+        angle[k] = c->st_angle[static_cast<size_t>(k)];
+        used[k] = c->st_used[static_cast<size_t>(k)];
     }
     return FD_OK;
 }

@@ -362,3 +362,31 @@ def lsd_map(frames, min_norm: float = 20.0, cap: int | None = None, ctx: Context
     _lib.check(ctx.ptr, rc)
     del keep
     return [(norm[i], ang[i], val[i], idx[i, :cnt[i]].copy()) for i in range(b)]
+
+
+# FeatureLineDetector::Options defaults (feature_line_detector.h:40-45); kDegToRad = kPai / 180 in float.
+LSD_TOL_RAD = float(np.float32(22.5) * (np.float32(3.14159265358979323846) / np.float32(180.0)))
+
+
+def lsd_lines(frames, needed: int = 1, min_norm: float = 20.0, tol_rad: float = LSD_TOL_RAD, min_length: float = 20.0,
+              min_inlier: float = 0.6, max_lines: int = 4096, threads: int = 0, ctx: Context | None = None):
+    """FeatureLineDetector::DetectGoodFeatures for a batch (fd_lsd_lines): GPU level-line map (compact
+    lists), region growing and rectangle fitting on `threads` host threads (0: all, capped by
+    OMP_NUM_THREADS). frames: numpy [B, R, C] / [R, C] u8 or a torch device tensor.
+
+    Returns a list over frames of float32 arrays [n, 12] (start x, y, end x, y, center x, y, length,
+    width, angle, dir x, y, inlier ratio); columns 0-3 are the reference's Vec4 features."""
+    ptr, on_dev, b, r, c, keep = _frames(frames)
+    ctx = _resolve_ctx(ctx, frames)
+    _bind_stream(ctx, on_dev)
+    opts = _lib.fd_lsd_opts(float(min_norm), float(tol_rad), float(min_length), float(min_inlier))
+    out = np.zeros((b, max(max_lines, 1), _lib.LSD_RECT_FLOATS), np.float32)
+    cnt = np.zeros((b,), np.int32)
+    rc = _lib.load().fd_lsd_lines(ctx.ptr, ctypes.c_void_p(ptr), 1 if on_dev else 0, b, r, c, ctypes.byref(opts),
+                                  int(needed), ctypes.c_void_p(out.ctypes.data), int(max_lines),
+                                  ctypes.c_void_p(cnt.ctypes.data), int(threads))
+    _lib.check(ctx.ptr, rc)
+    del keep
+    if (cnt > max_lines).any():
+        raise _lib.FdError(_lib.FD_ERR_CAPACITY, f"max_lines={max_lines} < {int(cnt.max())} segments found")
+    return [out[i, :cnt[i]].copy() for i in range(b)]

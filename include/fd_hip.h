@@ -170,6 +170,46 @@ int fd_lsd_map(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int bat
                float *norm, float *angle, uint8_t *valid, int32_t *valid_idx, int64_t idx_cap, int64_t *valid_counts,
                int outputs_on_device);
 
+/* ---- LSD line segments (level-line map on the GPU, region growing on host threads) --------------- */
+/* FeatureLineDetector::Options (feature_line_detector.h:40-45). */
+typedef struct fd_lsd_opts {
+    float min_valid_gradient_norm;         /* kMinValidGradientNorm (20) */
+    float min_tolerance_angle_residual_rad; /* kMinToleranceAngleResidualInRad (22.5 deg as float) */
+    float min_valid_line_length;           /* kMinValidLineLengthInPixel (20) */
+    float max_tolerance_inlier_ratio;      /* kMaxToleranceInlierRation (0.6) */
+} fd_lsd_opts;
+
+/* FeatureLineDetector::RectangleParam (feature_line_detector.h:29-38) of an accepted segment, as the
+ * reference leaves it in rectangles_ (start/end offset by +0.5, feature_line_detector.cpp:43-44). */
+typedef struct fd_lsd_rect {
+    float start[2], end[2], center[2]; /* (x, y) */
+    float length, width, angle;
+    float dir[2];
+    float inlier_ratio;
+} fd_lsd_rect;
+
+/*
+ * fd_lsd_lines -- FeatureLineDetector::DetectGoodFeatures (feature_line_detector.cpp:12-54) for a
+ * batch of frames. The level-line map runs on the GPU in compact mode (no dense maps: per valid pixel
+ * its map index, norm and angle in scan order, bit-exact to fd_lsd_map); the lists come back over PCIe
+ * once and region growing + rectangle fitting (:99-228) run per frame on `threads` host threads
+ * (<= 0: all hardware threads). Segment k of frame b is out_rects[b * rect_stride + k]; its endpoints
+ * are the reference's features[k] = (start.x, start.y, end.x, end.y). out_counts[b] = segments found
+ * (may exceed rect_stride: only rect_stride are written; FD_ERR_CAPACITY is not raised for lines).
+ * needed == 0 returns FD_OK with counts 0 and no work (:15). frames may be host or device memory.
+ * Unpinned semantics of the un-vendored Slam_Utility (CircularBuffer overflow, AngleDiffInRad): DESIGN.md.
+ */
+int fd_lsd_lines(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
+                 const fd_lsd_opts *opts, uint32_t needed, fd_lsd_rect *out_rects, int32_t rect_stride,
+                 int32_t *out_counts, int threads);
+
+/*
+ * fd_lsd_lines_state -- the last fd_lsd_lines call's frame 0 as the reference leaves its members
+ * (pixels_ / sorted_pixels_, feature_line_detector.h:74-75): the valid pixels in scan order (map index,
+ * norm, angle) and each one's final is_used flag. n receives the count; at most cap are written.
+ */
+int fd_lsd_lines_state(fd_ctx *ctx, int32_t *idx, float *norm, float *angle, uint8_t *used, int64_t cap, int64_t *n);
+
 /* ---- steered BRIEF descriptor ------------------------------------------------------------------- */
 /* BriefDescriptor::Options (descriptor_brief.h:17-20) plus the float-coordinate sampler of the
  * un-vendored GrayImage (descriptor_brief.cpp:24,42-43; see DESIGN.md: parity unpinned). */

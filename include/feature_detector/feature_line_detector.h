@@ -1,7 +1,7 @@
 // FeatureLineDetector (LSD): the reference's public API (src/feature_line_detector/
-// feature_line_detector.h:11-79). The level-line map (gradient norm, angle, validity, scan-ordered
-// valid list) is computed on the GPU by libfdhip.so; region growing and rectangle fitting run on the
-// host in the reference's order.
+// feature_line_detector.h:11-79). Segments come from fd_lsd_lines (GPU level-line map, host region
+// growing in libfdhip.so); pixels() / sorted_pixels() / rectangles() hold what the reference leaves
+// in its members after a call.
 #ifndef FEATURE_DETECTOR_FEATURE_LINE_DETECTOR_H_
 #define FEATURE_DETECTOR_FEATURE_LINE_DETECTOR_H_
 
@@ -14,34 +14,6 @@
 struct fd_ctx;
 
 namespace feature_detector {
-
-// Fixed-capacity FIFO standing in for Slam_Utility's CircularBuffer<T, N> (feature_line_detector.h:76-77).
-// Overflow policy (unpinned: the reference's implementation is not vendored): PushBack on a full buffer
-// overwrites the oldest element.
-template <typename T, int N>
-class LineRingBuffer {
-public:
-    void Clear() { head_ = size_ = 0; }
-    bool Empty() const { return size_ == 0; }
-    void PushBack(const T &v) {
-        if (size_ == N) {
-            buf_[head_] = v;
-            head_ = (head_ + 1) % N;
-            return;
-        }
-        buf_[(head_ + size_) % N] = v;
-        ++size_;
-    }
-    const T &Front() const { return buf_[head_]; }
-    void PopFront() {
-        head_ = (head_ + 1) % N;
-        --size_;
-    }
-
-private:
-    T buf_[N];
-    int head_ = 0, size_ = 0;
-};
 
 class FeatureLineDetector {
 public:
@@ -122,18 +94,15 @@ public:
     const std::string &last_error() const { return error_; }
 
 private:
+    bool EnsureContext();
+    // pixels_ / sorted_pixels_ as the reference leaves them (:56-97), from the GPU level-line map
     bool ComputeLineLevelAngleMap(const GrayImage &image);
-    void GrowRegion(PixelParam &seed_pixel, RegionParam &region);
-    void TryToAddPixelIntoCandidates(PixelParam &neighbour);
-    RectangleParam ConvertRegionToRectangle(const RegionParam &region);
 
 private:
     Options options_;
 
     PixelMatrix pixels_;
     std::vector<PixelParam *> sorted_pixels_;
-    LineRingBuffer<PixelParam *, 1000> candidates_;
-    LineRingBuffer<PixelParam *, 1000> visited_pixels_;
     std::vector<RectangleParam> rectangles_;
 
     fd_ctx *ctx_ = nullptr;

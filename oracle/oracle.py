@@ -14,7 +14,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "liborc.so")
-SRCS = [os.path.join(HERE, f) for f in ("fd_oracle.cpp", "fd_oracle_refflow.cpp", "Makefile")]
+SRCS = [os.path.join(HERE, f) for f in ("fd_oracle.cpp", "fd_oracle_refflow.cpp", "fd_oracle_lines.cpp", "Makefile")]
 
 HARRIS, SHI_TOMASI, FAST = 0, 1, 2
 _P = ctypes.c_void_p
@@ -52,6 +52,7 @@ def lib():
             "orc_brief": (None, [_P, i32, i32, _P, i32, i32, i32, i32, _P, _P, _P, _P]),
             "orc_nn_select": (i32, [_P, i32, i32, i32, i32, i32, f32, _P, i32, _P, i32]),
             "orc_nn_descriptors": (None, [_P, i32, i32, i32, _P, i32, _P]),
+            "orc_lsd_lines": (i64, [_P, i32, i32, _P, u32, _P, i64]),
             "orc_ref_state_new": (_P, []),
             "orc_ref_state_free": (None, [_P]),
             "orc_detect_refflow": (i32, [_P, i32, _P, i32, i32, i32, f32, u32, _P, i32]),
@@ -190,6 +191,22 @@ def lsd_sort(norm, idx, sort_mode=0):
     idx = np.array(idx, np.int32)
     lib().orc_lsd_sort(_ptr(norm), _ptr(idx), len(idx), sort_mode)
     return idx
+
+
+LSD_TOL_RAD = float(np.float32(22.5) * (np.float32(3.14159265358979323846) / np.float32(180.0)))
+
+
+def lsd_lines(img, needed=1, min_norm=20.0, tol_rad=LSD_TOL_RAD, min_length=20.0, min_inlier=0.6, cap=4096):
+    """FeatureLineDetector::DetectGoodFeatures (feature_line_detector.cpp:12-54) on one frame: [n, 12]
+    float32 rectangles (start x, y, end x, y, center x, y, length, width, angle, dir x, y, inlier)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    R, C = img.shape
+    opts = np.array([min_norm, tol_rad, min_length, min_inlier], np.float32)
+    out = np.zeros((max(cap, 1), 12), np.float32)
+    n = lib().orc_lsd_lines(_ptr(img), R, C, _ptr(opts), needed, _ptr(out), cap)
+    if n > cap:
+        raise RuntimeError(f"cap {cap} < {n} lines")
+    return out[:max(n, 0)].copy()
 
 
 def lsd_min_region_size(rows, cols, tol_rad=22.5 * 3.14159265358979323846 / 180.0):
