@@ -344,7 +344,17 @@ def graph_time_ms(torch, fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
-def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5):
+def _line_threads():
+    import multiprocessing
+
+    n = multiprocessing.cpu_count()
+    lease = os.environ.get("OMP_NUM_THREADS")
+    if lease and lease.isdigit() and int(lease) > 0:
+        n = min(n, int(lease))
+    return int(os.environ.get("FD_LINE_THREADS", n))
+
+
+def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5, line_reps=3):
     """BASELINE configs[3]: LSD level-line map (norm, angle, valid + column-major valid list) on
     structured 64-px checker frames, all on the device (the host region growing is not timed)."""
     frames = make_frames(torch, "checker", batch, rows, cols, seed, dev, period=64)
@@ -355,15 +365,30 @@ def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5):
     px = batch * rows * cols
     mpx = batch * (rows - 1) * (cols - 1)
     alg = px + 9 * mpx + 4 * valid  # read u8 frame; write norm f32 + angle f32 + valid u8; 4 B per listed pixel
-    del out, frames
+    del out
+    # Whole line detector (FeatureLineDetector::DetectGoodFeatures for every frame): GPU compact map,
+    # lists over PCIe, region growing + rectangles on host worker threads (fd_lsd_lines).
+    segs = fd.lsd_lines(frames, max_lines=2048)  # warm (workspace, pinned buffers, threads)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(line_reps):
+        segs = fd.lsd_lines(frames, max_lines=2048)
+    line_s = (time.perf_counter() - t0) / line_reps
+    n_lines = sum(len(x) for x in segs)
+    del frames
+    lines = {"ms_per_batch": round(line_s * 1e3, 3), "frames_per_s": round(batch / line_s, 1),
+             "lines_per_s": round(n_lines / line_s, 1), "lines_per_batch": n_lines,
+             "mpix_s": round(px / line_s / 1e6, 1), "host_threads": _line_threads(),
+             "note": "fd_lsd_lines: GPU level-line map (compact lists) + D2H + host region growing on worker threads"}
     return {
         "workload": f"LSD level-line map, {cols}x{rows} gray 64-px checker + noise, batch {batch}/GPU "
-                    "(BASELINE configs[3]; host region growing not timed)",
+                    "(BASELINE configs[3]); whole line detector under 'lines'",
         "ms_per_batch": round(ms, 4), "mpix_s": round(px / (ms * 1e-3) / 1e6, 1), "valid_pixels": valid,
         "kernels": "k_lsd_map + k_lsd_scan + k_lsd_scatter",
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_launch": alg},
+        "lines": lines,
     }
 
 
@@ -767,6 +792,14 @@ def main():
                 lsd, 1080 * 1920, leg,
                 label="ComputeLineLevelAngleMap restatement (maps + column-major valid list + std::sort by norm), "
                       "1920x1080 64-px checker")
+
+            def lines(i, tls):
+                O.lsd_lines(fr[i % len(fr)])
+
+            lb, lp = cpu_leg(lines, 1080 * 1920, leg,
+                             label="FeatureLineDetector::DetectGoodFeatures restatement (oracle/fd_oracle_lines.cpp, "
+                                   "the reference's data structures), 1920x1080 64-px checker")
+            out["config4_lsd_map"]["lines"]["cpu_baseline"], out["config4_lsd_map"]["lines"]["cpu_baseline_pool"] = lb, lp
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -112,6 +112,8 @@ private:
         state_.assign(n, 0);
         row_.resize(n);
         col_.resize(n);
+        cos_.resize(n);
+        sin_.resize(n);
         seeds_.resize(n);
         idx_ = fl.idx;
         norm_ = fl.norm;
@@ -123,6 +125,11 @@ private:
             row_[k] = i / pc_;
             col_[k] = i - row_[k] * pc_;
             seeds_[k] = {fl.norm[k], static_cast<int32_t>(k)};
+            // glibc cosf / sinf of the angle: GrowRegion calls them whenever a pixel seeds or joins a
+            // region, which happens many times per pixel (rejected regions release their pixels);
+            // the same call on the same value, made once
+            cos_[k] = std::cos(fl.angle[k]);
+            sin_[k] = std::sin(fl.angle[k]);
         }
         // sorted_pixels_: the scan-ordered list under the reference's comparator (:92-94)
         std::sort(seeds_.begin(), seeds_.end(),
@@ -155,15 +162,15 @@ private:
         state_[seed] |= kOccupied;
         region_.clear();
         float region_angle = angle_[seed];
-        float sum_dx = std::cos(angle_[seed]);
-        float sum_dy = std::sin(angle_[seed]);
+        float sum_dx = cos_[seed];
+        float sum_dy = sin_[seed];
         offer_neighbours(seed);
         while (!cand_.empty()) {
             const int32_t e = cand_.pop();
             seen_.push(e);
             if (std::fabs(wrap_diff(region_angle, angle_[e])) > o_.min_tolerance_angle_residual_rad) continue;
-            sum_dx += std::cos(angle_[e]);
-            sum_dy += std::sin(angle_[e]);
+            sum_dx += cos_[e];
+            sum_dy += sin_[e];
             region_angle = std::atan2(sum_dy, sum_dx);
             region_.push_back(e);
             state_[e] |= kUsed;
@@ -237,6 +244,7 @@ private:
     std::vector<uint64_t> mask_;
     std::vector<uint8_t> state_;
     std::vector<int32_t> row_, col_;
+    std::vector<float> cos_, sin_;
     std::vector<std::pair<float, int32_t>> seeds_;
     std::vector<int32_t> region_;
     const int32_t *idx_ = nullptr;

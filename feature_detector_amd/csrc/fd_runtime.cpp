@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -1126,6 +1127,8 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     c->st_used.clear();
     for (int b = 0; b < batch; ++b) out_counts[b] = 0;
     if (needed == 0) return FD_OK;  // :15
+    static const bool timing = std::getenv("FD_LINES_TIMING") != nullptr;  // diagnostic: phase times to stderr
+    const auto t_start = std::chrono::steady_clock::now();
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const uint8_t *dframes = nullptr;
     rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
@@ -1173,6 +1176,7 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     } else if (!frames_on_device) {
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // the staging copy reads the caller's buffer
     }
+    const auto t_gpu = std::chrono::steady_clock::now();
     // host: region growing + rectangles, frames over worker threads
     std::vector<fdl::FrameList> fl(static_cast<size_t>(batch));
     const int32_t *hidx = static_cast<const int32_t *>(c->h_idx.p);
@@ -1185,6 +1189,13 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     c->st_used.assign(static_cast<size_t>(n0), 0);
     fdl::detect_lines(rows, cols, *opts, fl.data(), batch, out_rects, rect_stride, out_counts, c->st_used.data(),
                       threads > 0 ? threads : default_line_threads());
+    if (timing) {
+        const auto t_end = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[fd_lsd_lines] batch %d: gpu+d2h %.3f ms, host %.3f ms, valid %lld\n", batch,
+                     std::chrono::duration<double, std::milli>(t_gpu - t_start).count(),
+                     std::chrono::duration<double, std::milli>(t_end - t_gpu).count(),
+                     static_cast<long long>(base[static_cast<size_t>(batch)]));
+    }
     if (n0 > 0) {
         c->st_idx.assign(fl[0].idx, fl[0].idx + n0);
         c->st_norm.assign(fl[0].norm, fl[0].norm + n0);

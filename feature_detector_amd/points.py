@@ -380,7 +380,7 @@ def lsd_lines(frames, needed: int = 1, min_norm: float = 20.0, tol_rad: float = 
     ctx = _resolve_ctx(ctx, frames)
     _bind_stream(ctx, on_dev)
     opts = _lib.fd_lsd_opts(float(min_norm), float(tol_rad), float(min_length), float(min_inlier))
-    out = np.zeros((b, max(max_lines, 1), _lib.LSD_RECT_FLOATS), np.float32)
+    out = np.empty((b, max(max_lines, 1), _lib.LSD_RECT_FLOATS), np.float32)
     cnt = np.zeros((b,), np.int32)
     rc = _lib.load().fd_lsd_lines(ctx.ptr, ctypes.c_void_p(ptr), 1 if on_dev else 0, b, r, c, ctypes.byref(opts),
                                   int(needed), ctypes.c_void_p(out.ctypes.data), int(max_lines),

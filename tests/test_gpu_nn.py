@@ -66,15 +66,16 @@ def test_nn_descriptors_matches_oracle(sp, oracle):
         assert not got[b, counts[b]:].any()
 
 
-def test_superpoint_end_to_end_device(sp, oracle):
+@pytest.mark.parametrize("rows,cols,n", [(240, 320, 3), (480, 640, 4)])  # 480x640: BASELINE configs[4]'s shape
+def test_superpoint_end_to_end_device(sp, oracle, rows, cols, n):
     """Random-weight SuperPoint on device frames: GPU selection + descriptors equal the oracle's
     post-processing of the very same network outputs."""
     torch = pytest.importorskip("torch")
-    det = sp.SuperPointDetector(sp.Options(kComputeDescriptors=True, kMaxImageRows=240, kMaxImageCols=320))
+    det = sp.SuperPointDetector(sp.Options(kComputeDescriptors=True, kMaxImageRows=rows, kMaxImageCols=cols))
     assert det.Initialize()
-    frames = torch.from_numpy(np.stack([oracle.make_frame("noise", 900 + i, 240, 320) for i in range(3)])).cuda()
+    frames = torch.from_numpy(np.stack([oracle.make_frame("noise", 900 + i, rows, cols) for i in range(n)])).cuda()
     xy2, cnt2, d2 = det.DetectGoodFeaturesWithDescriptor(frames)
-    assert tuple(xy2.shape) == (3, 241, 2) and tuple(d2.shape) == (3, 241, 256)
+    assert tuple(xy2.shape) == (n, 241, 2) and tuple(d2.shape) == (n, 241, 256)
     # the same post-processing on one network run (MIOpen may pick different algorithms per call)
     heat, desc = det.InferenceSession(frames)
     xy, cnt = sp.nn_select(heat, det.options())
@@ -83,7 +84,7 @@ def test_superpoint_end_to_end_device(sp, oracle):
     heat_h, desc_h = heat.float().cpu().numpy(), desc.float().cpu().numpy()
     cnt_h = cnt.cpu().numpy()
     assert cnt_h.min() > 0
-    for b in range(3):
+    for b in range(n):
         exp = oracle.nn_select(heat_h[b], 3, 15, 240, 0.1)
         got = features(xy, cnt, b)
         assert np.array_equal(got, exp)
