@@ -15,6 +15,7 @@ constexpr int kSelectChunk = 2048;      // candidates sorted per greedy chunk (L
 constexpr int kGridLdsCells = 16384;    // occupancy grid kept in LDS up to this many cells
 constexpr int kMaxOffsetSegs = 48;
 constexpr int kSegHead = 64;           // selection keys kept per sorted segment head (PointsArgs::seghead)
+constexpr int kWideKeys = 8192;        // keys per frame of k_select's wide first pass (SelectArgs::wide_keys)
 constexpr int kHistBins = 4096;         // level-0 digit of the selection key: top 12 bits of the mapped response
 
 // A raster-mode segment entry (fd_points_candidates only).
@@ -106,6 +107,7 @@ struct SelectArgs {
     const uint64_t *seghead;  // their first kSegHead selection keys (PointsArgs::seghead)
     uint32_t *seg_bad;      // [batch], reset by k_select
     int nseg;               // segments per frame
+    uint64_t *wide_keys;  // [batch][kWideKeys] scratch of the wide first pass, or null (one pass per chunk)
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 

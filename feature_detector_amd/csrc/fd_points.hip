@@ -19,7 +19,10 @@ namespace fdk {
 
 namespace {
 
-constexpr int kStage = 512;  // per-wave LDS staging of candidates (detect mode)
+// Per-wave LDS staging of candidates (detect mode). 508, not 512: with the few bytes of workgroup
+// flags the corner kernel's LDS is exactly 32 KiB, 5 workgroups per CU (160 KiB); at 512 it was 24
+// bytes over and only 4 fit.
+constexpr int kStage = FD_STAGE_CORNER;
 constexpr int kStageFast = FD_STAGE_FAST;  // FAST: fewer flushes (each drains the wave's stores)
 constexpr float kInvCnt = 1.0f / 9.0f;                  // 1 / (3*3)  (:71)
 constexpr float kInvCnt2 = (1.0f / 9.0f) * (1.0f / 9.0f);  // harris :72

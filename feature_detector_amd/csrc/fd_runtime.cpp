@@ -44,7 +44,7 @@ struct fd_ctx {
     // selection control block: [batch][kHistBins] level-0 histograms, then list_count per frame.
     // Zero between calls: k_select resets what a call used. sel_dirty marks a call whose kernels may
     // not have run to the end (the next call clears the block first).
-    DevBuf selctl, pre_keys, segdesc, seghead;
+    DevBuf selctl, pre_keys, wide_keys, segdesc, seghead;
     bool sel_dirty = true;
     DevBuf seg_cnt, seg, resp_map, c_resp, c_x, c_y, c_counts;
     DevBuf l_norm, l_angle, l_valid, l_cnt, l_base, l_idx, l_counts, l_bits;
@@ -334,7 +334,7 @@ int64_t detect_list_cap(int kind, int rows, int cols) {
 
 struct SelectBufs {
     uint32_t *hist0, *list_count, *pre_count, *seg_bad;
-    uint64_t *pre_keys;
+    uint64_t *pre_keys, *wide_keys;
     uint32_t *status, *cand_n;
 };
 
@@ -343,6 +343,7 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     FD_HIP_TRY(c, ensure(c, c->list_resp, sizeof(float) * cap * batch));
     FD_HIP_TRY(c, ensure(c, c->list_idx, sizeof(uint32_t) * cap * batch));
     FD_HIP_TRY(c, ensure(c, c->pre_keys, sizeof(uint64_t) * fdk::kSelectChunk * batch));
+    FD_HIP_TRY(c, ensure(c, c->wide_keys, sizeof(uint64_t) * fdk::kWideKeys * batch));
     const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 3);
     if (c->selctl.n < ctl) {
         FD_HIP_TRY(c, ensure(c, c->selctl, ctl));
@@ -358,6 +359,7 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     sb.pre_count = sb.list_count + batch;
     sb.seg_bad = sb.pre_count + batch;
     sb.pre_keys = as<uint64_t>(c->pre_keys);
+    sb.wide_keys = as<uint64_t>(c->wide_keys);
     FD_HIP_TRY(c, ensure(c, c->status, sizeof(uint32_t) * 2 * static_cast<size_t>(batch)));
     sb.status = as<uint32_t>(c->status);
     sb.cand_n = sb.status + batch;
@@ -537,6 +539,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.pre_count = sb.pre_count;
     s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
     s.seg_bad = sb.seg_bad;
+    s.wide_keys = std::getenv("FD_NO_WIDE") ? nullptr : sb.wide_keys;  // (A/B switch)
     if (q.segdesc && !s.pre_keys) {
         s.segdesc = q.segdesc;
         s.seghead = q.seghead;
@@ -565,6 +568,25 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         std::fprintf(stderr, "  fine:");
         for (int i = 16; i < 32; ++i) std::fprintf(stderr, " %llu", (unsigned long long)h[i]);
         std::fprintf(stderr, "\n");
+        if (batch > 1) {  // spread over the frames: the kernel lasts as long as its slowest frame
+            std::vector<uint64_t> all(static_cast<size_t>(batch) * 32);
+            FD_HIP_TRY(c, hipMemcpyAsync(all.data(), c->dbg.p, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost,
+                                         c->stream));
+            FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+            uint64_t mn = ~0ull, mx = 0, gmx = 0, grmx = 0;
+            int fmx = 0;
+            for (int b = 0; b < batch; ++b) {
+                const uint64_t *q = all.data() + static_cast<size_t>(b) * 32;
+                const uint64_t t = q[1] + q[2] + q[3] + q[4] + q[5] + q[6] + q[7];
+                if (t > mx) mx = t, fmx = b;
+                mn = std::min(mn, t);
+                gmx = std::max(gmx, q[3]);
+                grmx = std::max(grmx, q[5]);
+            }
+            std::fprintf(stderr, "  frames: total cycles min %llu max %llu (frame %d), max gather %llu, max greedy %llu\n",
+                         (unsigned long long)mn, (unsigned long long)mx, fmx, (unsigned long long)gmx,
+                         (unsigned long long)grmx);
+        }
     }
     if (c->tie_order == FD_TIES_REFERENCE && !q.tie_idx_desc) {
         const int rc = resolve_ties(c, s, batch, sb);
@@ -659,7 +681,7 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
                       &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
-                      &c->l_lnorm,  &c->l_langle, &c->l_fbase};
+                      &c->l_lnorm,  &c->l_langle, &c->l_fbase, &c->wide_keys};
     for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle}) release(*b);
     for (DevBuf *b : bufs) release(*b);
     if (c->xev) (void)hipEventDestroy(c->xev);

@@ -439,12 +439,26 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         __syncthreads();
         return L.ff_res[slot];
     };
+    // Wide scratch of the first list pass (see wide_gather below).
+    uint64_t *const wk = a.wide_keys ? a.wide_keys + static_cast<int64_t>(f) * kWideKeys : nullptr;
+    int wide_lo = kHistBins;  // level-0 bins >= wide_lo are in wk (when wide_n > 0)
+    uint32_t wide_n = 0;
+    auto in_wide = [&](uint64_t klo) { return wide_n > 0 && static_cast<int>(klo >> 52) >= wide_lo; };
     // Histogram of digit `lvl` (>= 1) over keys in [klo, khi] (one pass over the list).
     auto build = [&](int lvl, uint64_t klo, uint64_t khi, uint32_t *S) {
         const int nb = 1 << lvl_width(lvl);
         const int rem = 64 - lvl_top(lvl);
         for (int b = tid; b <= nb; b += nthr) S[b] = 0;
         __syncthreads();
+        if (in_wide(klo)) {  // the bin's keys are all in the wide scratch
+            for (uint32_t i = static_cast<uint32_t>(tid); i < wide_n; i += static_cast<uint32_t>(nthr)) {
+                const uint64_t sk = wk[i];
+                if (sk >= klo && sk <= khi) atomicAdd(&S[(sk >> rem) & static_cast<uint64_t>(nb - 1)], 1u);
+            }
+            __syncthreads();
+            suffix(S, nb);
+            return;
+        }
         for (int64_t b0 = tid; b0 < n; b0 += static_cast<int64_t>(kPassUnroll) * nthr) {
             float r[kPassUnroll];
             uint32_t ix[kPassUnroll];
@@ -537,6 +551,100 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         __syncthreads();  // sup complete; gcount read by every thread before anyone reuses it
     };
 
+    // Wide first pass (SelectArgs::wide_keys): the list pass that gathers the first chunk collects every
+    // key of the top level-0 bins holding <= kWideKeys candidates into the frame's global scratch, so
+    // that later chunks (and descents) inside those bins scan that scratch instead of the whole list:
+    // one pass over the list instead of one per chunk (FAST on noise visits ~5k candidates of ~265k,
+    // 3 chunks: 3 list passes of ~90k cycles each by this one workgroup before).
+    auto wide_gather = [&](uint32_t k32lo, const float *pre) {
+        if (tid == 0) gcount = 0;
+        __syncthreads();
+        const uint32_t nn = static_cast<uint32_t>(n);
+        const uint32_t step = static_cast<uint32_t>(nthr);
+        auto round = [&](const float (&rr)[kRegGather], uint32_t base) {
+            uint32_t hm = 0;
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) {
+                const bool hit = base + tid + k * step < nn && map_key32(rr[k], a) >= k32lo;
+                hm |= static_cast<uint32_t>(hit) << k;
+            }
+            uint32_t wtotal = 0;
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) wtotal += popc64(ballot((hm >> k) & 1u));
+            if (wtotal == 0) return;
+            uint32_t off = 0;
+            if (lane == 0) off = atomicAdd(&gcount, wtotal);
+            off = __builtin_amdgcn_readfirstlane(off);
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) {
+                const bool hit = (hm >> k) & 1u;
+                const uint64_t m = ballot(hit);
+                const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
+                if (hit && pos < static_cast<uint32_t>(kWideKeys))  // (response, list index); keyed below
+                    wk[pos] = (static_cast<uint64_t>(__float_as_uint(rr[k])) << 32) | (base + tid + k * step);
+                off += popc64(m);
+            }
+        };
+        uint32_t base = 0;
+        if (pre) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this thread's LDS-direct loads have landed
+            float rr[kRegGather];
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) rr[k] = pre[tid + k * step];
+            round(rr, 0);
+            base = kRegGather * step;
+        }
+        for (; base < nn; base += kRegGather * step) {
+            float rr[kRegGather];
+#pragma unroll
+            for (int k = 0; k < kRegGather; ++k) rr[k] = lresp[min(base + tid + k * step, nn - 1u)];
+            round(rr, base);
+        }
+        // Staged entries -> selection keys: the pixel indices are fetched here, all at once, rather
+        // than per hit inside the pass (a dependent load per round).
+        __threadfence_block();  // the scratch is read back by other threads of this workgroup
+        __syncthreads();
+        const uint32_t staged = min(gcount, static_cast<uint32_t>(kWideKeys));
+        constexpr int kPer = (kWideKeys + kSelectThreads - 1) / kSelectThreads;
+        uint64_t e[kPer];
+        uint32_t li[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {  // independent loads: one latency for the whole conversion
+            const uint32_t i = static_cast<uint32_t>(tid) + k * step;
+            e[k] = i < staged ? wk[i] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t i = static_cast<uint32_t>(tid) + k * step;
+            li[k] = i < staged ? lidx[static_cast<uint32_t>(e[k])] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t i = static_cast<uint32_t>(tid) + k * step;
+            if (i < staged) wk[i] = make_key(__uint_as_float(static_cast<uint32_t>(e[k] >> 32)), li[k], a);
+        }
+        __threadfence_block();
+        __syncthreads();
+    };
+    // Keys of wk in [klo, khi] into sup (unordered); gcount = their number.
+    auto wide_pick = [&](uint64_t klo, uint64_t khi) {
+        if (tid == 0) gcount = 0;
+        __syncthreads();
+        for (uint32_t i0 = static_cast<uint32_t>(wave) * kWave; i0 < wide_n; i0 += static_cast<uint32_t>(nthr)) {
+            const uint32_t i = i0 + lane;
+            const uint64_t key = i < wide_n ? wk[i] : 0ull;
+            const bool hit = i < wide_n && key >= klo && key <= khi;
+            const uint64_t m = ballot(hit);
+            if (m) {
+                uint32_t off = 0;
+                if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
+                off = __builtin_amdgcn_readfirstlane(off);
+                const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
+                if (hit && pos < static_cast<uint32_t>(kSelectChunk)) sup[pos] = key;
+            }
+        }
+        __syncthreads();
+    };
     // First chunk from the sorted segments (PointsArgs::segdesc): every workgroup segment of the list
     // is ordered by level-0 bin, descending, so the keys of bins >= lo are a prefix of each segment.
     // T threads per segment read its entries T at a time while the last one read is still >= lo.
@@ -618,6 +726,17 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 __syncthreads();
             } else if (seg_mode && seg_bad == 0) {
                 seg_gather(lo_b);
+            } else if (wk) {
+                if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
+                    atomicOr(&a.status[f], 0x02000000u);
+                // the top bins holding <= kWideKeys keys (a superset of the first chunk's), one pass
+                const int wl = first_le(suf0, 0, lo_b + 1, 0u, static_cast<uint32_t>(kWideKeys));
+                wide_gather(static_cast<uint32_t>(wl) << 20, (a.pre_keys || seg_mode) ? nullptr : pre_lds);
+                if (tid == 0 && gcount != suf0[wl])  // consistency guard: gathered == histogram count
+                    atomicOr(&a.status[f], 0x04000000u);
+                wide_lo = wl;
+                wide_n = min(suf0[wl], static_cast<uint32_t>(kWideKeys));
+                wide_pick(static_cast<uint64_t>(lo_b) << 52, ~0ull);
             } else {
                 if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
                     atomicOr(&a.status[f], 0x02000000u);
@@ -694,8 +813,11 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             if (first_ready && level == 0) {  // gathered before the loop (sup holds it)
                 first_ready = false;
                 if (tid == 0) gcount = cnt;
+            } else if (in_wide(klo)) {
+                wide_pick(klo, khi);
             } else if (k32_exact) {
-                gather_exact(k32lo, k32hi, nullptr);            } else
+                gather_exact(k32lo, k32hi, nullptr);
+            } else
             for (int64_t b0 = static_cast<int64_t>(wave) * kWave; b0 < n;
                  b0 += static_cast<int64_t>(kPassUnroll) * nthr) {
                 float r[kPassUnroll];
