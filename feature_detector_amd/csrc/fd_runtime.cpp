@@ -18,6 +18,7 @@
 #include "fd_hip.h"
 #include "fd_kernels.h"
 #include "fd_lines.h"
+#include "fd_png.h"
 
 namespace {
 
@@ -61,6 +62,8 @@ struct fd_ctx {
     // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
     DevBuf l_lnorm, l_langle, l_fbase;
     HostBuf h_idx, h_norm, h_angle;
+    HostBuf h_png;  // fd_png_frames: decoded samples of a batch (pinned)
+    DevBuf d_png;
     std::vector<int32_t> st_idx;
     std::vector<float> st_norm, st_angle;
     std::vector<uint8_t> st_used;
@@ -682,7 +685,8 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
                       &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
                       &c->l_lnorm,  &c->l_langle, &c->l_fbase, &c->wide_keys};
-    for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle}) release(*b);
+    for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle, &c->h_png}) release(*b);
+    release(c->d_png);
     for (DevBuf *b : bufs) release(*b);
     if (c->xev) (void)hipEventDestroy(c->xev);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -1238,6 +1242,72 @@ int fd_lsd_lines_state(fd_ctx *c, int32_t *idx, float *norm, float *angle, uint8
         angle[k] = c->st_angle[static_cast<size_t>(k)];
         used[k] = c->st_used[static_cast<size_t>(k)];
     }
+    return FD_OK;
+}
+
+int fd_png_info(const uint8_t *png, size_t len, int32_t *rows, int32_t *cols, int32_t *channels) {
+    fdp::PngInfo in;
+    if (fdp::png_info(png, len, in) != fdp::kPngOk) return FD_ERR_INVALID;
+    if (rows) *rows = in.rows;
+    if (cols) *cols = in.cols;
+    if (channels) *channels = in.channels;
+    return FD_OK;
+}
+
+int fd_png_decode(const uint8_t *png, size_t len, uint8_t *out_gray, size_t cap, int32_t *rows, int32_t *cols) {
+    fdp::PngInfo in;
+    if (fdp::png_info(png, len, in) != fdp::kPngOk) return FD_ERR_INVALID;
+    if (rows) *rows = in.rows;
+    if (cols) *cols = in.cols;
+    const size_t npx = static_cast<size_t>(in.rows) * in.cols;
+    if (!out_gray || cap < npx) return FD_ERR_CAPACITY;
+    std::vector<uint8_t> samples(npx * in.channels);
+    const int rc = fdp::png_decode(png, len, samples.data(), samples.size(), in);
+    if (rc == fdp::kPngCapacity) return FD_ERR_CAPACITY;
+    if (rc) return FD_ERR_INVALID;
+    const int ch = in.channels;
+    for (size_t i = 0; i < npx; ++i) {  // the same conversion as k_rgb_gray (fd_gray.hip)
+        const uint8_t *p = samples.data() + i * ch;
+        out_gray[i] = ch <= 2 ? p[0]
+                              : static_cast<uint8_t>((4899u * p[0] + 9617u * p[1] + 1868u * p[2] + 8192u) >> 14);
+    }
+    return FD_OK;
+}
+
+int fd_png_frames(fd_ctx *c, const uint8_t *const *pngs, const size_t *lens, int n, int rows, int cols,
+                  uint8_t *frames_device, int threads) {
+    if (!c) return FD_ERR_INVALID;
+    if (n < 1 || rows < 1 || cols < 1 || !pngs || !lens || !frames_device) return fail(c, FD_ERR_INVALID, "bad arguments");
+    // every image must have the batch geometry; its channel count sets the staging layout (all equal)
+    int channels = 0;
+    for (int i = 0; i < n; ++i) {
+        fdp::PngInfo in;
+        if (fdp::png_info(pngs[i], lens[i], in) != fdp::kPngOk)
+            return fail(c, FD_ERR_INVALID, "image " + std::to_string(i) + ": not a supported PNG");
+        if (in.rows != rows || in.cols != cols)
+            return fail(c, FD_ERR_INVALID, "image " + std::to_string(i) + ": size differs from the batch");
+        if (i > 0 && in.channels != channels)
+            return fail(c, FD_ERR_INVALID, "image " + std::to_string(i) + ": channel count differs from the batch");
+        channels = in.channels;
+    }
+    const size_t per = static_cast<size_t>(rows) * cols * channels;
+    if (per * n >= (size_t(1) << 32)) return fail(c, FD_ERR_INVALID, "batch too large (samples >= 4 GiB)");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    // the previous call's upload may still read the pinned staging: wait for the stream first
+    FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+    FD_HIP_TRY(c, ensure_host(c->h_png, per * n));
+    std::vector<fdp::PngInfo> infos(static_cast<size_t>(n));
+    const int rc = fdp::png_decode_batch(pngs, lens, n, static_cast<uint8_t *>(c->h_png.p), per, infos.data(),
+                                         threads > 0 ? threads : default_line_threads());
+    if (rc) return fail(c, rc == fdp::kPngCapacity ? FD_ERR_CAPACITY : FD_ERR_INVALID, "PNG decode failed");
+    uint8_t *src = frames_device;  // gray input: straight into the frames
+    if (channels != 1) {
+        FD_HIP_TRY(c, ensure(c, c->d_png, per * n));
+        src = as<uint8_t>(c->d_png);
+    }
+    FD_HIP_TRY(c, hipMemcpyAsync(src, c->h_png.p, per * n, hipMemcpyHostToDevice, c->stream));
+    if (channels != 1)
+        FD_HIP_TRY(c, fdk::launch_rgb_gray(src, channels, frames_device, static_cast<int64_t>(rows) * cols * n, c->stream));
     return FD_OK;
 }
 

@@ -65,3 +65,51 @@ class Ingest:
             self.close()
         except Exception:
             pass
+
+
+# ------------------------------------------------------------------------------ PNG front end (f4)
+def png_info(data: bytes):
+    """(rows, cols, channels) of a PNG stream (fd_png_info)."""
+    L = _lib.load()
+    r, c, ch = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    rc = L.fd_png_info(data, len(data), ctypes.byref(r), ctypes.byref(c), ctypes.byref(ch))
+    if rc:
+        raise _lib.FdError(rc, "not a supported PNG (8-bit gray / gray+alpha / RGB / RGBA, no interlace)")
+    return r.value, c.value, ch.value
+
+
+def load_png(path_or_bytes) -> np.ndarray:
+    """One PNG as a gray u8 image [rows, cols] (fd_png_decode): what the reference's
+    Visualizor2D::LoadImage hands DetectGoodFeatures (colour -> gray: BT.601 fixed point, unpinned)."""
+    data = bytes(path_or_bytes) if isinstance(path_or_bytes, (bytes, bytearray)) else open(path_or_bytes, "rb").read()
+    rows, cols, _ = png_info(data)
+    out = np.empty((rows, cols), np.uint8)
+    r, c = ctypes.c_int32(), ctypes.c_int32()
+    rc = _lib.load().fd_png_decode(data, len(data), ctypes.c_void_p(out.ctypes.data), out.size, ctypes.byref(r),
+                                   ctypes.byref(c))
+    if rc:
+        raise _lib.FdError(rc, "PNG decode failed")
+    return out
+
+
+def png_frames(images, threads: int = 0, ctx: Context | None = None, out=None):
+    """A batch of same-size PNG streams (bytes) -> device gray frames, a torch uint8 tensor
+    [n, rows, cols] on the context's device (fd_png_frames: host decode threads, one upload, colour ->
+    gray on the GPU), stream-ordered on torch's current stream."""
+    import torch
+
+    from .points import _bind_stream, default_context
+
+    images = [bytes(x) for x in images]
+    rows, cols, _ = png_info(images[0])
+    ctx = ctx or default_context(torch.cuda.current_device())
+    _bind_stream(ctx, True)
+    n = len(images)
+    if out is None:
+        out = torch.empty((n, rows, cols), dtype=torch.uint8, device=f"cuda:{ctx.device}")
+    bufs = (ctypes.c_char_p * n)(*images)
+    lens = (ctypes.c_size_t * n)(*[len(x) for x in images])
+    rc = _lib.load().fd_png_frames(ctx.ptr, ctypes.cast(bufs, ctypes.c_void_p), ctypes.cast(lens, ctypes.c_void_p), n,
+                                   rows, cols, ctypes.c_void_p(out.data_ptr()), int(threads))
+    _lib.check(ctx.ptr, rc)
+    return out

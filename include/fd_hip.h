@@ -20,6 +20,7 @@
 #ifndef FD_HIP_H_
 #define FD_HIP_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -209,6 +210,26 @@ int fd_lsd_lines(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int b
  * norm, angle) and each one's final is_used flag. n receives the count; at most cap are written.
  */
 int fd_lsd_lines_state(fd_ctx *ctx, int32_t *idx, float *norm, float *angle, uint8_t *used, int64_t cap, int64_t *n);
+
+/* ---- ingest front end: PNG frames ----------------------------------------------------------------- */
+/*
+ * The reference loads frames with Visualizor2D::LoadImage (test/test_feature_point_detector.cpp:104,
+ * un-vendored). PNG files with 8-bit samples, colour type gray / gray+alpha / RGB / RGBA, no interlace.
+ * Colour becomes gray as (4899 R + 9617 G + 1868 B + 8192) >> 14 (BT.601; the reference's conversion
+ * is parity-unpinned); alpha is dropped. Errors: FD_ERR_INVALID (not a PNG, corrupt or
+ * unsupported variant), FD_ERR_CAPACITY (output too small).
+ *
+ * fd_png_info   -- geometry of one PNG (no context, no GPU).
+ * fd_png_decode -- one PNG to a host gray image (host decode; the C++ loader uses it).
+ * fd_png_frames -- a batch of same-size PNGs to device gray frames [n][rows][cols] (the layout
+ *                  fd_points_detect / fd_lsd_lines take): zlib inflate + PNG row filters on `threads`
+ *                  host threads (<= 0: all, capped by OMP_NUM_THREADS) into pinned memory, one H2D copy,
+ *                  colour -> gray on the GPU, stream-ordered on the context stream.
+ */
+int fd_png_info(const uint8_t *png, size_t len, int32_t *rows, int32_t *cols, int32_t *channels);
+int fd_png_decode(const uint8_t *png, size_t len, uint8_t *out_gray, size_t cap, int32_t *rows, int32_t *cols);
+int fd_png_frames(fd_ctx *ctx, const uint8_t *const *pngs, const size_t *lens, int n, int rows, int cols,
+                  uint8_t *frames_device, int threads);
 
 /* ---- steered BRIEF descriptor ------------------------------------------------------------------- */
 /* BriefDescriptor::Options (descriptor_brief.h:17-20) plus the float-coordinate sampler of the

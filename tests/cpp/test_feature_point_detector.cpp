@@ -2,12 +2,14 @@
 // detector calls with the same options, compiled against the drop-in API (include/feature_detector),
 // minus the visualisation. Prints one JSON object per test to stdout.
 //   usage: fd_demo_points <raw u8 gray file> <rows> <cols> [need]
+//          fd_demo_points <image.png> [need]      (LoadImage, as the reference demo does at :104)
 #include <cstdio>
 #include <cstdlib>
 #include <string>
 #include <vector>
 
 #include "feature_detector/feature_point_detector.h"
+#include "feature_detector/image_io.h"
 
 using namespace feature_detector;
 
@@ -65,20 +67,31 @@ void TestFastFeatureDetector(GrayImage &image, int32_t feature_num_need) {  // :
 }
 
 int main(int argc, char **argv) {
-    if (argc < 4) {
-        std::fprintf(stderr, "usage: %s <raw u8 file> <rows> <cols> [need]\n", argv[0]);
-        return 2;
+    GrayImage image;
+    int32_t feature_num_need = 200;  // :101
+    const std::string path = argc > 1 ? argv[1] : "";
+    if (path.size() > 4 && path.compare(path.size() - 4, 4, ".png") == 0) {
+        if (!LoadImage(path, image)) {  // :103-104
+            std::fprintf(stderr, "cannot load %s\n", argv[1]);
+            return 2;
+        }
+        if (argc > 2) feature_num_need = std::atoi(argv[2]);
+    } else {
+        if (argc < 4) {
+            std::fprintf(stderr, "usage: %s <raw u8 file> <rows> <cols> [need] | <image.png> [need]\n", argv[0]);
+            return 2;
+        }
+        const int rows = std::atoi(argv[2]), cols = std::atoi(argv[3]);
+        if (argc > 4) feature_num_need = std::atoi(argv[4]);
+        uint8_t *buf = static_cast<uint8_t *>(std::malloc(static_cast<size_t>(rows) * cols));
+        FILE *f = std::fopen(argv[1], "rb");
+        if (!f || std::fread(buf, 1, static_cast<size_t>(rows) * cols, f) != static_cast<size_t>(rows) * cols) {
+            std::fprintf(stderr, "cannot read %s\n", argv[1]);
+            return 2;
+        }
+        std::fclose(f);
+        image.SetImage(buf, rows, cols, true);
     }
-    const int rows = std::atoi(argv[2]), cols = std::atoi(argv[3]);
-    const int32_t feature_num_need = argc > 4 ? std::atoi(argv[4]) : 200;  // :101
-    uint8_t *buf = static_cast<uint8_t *>(std::malloc(static_cast<size_t>(rows) * cols));
-    FILE *f = std::fopen(argv[1], "rb");
-    if (!f || std::fread(buf, 1, static_cast<size_t>(rows) * cols, f) != static_cast<size_t>(rows) * cols) {
-        std::fprintf(stderr, "cannot read %s\n", argv[1]);
-        return 2;
-    }
-    std::fclose(f);
-    GrayImage image(buf, rows, cols, true);
 
     TestFastFeatureDetector(image, feature_num_need);  // :106-109
     TestHarrisFeatureDetector(image, feature_num_need);
