@@ -5,6 +5,8 @@ fixed number of times, on seeded uniform-noise frames generated on the GPU.
   --shape northstar  fd_points_response (per-pixel kernel alone), 1920x1080 batch 256, 10 calls
                      (--kind shi_tomasi by default: the north-star kernel)
   --shape fast720    fd_points_detect, FAST, 1280x720 batch 64 (BASELINE configs[2]), 10 calls
+  --shape lsd        fd_lsd_map (dense) and fd_lsd_lines (compact map + host stage), 1920x1080 batch 256,
+                     64-px checker + noise (BASELINE configs[3]), 3 calls each
 """
 import argparse
 import os
@@ -17,7 +19,7 @@ import feature_detector_amd as fd  # noqa: E402
 
 THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 p = argparse.ArgumentParser()
-p.add_argument("--shape", default="bench", choices=["bench", "northstar", "fast720"])
+p.add_argument("--shape", default="bench", choices=["bench", "northstar", "fast720", "lsd"])
 p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast"])
 p.add_argument("--calls", type=int, default=0)
 a = p.parse_args()
@@ -42,6 +44,16 @@ elif a.shape == "northstar":
            torch.empty((256, cap), dtype=torch.int32, device="cuda"), torch.empty((256,), dtype=torch.int32, device="cuda"))
     for _ in range(a.calls or 10):
         fd.point_response(kind, frames, THR[kind], out=out)
+elif a.shape == "lsd":
+    kind = "lsd"
+    rows, cols, n = 1080, 1920, 256
+    r = torch.arange(rows, device="cuda").view(1, rows, 1) // 64
+    c = torch.arange(cols, device="cuda").view(1, 1, cols) // 64
+    base = torch.where(((r + c) % 2) == 1, 180, 60)
+    frames = (base + torch.randint(-10, 11, (n, rows, cols), generator=g, device="cuda", dtype=torch.int32)).clamp(0, 255).to(torch.uint8)
+    for _ in range(a.calls or 3):
+        fd.lsd_map(frames)
+        fd.lsd_lines(frames, max_lines=2048)
 else:
     kind = a.kind or "fast"
     frames = noise(64, 720, 1280)
