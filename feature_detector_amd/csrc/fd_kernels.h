@@ -107,7 +107,8 @@ struct SelectArgs {
     const uint64_t *seghead;  // their first kSegHead selection keys (PointsArgs::seghead)
     uint32_t *seg_bad;      // [batch], reset by k_select
     int nseg;               // segments per frame
-    uint64_t *wide_keys;  // [batch][kWideKeys] scratch of the wide first pass, or null (one pass per chunk)
+    uint64_t *wide_keys;  // [batch][kWideKeys] scratch of the wide pass, or null (one list pass per chunk)
+    int wide_eager;       // wide pass with the first chunk (FAST) instead of at the first later list pass
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 

@@ -396,6 +396,7 @@ struct SelectCall {
     uint32_t key_base = 0;
     int key_lz = 0;
     int tie_idx_desc = 0;  // equal responses: raster index descending (SuperPoint multimap) instead of ascending
+    bool wide_eager = false;  // FAST: the wide pass comes with the first chunk (SelectArgs::wide_eager)
     bool value_flag = false;  // the candidate kernel flags out-of-range values in pre_count (gather kernel off)
     const uint2 *segdesc = nullptr;  // sorted segments of the candidate kernel (PointsArgs::segdesc)
     const uint64_t *seghead = nullptr;
@@ -543,6 +544,10 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
     s.seg_bad = sb.seg_bad;
     s.wide_keys = std::getenv("FD_NO_WIDE") ? nullptr : sb.wide_keys;  // (A/B switch)
+    // FAST's top responses are scores plus a slowly growing offset: thousands of candidates share the
+    // top bins and the greedy scan runs over several chunks (1280x720 noise: ~5k), so the wide pass
+    // comes with the first chunk; the corner detectors usually finish within it (wide pass deferred).
+    s.wide_eager = q.wide_eager ? 1 : 0;
     if (q.segdesc && !s.pre_keys) {
         s.segdesc = q.segdesc;
         s.seghead = q.seghead;
@@ -883,6 +888,7 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     sc.segdesc = a.segdesc;
     sc.seghead = a.seghead;
     sc.nseg = g.blocks_per_frame;
+    sc.wide_eager = kind == FD_FAST;
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
 }
 

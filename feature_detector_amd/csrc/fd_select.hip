@@ -297,7 +297,7 @@ struct alignas(16) SelectLds {
     uint64_t st[32];  // diagnostic phase clocks (a.stamps only); 16..31 free for ad-hoc probes
 };
 
-template <int NT>
+template <int NT, bool WIDE>
 __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, SelectLds &L) {
     constexpr int kHistPerThread = kHistBins / NT;
     static_assert(kHistBins % NT == 0 && NT <= kSelectThreads, "histogram bins per thread");
@@ -440,10 +440,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         return L.ff_res[slot];
     };
     // Wide scratch of the first list pass (see wide_gather below).
-    uint64_t *const wk = a.wide_keys ? a.wide_keys + static_cast<int64_t>(f) * kWideKeys : nullptr;
-    int wide_lo = kHistBins;  // level-0 bins >= wide_lo are in wk (when wide_n > 0)
+    // (WIDE = false: the code below folds away -- small frames in sorted-segment mode never need it,
+    // and it would cost the hot small-frame path registers)
+    uint64_t *const wk = (WIDE && a.wide_keys) ? a.wide_keys + static_cast<int64_t>(f) * kWideKeys : nullptr;
+    int wide_lo = kHistBins, wide_hi = -1;  // level-0 bins [wide_lo, wide_hi] are in wk (when wide_n > 0)
     uint32_t wide_n = 0;
-    auto in_wide = [&](uint64_t klo) { return wide_n > 0 && static_cast<int>(klo >> 52) >= wide_lo; };
+    auto in_wide = [&](uint64_t klo) {
+        const int b = static_cast<int>(klo >> 52);
+        return wide_n > 0 && b >= wide_lo && b <= wide_hi;
+    };
     // Histogram of digit `lvl` (>= 1) over keys in [klo, khi] (one pass over the list).
     auto build = [&](int lvl, uint64_t klo, uint64_t khi, uint32_t *S) {
         const int nb = 1 << lvl_width(lvl);
@@ -556,27 +561,31 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // that later chunks (and descents) inside those bins scan that scratch instead of the whole list:
     // one pass over the list instead of one per chunk (FAST on noise visits ~5k candidates of ~265k,
     // 3 chunks: 3 list passes of ~90k cycles each by this one workgroup before).
-    auto wide_gather = [&](uint32_t k32lo, const float *pre) {
+    auto wide_gather = [&](uint32_t k32lo, uint32_t k32hi) {
         if (tid == 0) gcount = 0;
         __syncthreads();
         const uint32_t nn = static_cast<uint32_t>(n);
         const uint32_t step = static_cast<uint32_t>(nthr);
-        auto round = [&](const float (&rr)[kRegGather], uint32_t base) {
+        constexpr int kWideReg = 8;  // (half of gather_exact's round: the pass is not latency-critical)
+        for (uint32_t base = 0; base < nn; base += kWideReg * step) {
+            float rr[kWideReg];
+#pragma unroll
+            for (int k = 0; k < kWideReg; ++k) rr[k] = lresp[min(base + tid + k * step, nn - 1u)];
             uint32_t hm = 0;
 #pragma unroll
-            for (int k = 0; k < kRegGather; ++k) {
-                const bool hit = base + tid + k * step < nn && map_key32(rr[k], a) >= k32lo;
-                hm |= static_cast<uint32_t>(hit) << k;
+            for (int k = 0; k < kWideReg; ++k) {
+                const uint32_t k32 = map_key32(rr[k], a);
+                hm |= static_cast<uint32_t>(base + tid + k * step < nn && k32 >= k32lo && k32 <= k32hi) << k;
             }
             uint32_t wtotal = 0;
 #pragma unroll
-            for (int k = 0; k < kRegGather; ++k) wtotal += popc64(ballot((hm >> k) & 1u));
-            if (wtotal == 0) return;
+            for (int k = 0; k < kWideReg; ++k) wtotal += popc64(ballot((hm >> k) & 1u));
+            if (wtotal == 0) continue;
             uint32_t off = 0;
             if (lane == 0) off = atomicAdd(&gcount, wtotal);
             off = __builtin_amdgcn_readfirstlane(off);
 #pragma unroll
-            for (int k = 0; k < kRegGather; ++k) {
+            for (int k = 0; k < kWideReg; ++k) {
                 const bool hit = (hm >> k) & 1u;
                 const uint64_t m = ballot(hit);
                 const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
@@ -584,44 +593,24 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     wk[pos] = (static_cast<uint64_t>(__float_as_uint(rr[k])) << 32) | (base + tid + k * step);
                 off += popc64(m);
             }
-        };
-        uint32_t base = 0;
-        if (pre) {
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this thread's LDS-direct loads have landed
-            float rr[kRegGather];
-#pragma unroll
-            for (int k = 0; k < kRegGather; ++k) rr[k] = pre[tid + k * step];
-            round(rr, 0);
-            base = kRegGather * step;
         }
-        for (; base < nn; base += kRegGather * step) {
-            float rr[kRegGather];
-#pragma unroll
-            for (int k = 0; k < kRegGather; ++k) rr[k] = lresp[min(base + tid + k * step, nn - 1u)];
-            round(rr, base);
-        }
-        // Staged entries -> selection keys: the pixel indices are fetched here, all at once, rather
-        // than per hit inside the pass (a dependent load per round).
+        // staged entries -> selection keys: pixel indices fetched a few at a time per thread (independent
+        // loads), not per hit inside the pass
         __threadfence_block();  // the scratch is read back by other threads of this workgroup
         __syncthreads();
         const uint32_t staged = min(gcount, static_cast<uint32_t>(kWideKeys));
-        constexpr int kPer = (kWideKeys + kSelectThreads - 1) / kSelectThreads;
-        uint64_t e[kPer];
-        uint32_t li[kPer];
+        constexpr int kPer = 2;
+        for (uint32_t i0 = static_cast<uint32_t>(tid); i0 < staged; i0 += kPer * step) {
+            uint64_t e[kPer];
+            uint32_t li[kPer];
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {  // independent loads: one latency for the whole conversion
-            const uint32_t i = static_cast<uint32_t>(tid) + k * step;
-            e[k] = i < staged ? wk[i] : 0ull;
-        }
+            for (int k = 0; k < kPer; ++k) e[k] = i0 + k * step < staged ? wk[i0 + k * step] : 0ull;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const uint32_t i = static_cast<uint32_t>(tid) + k * step;
-            li[k] = i < staged ? lidx[static_cast<uint32_t>(e[k])] : 0u;
-        }
+            for (int k = 0; k < kPer; ++k) li[k] = i0 + k * step < staged ? lidx[static_cast<uint32_t>(e[k])] : 0u;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const uint32_t i = static_cast<uint32_t>(tid) + k * step;
-            if (i < staged) wk[i] = make_key(__uint_as_float(static_cast<uint32_t>(e[k] >> 32)), li[k], a);
+            for (int k = 0; k < kPer; ++k)
+                if (i0 + k * step < staged)
+                    wk[i0 + k * step] = make_key(__uint_as_float(static_cast<uint32_t>(e[k] >> 32)), li[k], a);
         }
         __threadfence_block();
         __syncthreads();
@@ -645,6 +634,23 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         }
         __syncthreads();
     };
+    // Level-0 bins at and below `hi` (the highest not yet visited), as many as hold <= kWideKeys keys,
+    // gathered in one list pass -- done at the first list pass the scan needs after its first chunk
+    // (a frame that finishes within the first chunk never pays for it).
+    auto ensure_wide = [&](int hi_bin) {
+        if (!wk || wide_n > 0) return;
+        const int wl = first_le(suf0, 0, hi_bin + 1, suf0[hi_bin + 1], static_cast<uint32_t>(kWideKeys));
+        if (wl > hi_bin) return;  // the bin alone holds more than kWideKeys keys
+        const uint32_t k32hi = hi_bin == kHistBins - 1 ? 0xFFFFFFFFu : (static_cast<uint32_t>(hi_bin + 1) << 20) - 1u;
+        wide_gather(static_cast<uint32_t>(wl) << 20, k32hi);
+        const uint32_t expect = suf0[wl] - suf0[hi_bin + 1];
+        if (tid == 0 && gcount != expect)  // consistency guard: gathered == histogram count
+            atomicOr(&a.status[f], 0x04000000u);
+        wide_lo = wl;
+        wide_hi = hi_bin;
+        wide_n = min(expect, static_cast<uint32_t>(kWideKeys));
+    };
+
     // First chunk from the sorted segments (PointsArgs::segdesc): every workgroup segment of the list
     // is ordered by level-0 bin, descending, so the keys of bins >= lo are a prefix of each segment.
     // T threads per segment read its entries T at a time while the last one read is still >= lo.
@@ -726,17 +732,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 __syncthreads();
             } else if (seg_mode && seg_bad == 0) {
                 seg_gather(lo_b);
-            } else if (wk) {
-                if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
-                    atomicOr(&a.status[f], 0x02000000u);
-                // the top bins holding <= kWideKeys keys (a superset of the first chunk's), one pass
-                const int wl = first_le(suf0, 0, lo_b + 1, 0u, static_cast<uint32_t>(kWideKeys));
-                wide_gather(static_cast<uint32_t>(wl) << 20, (a.pre_keys || seg_mode) ? nullptr : pre_lds);
-                if (tid == 0 && gcount != suf0[wl])  // consistency guard: gathered == histogram count
-                    atomicOr(&a.status[f], 0x04000000u);
-                wide_lo = wl;
-                wide_n = min(suf0[wl], static_cast<uint32_t>(kWideKeys));
-                wide_pick(static_cast<uint64_t>(lo_b) << 52, ~0ull);
+            } else if (wk && a.wide_eager) {
+                // long scans expected (FAST: scores plus a slowly growing offset crowd the top bins):
+                // the first list pass already collects the bins below the first chunk
+                ensure_wide(kHistBins - 1);
+                if (wide_n > 0 && wide_lo <= lo_b) {
+                    wide_pick(static_cast<uint64_t>(lo_b) << 52, ~0ull);
+                } else {
+                    gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, nullptr);
+                }
             } else {
                 if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
                     atomicOr(&a.status[f], 0x02000000u);
@@ -790,6 +794,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             const uint64_t klo = ((pre << w) | static_cast<uint64_t>(hi)) << rem;
             const uint64_t khi = klo | ((1ull << rem) - 1ull);
             const uint32_t expect = S[hi] - S[hi + 1];
+            if (level == 0) ensure_wide(hi);
             ++level;
             FD_COUNT(9, 1);
             FD_STAMP(7);
@@ -813,6 +818,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             if (first_ready && level == 0) {  // gathered before the loop (sup holds it)
                 first_ready = false;
                 if (tid == 0) gcount = cnt;
+            } else if (level == 0 && (ensure_wide(hi), in_wide(klo))) {
+                wide_pick(klo, khi);
             } else if (in_wide(klo)) {
                 wide_pick(klo, khi);
             } else if (k32_exact) {
@@ -1054,11 +1061,11 @@ __global__ __launch_bounds__(1024) void k_gather(SelectArgs a) {
     gather_first_chunk<1024>(v, g, G, L);
 }
 
-template <int NT>
+template <int NT, bool WIDE>
 __global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
     __shared__ SelectLds L;
     const int f = blockIdx.x;
-    select_frame<NT>(a, f, L);
+    select_frame<NT, WIDE>(a, f, L);
     finish_frame(a, f);
 }
 
@@ -1155,7 +1162,12 @@ hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_select<kSelectThreads>, dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
+    // the wide pass (k_select<.., true>) for FAST and for list mode; the corner detectors' small frames
+    // (sorted segments) keep the leaner instance
+    if (a.wide_keys && (a.wide_eager || !a.segdesc))
+        hipLaunchKernelGGL((k_select<kSelectThreads, true>), dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_select<kSelectThreads, false>), dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
     return hipGetLastError();
 }
 
