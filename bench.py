@@ -12,7 +12,7 @@ batch (weak scaling) with no collective on the data path; only the timing barrie
 the process group. value = pixels processed by all ranks / max-over-ranks time.
 
 Also reported: the roofline of the per-pixel kernel (HIP-event timed, algorithmic bytes = 1 B/px of
-frame input; traffic = measured FETCH_SIZE from profiles/r01_traffic.json), the north-star shape
+frame input; traffic = measured FETCH_SIZE from profiles/r02_traffic.json), the north-star shape
 (Shi-Tomasi 1920x1080 batch 256), and the CPU baseline (the oracle restatement on a bounded sample of
 the same workload: single thread, and a pool of up to 16 threads).
 """
@@ -37,8 +37,25 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level param
 MFMA_PEAK_TFLOPS_FP16 = 2500.0  # dense BF16/FP16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)
 # HBM traffic per launch measured with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) and
 # corrected by the calibrated gfx950 factor (tools/gpu_traffic.sh, tools/calib/fetch_calib.hip).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r01_traffic.json")
-VALU_FILE = "profiles/r01_k1_northstar_st_pmc_sq.csv"
+# (tools/gpu_round_pmc.sh + tools/make_round_profiles.py write both files)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
+SQ_FILE = os.path.join(ROOT, "profiles", "r02_sq.json")
+
+
+def north_star_issue():
+    """What bounds the north-star kernel, from the committed SQ counter pass (None if absent)."""
+    try:
+        with open(SQ_FILE) as fh:
+            q = json.load(fh)["ns_sq"]
+    except (OSError, KeyError, ValueError):
+        return None
+    return {"source": os.path.relpath(SQ_FILE, ROOT),
+            "simd_valu_utilisation": q["simd_valu_utilisation"],
+            "waves_resident_per_simd": q["waves_resident_per_simd"],
+            "wave_time_issue_stalled": q["wave_time_issue_stalled"],
+            "note": ("neither HBM nor VALU issue saturates: SIMD VALU utilisation = SQ_INSTS_VALU x 2 cycles / "
+                     "(1024 SIMDs x kernel cycles); the rest is dependency latency at ~3 resident waves per SIMD "
+                     "(LDS-limited occupancy) -- DESIGN.md section 4")}
 
 
 def measured_traffic(key):
@@ -712,9 +729,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb,
                          "traffic": measured_traffic("northstar_k_corner")[0]},
-            "valu_bound": ("~90% VALU busy (SQ_ACTIVE_INST_VALU vs SIMD issue capacity; " + VALU_FILE + "): "
-                           "~37 VALU lane-instr/px (309 M wave-instructions per launch), so VALU issue, not HBM, bounds "
-                           "this kernel (DESIGN.md)"),
+            "issue": north_star_issue(),
         }
 
     # ---- BASELINE configs[2]: FAST-12 + BRIEF-256, 1280x720 batch 64 (detect -> describe on device) --

@@ -6,7 +6,7 @@ fixed number of times, on seeded uniform-noise frames generated on the GPU.
                      (--kind shi_tomasi by default: the north-star kernel)
   --shape fast720    fd_points_detect, FAST, 1280x720 batch 64 (BASELINE configs[2]), 10 calls
   --shape lsd        fd_lsd_map (dense) and fd_lsd_lines (compact map + host stage), 1920x1080 batch 256,
-                     64-px checker + noise (BASELINE configs[3]), 3 calls each
+                     64-px checker + noise (BASELINE configs[3]), 3 calls each (--kind dense / compact: one)
 """
 import argparse
 import os
@@ -20,7 +20,7 @@ import feature_detector_amd as fd  # noqa: E402
 THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 p = argparse.ArgumentParser()
 p.add_argument("--shape", default="bench", choices=["bench", "northstar", "fast720", "lsd"])
-p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast"])
+p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast", "dense", "compact"])
 p.add_argument("--calls", type=int, default=0)
 a = p.parse_args()
 g = torch.Generator(device="cuda")
@@ -51,9 +51,11 @@ elif a.shape == "lsd":
     c = torch.arange(cols, device="cuda").view(1, 1, cols) // 64
     base = torch.where(((r + c) % 2) == 1, 180, 60)
     frames = (base + torch.randint(-10, 11, (n, rows, cols), generator=g, device="cuda", dtype=torch.int32)).clamp(0, 255).to(torch.uint8)
-    for _ in range(a.calls or 3):
-        fd.lsd_map(frames)
-        fd.lsd_lines(frames, max_lines=2048)
+    for _ in range(a.calls or 3):  # --kind dense / compact: one of the two only
+        if a.kind != "compact":
+            fd.lsd_map(frames)
+        if a.kind != "dense":
+            fd.lsd_lines(frames, max_lines=2048)
 else:
     kind = a.kind or "fast"
     frames = noise(64, 720, 1280)
