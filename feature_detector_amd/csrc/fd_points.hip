@@ -44,6 +44,9 @@ __device__ __forceinline__ bool decode_tile(const PointsArgs &a, int &f, int &ty
 // A compile-time choice: a runtime branch here makes the waitcnt pass drain the prefetch queue.
 template <bool ALIGNED>
 __device__ __forceinline__ uint32_t load_px4(__amdgpu_buffer_rsrc_t r, int32_t off) {
+#ifdef FD_NOLOAD  // diagnostic build only (tools/gpu_noload_ab.sh): same instruction stream, no frame reads
+    return static_cast<uint32_t>(off) * 2654435761u;
+#endif
     if constexpr (ALIGNED) return buf_load_u32(r, off);
     return buf_load_u8(r, off) | (buf_load_u8(r, off + 1) << 8) | (buf_load_u8(r, off + 2) << 16) |
            (buf_load_u8(r, off + 3) << 24);

@@ -22,6 +22,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--shape", default="bench", choices=["bench", "northstar", "fast720", "lsd"])
 p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast", "dense", "compact"])
 p.add_argument("--calls", type=int, default=0)
+p.add_argument("--thr", type=float, default=None, help="response threshold override (e.g. 1e30: no candidates)")
 a = p.parse_args()
 g = torch.Generator(device="cuda")
 g.manual_seed(7)
@@ -43,7 +44,7 @@ elif a.shape == "northstar":
     out = (torch.empty((256, cap), dtype=torch.float32, device="cuda"),
            torch.empty((256, cap), dtype=torch.int32, device="cuda"), torch.empty((256,), dtype=torch.int32, device="cuda"))
     for _ in range(a.calls or 10):
-        fd.point_response(kind, frames, THR[kind], out=out)
+        fd.point_response(kind, frames, THR[kind] if a.thr is None else a.thr, out=out)
 elif a.shape == "lsd":
     kind = "lsd"
     rows, cols, n = 1080, 1920, 256
