@@ -28,10 +28,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# SuperPoint leg: MIOpen's default find mode benchmarks every conv solver on first use (incl. naive
-# reference kernels: ~30 s per run, outside the timed region). FAST mode takes the find-db/heuristic
-# choice; measured on MI355X: network 14.21 ms vs 14.26 ms with full find (same solvers).
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
+# (SuperPoint leg: MIOpen's solver search is set up in superpoint.SuperPointDetector.Initialize.)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip-level parameters)
 MFMA_PEAK_TFLOPS_FP16 = 2500.0  # dense BF16/FP16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense, no sparsity)

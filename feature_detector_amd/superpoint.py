@@ -17,6 +17,8 @@ kSuperpointNms / DISK variants are not provided (their in-graph NMS / UNet need 
 """
 from __future__ import annotations
 
+import os
+
 import ctypes
 from dataclasses import dataclass
 
@@ -217,7 +219,13 @@ class SuperPointDetector:
         if self.dtype == "fp16":
             net = net.half()
         self.net = net.to(memory_format=torch.channels_last)
-        torch.backends.cudnn.benchmark = True
+        # MIOpen solver choice (measured, tools/gpu_sp_find_probe.sh, 64x640x480 fp16): exhaustive find
+        # (benchmark=True) picks solvers worth 14.3 ms per 64 frames against 17.1 ms for immediate mode
+        # (FD_SP_FIND_EXHAUSTIVE=0), but its first use also times the naive direct solver on every
+        # conv shape (~30 s). That solver never wins, so it is left out of the search unless the caller
+        # set the variable: first find ~10 s, ~0.6 s once MIOpen's user find-db holds the shapes.
+        os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
+        torch.backends.cudnn.benchmark = os.environ.get("FD_SP_FIND_EXHAUSTIVE", "1") == "1"
         ones = torch.ones((1, self._options.kMaxImageRows, self._options.kMaxImageCols), dtype=torch.uint8, device=dev)
         self.InferenceSession(ones)
         return True
