@@ -140,10 +140,11 @@ struct LsdArgs {
     float min_norm;
     float *norm, *angle;
     uint8_t *valid;
-    uint32_t *rowbits;  // [batch][cols-1][chunks][words]: valid rows of each (column, chunk), bit r - r0
+    uint32_t *rowbits;  // [batch][chunks][words][cols-1]: valid rows of each (column, chunk), bit r - r0
+                        // (column fastest: a wave's stores and loads are contiguous)
     int words;          // ceil(chunk_h / 32)
-    int32_t *col_cnt;   // [batch][cols-1][chunks]
-    int32_t *col_base;  // same shape, exclusive scan in column-major order
+    int32_t *col_cnt;   // [batch][chunks][cols-1]
+    int32_t *col_base;  // same layout, exclusive scan in column-major order (column outer, chunk inner)
     int32_t *idx;
     int64_t idx_cap;
     int64_t *counts;

@@ -297,7 +297,7 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
                 if (INTERIOR || colv[m])
-                    a.rowbits[((static_cast<int64_t>(f) * mc + c0 + m) * a.chunks + chunk) * a.words + ((done - 1) >> 5)] =
+                    a.rowbits[((static_cast<int64_t>(f) * a.chunks + chunk) * a.words + ((done - 1) >> 5)) * mc + c0 + m] =
                         word[m];
                 word[m] = 0;
             }
@@ -325,7 +325,7 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
-        if (INTERIOR || colv[m]) a.col_cnt[(static_cast<int64_t>(f) * mc + c0 + m) * a.chunks + chunk] = cnt[m];
+        if (INTERIOR || colv[m]) a.col_cnt[(static_cast<int64_t>(f) * a.chunks + chunk) * mc + c0 + m] = cnt[m];
 }
 
 template <bool ALIGNED>
@@ -356,8 +356,9 @@ __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
     for (int64_t s0 = 0; s0 < n; s0 += 1024) {
         const int64_t s = s0 + tid;
         // entries of columns outside [1, cols-3] were never written: treat them as 0
-        const int col = static_cast<int>(s / a.chunks);
-        const int c = (s < n && col >= 1 && col <= a.cols - 3) ? cnt[s] : 0;
+        const int col = static_cast<int>(s / a.chunks), chunk = static_cast<int>(s - static_cast<int64_t>(col) * a.chunks);
+        const int64_t at = static_cast<int64_t>(chunk) * mc + col;  // (chunk, column) layout
+        const int c = (s < n && col >= 1 && col <= a.cols - 3) ? cnt[at] : 0;
         int64_t incl = c;
         for (int o = 1; o < kWave; o <<= 1) {
             const int64_t t = __shfl_up(incl, o);
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
         for (int q = 0; q < wv; ++q) wpre += wsum[q];
         const int64_t start = carry + wpre + incl - c;
         __syncthreads();
-        if (s < n) base[s] = static_cast<int32_t>(start);
+        if (s < n) base[at] = static_cast<int32_t>(start);
         if (tid == 1023) carry = start + c;
         __syncthreads();
     }
@@ -388,9 +389,9 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     if (!(col >= 1 && col <= cols - 3)) return;
     const int r0 = 1 + chunk * a.chunk_h;
     const int r1 = min(r0 + a.chunk_h, rows - 2);
-    const int64_t cc = (static_cast<int64_t>(f) * mc + col) * a.chunks + chunk;
-    int64_t pos = a.col_base[cc];
-    const uint32_t *bits = a.rowbits + cc * a.words;
+    const int64_t fc = static_cast<int64_t>(f) * a.chunks + chunk;
+    int64_t pos = a.col_base[fc * mc + col];
+    const uint32_t *bits = a.rowbits + fc * a.words * mc + col;  // word w at bits[w * mc]
     const int nw = (r1 - r0 + 31) >> 5;
     if (a.frame_base) {
         // Compact mode: the list entry carries the pixel's norm and angle, recomputed here from the
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
         const int64_t base = a.frame_base[f];
         const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
         for (int w = 0; w < nw; ++w) {
-            uint32_t m = bits[w];
+            uint32_t m = bits[static_cast<int64_t>(w) * mc];
             while (m) {
                 const int rr = r0 + 32 * w + __builtin_ctz(m);
                 m &= m - 1u;
@@ -420,7 +421,7 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     }
     int32_t *out = a.idx + static_cast<int64_t>(f) * a.idx_cap;
     for (int w = 0; w < nw; ++w) {
-        uint32_t m = bits[w];
+        uint32_t m = bits[static_cast<int64_t>(w) * mc];
         while (m) {
             const int rr = r0 + 32 * w + __builtin_ctz(m);
             m &= m - 1u;

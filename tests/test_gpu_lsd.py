@@ -100,3 +100,32 @@ def test_device_path_matches_host(fd, oracle):
         assert np.array_equal(v[b].cpu().numpy(), hv)
         assert int(cnt[b]) == len(hidx)
         assert np.array_equal(idx[b, :len(hidx)].cpu().numpy(), hidx)
+
+
+def test_config4_batch_spot_check(fd, oracle):
+    """BASELINE configs[3] shape (1920x1080 x256, the bench's 64-px checker + noise): the dense maps and
+    the valid list of frames 0, 127 and 255 against the oracle, and every frame's count consistent."""
+    torch = pytest.importorskip("torch")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4243)
+    rows, cols, n = 1080, 1920, 256
+    r = torch.arange(rows, device="cuda").view(1, rows, 1) // 64
+    c = torch.arange(cols, device="cuda").view(1, 1, cols) // 64
+    base = torch.where(((r + c) % 2) == 1, 180, 60)
+    noise = torch.randint(-10, 11, (n, rows, cols), generator=g, device="cuda", dtype=torch.int32)
+    frames = (base + noise).clamp(0, 255).to(torch.uint8)
+    mr, mc = rows - 1, cols - 1
+    out = (torch.empty((n, mr, mc), device="cuda"), torch.empty((n, mr, mc), device="cuda"),
+           torch.empty((n, mr, mc), dtype=torch.uint8, device="cuda"),
+           torch.empty((n, mr * mc), dtype=torch.int32, device="cuda"), torch.empty((n,), dtype=torch.int64, device="cuda"))
+    nm, am, vm, idx, cnt = fd.lsd_map(frames, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(cnt, vm.view(n, -1).sum(dim=1, dtype=torch.int64))
+    host = frames.cpu().numpy()
+    for b in (0, 127, 255):
+        en, ea, ev, eidx = oracle.lsd_map(host[b])
+        k = int(cnt[b])
+        assert np.array_equal(nm[b].cpu().numpy().view(np.uint32), en.view(np.uint32)), b
+        assert np.array_equal(vm[b].cpu().numpy(), ev), b
+        assert np.array_equal(am[b].cpu().numpy().view(np.uint32), ea.view(np.uint32)), b
+        assert np.array_equal(idx[b, :k].cpu().numpy(), eidx), b

@@ -9,6 +9,6 @@ for L in "$@"; do
 import csv,glob
 for f in glob.glob('gpurun_out/abl/$n/**/*kernel_stats.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        if r['Name'].startswith('void fdk'): print('$n', r['Name'][:50], r['Calls'], r['AverageNs'])
+        if 'fdk::' in r['Name']: print('$n', r['Name'].replace('void ','')[:45], r['Calls'], r['AverageNs'])
 "
 done
