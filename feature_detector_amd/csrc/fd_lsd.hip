@@ -394,27 +394,16 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     const uint32_t *bits = a.rowbits + fc * a.words * mc + col;  // word w at bits[w * mc]
     const int nw = (r1 - r0 + 31) >> 5;
     if (a.frame_base) {
-        // Compact mode: the list entry carries the pixel's norm and angle, recomputed here from the
-        // four pixels (the same operations as the map pass: bit-identical), so no dense map is written.
-        const int64_t base = a.frame_base[f];
-        const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
+        // Compact mode: all frames' lists back to back (frame_base); norm and angle follow in
+        // k_lsd_values, one thread per entry (here a column with many valid rows would keep its whole
+        // wave in the atan2f loop).
+        int32_t *out = a.idx + a.frame_base[f];
         for (int w = 0; w < nw; ++w) {
             uint32_t m = bits[static_cast<int64_t>(w) * mc];
             while (m) {
                 const int rr = r0 + 32 * w + __builtin_ctz(m);
                 m &= m - 1u;
-                const int o = rr * cols + col;
-                const int ad = static_cast<int>(buf_load_u8(rs, o + cols + 1)) - static_cast<int>(buf_load_u8(rs, o));  // :76-77
-                const int bc = static_cast<int>(buf_load_u8(rs, o + 1)) - static_cast<int>(buf_load_u8(rs, o + cols));  // :78-79
-                const int sv = ad + bc, dv = ad - bc;
-                const float q = static_cast<float>(static_cast<uint32_t>(sv * sv + dv * dv));
-                const float nrm = sqrt_rn_rsq2(f2{q, q}).x * 0.5f;  // :82 (as in the map pass)
-                const float gx = static_cast<float>(sv) / 2.0f, gy = static_cast<float>(dv) / 2.0f;  // :80-81
-                const int64_t at = base + pos;
-                a.idx[at] = static_cast<int32_t>(static_cast<int64_t>(rr) * mc + col);
-                a.lnorm[at] = nrm;
-                a.langle[at] = fd_atan2f(gx, -gy);  // :85
-                ++pos;
+                out[pos++] = static_cast<int32_t>(static_cast<int64_t>(rr) * mc + col);
             }
         }
         return;
@@ -429,6 +418,29 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
             ++pos;
         }
     }
+}
+
+// Compact mode, after the scatter: each list entry's norm and angle, recomputed from its four pixels
+// with the map pass's operations (bit-identical), one thread per entry.
+__global__ __launch_bounds__(256) void k_lsd_values(LsdArgs a, int64_t total) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= total) return;
+    int lo = 0, hi = a.batch - 1;  // frame of entry i: last f with frame_base[f] <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.frame_base[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int f = lo, rows = a.rows, cols = a.cols, mc = cols - 1;
+    const int32_t mi = a.idx[i];
+    const int rr = mi / mc, col = mi - rr * mc;
+    const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
+    const int o = rr * cols + col;
+    const int ad = static_cast<int>(buf_load_u8(rs, o + cols + 1)) - static_cast<int>(buf_load_u8(rs, o));  // :76-77
+    const int bc = static_cast<int>(buf_load_u8(rs, o + 1)) - static_cast<int>(buf_load_u8(rs, o + cols));  // :78-79
+    const int sv = ad + bc, dv = ad - bc;
+    const float q = static_cast<float>(static_cast<uint32_t>(sv * sv + dv * dv));
+    a.lnorm[i] = sqrt_rn_rsq2(f2{q, q}).x * 0.5f;                                          // :82 (as in the map pass)
+    a.langle[i] = fd_atan2f(static_cast<float>(sv) / 2.0f, -(static_cast<float>(dv) / 2.0f));  // :80-81, :85
 }
 
 // Compact mode: frame_base[f] = valid pixels of frames [0, f) (one workgroup; batch is small).
@@ -461,6 +473,10 @@ hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s) {
 hipError_t launch_lsd_scatter(const LsdArgs &a, hipStream_t s) {
     const int64_t waves = static_cast<int64_t>(a.batch) * a.chunks * a.strips;
     hipLaunchKernelGGL(k_lsd_scatter, dim3(static_cast<unsigned>((waves + 3) / 4)), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !a.frame_base || a.idx_cap <= 0) return e;
+    // compact mode: idx_cap = the batch's total number of entries (frame_base[batch])
+    hipLaunchKernelGGL(k_lsd_values, dim3(static_cast<unsigned>((a.idx_cap + 255) / 256)), dim3(256), 0, s, a, a.idx_cap);
     return hipGetLastError();
 }
 
