@@ -31,9 +31,20 @@ constexpr float kHarrisAlpha = 0.04f;                  // feature_point_harris_d
 // Workgroup -> (frame, 4 consecutive tiles of that frame); returns false for the idle waves of a
 // frame's last workgroup (they still take part in the workgroup barriers).
 // The tile coordinates are made visibly wave-uniform (readfirstlane), so row/tile logic stays scalar.
+// Logical workgroup id: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share an L2), so
+// the grid is remapped to give each XCD a contiguous range of logical ids -- a band of a frame's tile
+// rows, whose halo rows then come from that XCD's own L2 (for speed only: any placement is correct).
+// Bijective for any grid size: XCD group x = b % 8 holds q (+1 for x < r) workgroups.
+__device__ __forceinline__ int logical_block() {
+    const int b = static_cast<int>(blockIdx.x), n = static_cast<int>(gridDim.x);
+    const int q = n >> 3, r = n & 7, x = b & 7;
+    return x * q + min(x, r) + (b >> 3);
+}
+
 __device__ __forceinline__ bool decode_tile(const PointsArgs &a, int &f, int &ty, int &tx) {
-    f = blockIdx.x / a.blocks_per_frame;
-    const int t = __builtin_amdgcn_readfirstlane((blockIdx.x % a.blocks_per_frame) * 4 + (threadIdx.x >> 6));
+    const int lb = logical_block();
+    f = lb / a.blocks_per_frame;
+    const int t = __builtin_amdgcn_readfirstlane((lb % a.blocks_per_frame) * 4 + (threadIdx.x >> 6));
     tx = t % a.tiles_x;
     ty = t / a.tiles_x;
     return t < a.tiles_x * a.tiles_y;
@@ -206,14 +217,14 @@ __device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, 
     }
     if (tid == 0) {
         wg_base = total ? atomicAdd(&a.list_count[f], total) : 0u;
-        const int g = static_cast<int>(blockIdx.x) % a.blocks_per_frame;
+        const int g = logical_block() % a.blocks_per_frame;
         a.segdesc[static_cast<int64_t>(f) * a.blocks_per_frame + g] = make_uint2(wg_base, total);
     }
     __syncthreads();
     float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
     uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
     const int64_t base = wg_base;
-    const int g = static_cast<int>(blockIdx.x) % a.blocks_per_frame;
+    const int g = logical_block() % a.blocks_per_frame;
     uint64_t *head = a.seghead + (static_cast<int64_t>(f) * a.blocks_per_frame + g) * kSegHead;
     for (int i = lane; i < n; i += kWave) {
         const float r = sk.resp[i];
