@@ -89,7 +89,7 @@ template <int GRID>
 __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
                                              const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
                                              uint32_t prior, int &s_acc, int &s_done, const uint32_t *pk32,
-                                             uint32_t &tie_prev, int &tie_has_prev) {
+                                             const uint64_t *tmask, uint32_t &tie_prev, int &tie_has_prev) {
     const int lane = lane_id();
     const int d = a.dist;
     const bool pk16 = a.rows + 3 * d < 65536 && a.cols + 3 * d < 65536;  // no wrap-around in 16-bit halves
@@ -101,10 +101,11 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     bool tied = false;
     // Software pipeline: a batch's position, cell and conflict mask are loaded during the previous
     // batch's resolution (they are read-only here; only the grid is written).
-    auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C) {
+    auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C, uint64_t &T) {
         const int i = b + lane;
         const bool in = i < cnt;
         e = in ? pxy[i] : kEmpty;
+        T = pk32 ? tmask[b >> 6] : 0ull;  // (one address: a broadcast read)
         cell = gw2 + 1;
         C = 0;
         if constexpr (GRID != 0) {
@@ -114,12 +115,14 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     };
     uint32_t e_n;
     int cell_n;
-    uint64_t C_n;
-    fetch(0, e_n, cell_n, C_n);
+    uint64_t C_n, T_n;
+    fetch(0, e_n, cell_n, C_n, T_n);
     for (int b0 = 0; b0 < cnt && !done; b0 += kWave) {
         const uint32_t e = e_n;
         const int cell = cell_n;
         uint64_t C = C_n;
+        const uint64_t T = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(T_n)) |
+                           (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(T_n >> 32))) << 32);
         bool ok = e != kEmpty;
         const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
         if constexpr (GRID != 0) {
@@ -146,24 +149,18 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                 }
             }
         }
-        if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n);
+        if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n, T_n);
         const uint64_t m = ballot(ok);
         C &= m;
-        // Fixed point: a lane is decided once all of C is; accepted iff none of C was accepted.
-        uint64_t acc_m = 0, dec_m = ~m;
-        bool mine = !ok;
-        // Each pass decides at least the lowest undecided lane (its conflicts are all earlier), so
-        // 64 passes always suffice; the bound only guards against inconsistent input.
-        for (int pass = 0; dec_m != ~0ull; ++pass) {
-            if (pass >= kWave) {
-                if (lane == 0) atomicOr(&a.status[f], 0x20000000u);
-                break;
-            }
-            const bool can = !mine && (C & ~dec_m) == 0;
-            const bool take = can && (C & acc_m) == 0;
-            dec_m |= ballot(can);
-            acc_m |= ballot(take);
-            mine = mine || can;
+        // Resolution in scan order: a lane with no earlier ok neighbour in the batch is accepted; the
+        // others (few: distance-d pairs inside 64 consecutive candidates) are decided one by one in
+        // ascending order on the scalar unit -- accepted iff none of their earlier neighbours was.
+        const uint64_t conf = ballot(C != 0ull) & m;
+        uint64_t acc_m = m & ~conf;
+        for (uint64_t rest = conf; rest; rest &= rest - 1ull) {
+            const int i = __builtin_ctzll(rest);
+            const uint64_t free_m = ballot((C & acc_m) == 0ull);
+            acc_m |= free_m & (1ull << i);
         }
         // need cutoff (:67-69): features.size() >= need is checked after every append
         const uint32_t have = prior + static_cast<uint32_t>(acc);
@@ -178,23 +175,18 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
             done = true;
         }
         if (pk32) {
-            // visited lanes: all of the batch, or up to the append that reached `need`; plus the next one
+            // visited lanes: all of the batch, or up to the append that reached `need`; plus the next one.
+            // T (tmask): bit l = candidate b0 + l has the same response as its predecessor.
             const int last = done ? 63 - __builtin_clzll(acc_m) : kWave - 1;
-            const int i = b0 + lane;
-            bool t = false;
-            if (lane <= last && i < cnt) {
-                const uint32_t k = pk32[i];
-                t = i > 0 ? k == pk32[i - 1] : (t_has && k == t_prev);
-            }
-            tied = tied || ballot(t) != 0ull;
+            const uint64_t vis = last >= kWave - 1 ? ~0ull : ((2ull << last) - 1ull);
+            if (T & vis) tied = true;
+            if (b0 == 0 && t_has && pk32[0] == t_prev) tied = true;  // first candidate vs the previous chunk
             if (done) {  // the candidate after the stop (wave-uniform)
                 const int nx = b0 + last + 1;
                 // the stop is the chunk's last candidate: its successor is not at hand, so assume a
                 // tie (a reference-order resolution then re-selects the frame, with the same result)
-                if (nx >= cnt || pk32[nx] == pk32[nx - 1]) tied = true;
+                if (nx >= cnt || ((last < kWave - 1 ? (T >> (last + 1)) : tmask[(b0 >> 6) + 1]) & 1ull)) tied = true;
             }
-            t_prev = pk32[min(b0 + kWave, cnt) - 1];
-            t_has = true;
         }
         if ((acc_m >> lane) & 1ull) {
             const int pos = mbcnt64(acc_m, acc);
@@ -210,6 +202,10 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         }
         acc += popc64(acc_m);
         if constexpr (GRID == 2) __builtin_amdgcn_s_waitcnt(0);
+    }
+    if (pk32 && cnt > 0) {  // the chunk's last key, for the next chunk's first comparison
+        t_prev = pk32[cnt - 1];
+        t_has = true;
     }
     if (lane == 0) {
         s_acc = acc;
@@ -284,6 +280,7 @@ struct alignas(16) SelectLds {
     uint32_t pxy[kSelectChunk];
     uint32_t pcell[kSelectChunk];
     uint32_t pk32[kSelectChunk];  // 32-bit response keys in scan order (tie check)
+    uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor
     uint32_t grid_lds[kGridLdsCells];
     uint32_t tie_prev;
     int tie_has_prev;
@@ -997,6 +994,14 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     }
                     // conflict masks: earlier candidates of the same 64-batch within distance d
                     if (use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
+                    if (!a.tie_idx_desc) {  // tie bits for the greedy's check (wave-aligned 64-batches)
+                        const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;
+                        for (int i = tid; i < c64; i += nthr) {
+                            const bool t = i > 0 && i < c && L.pk32[i] == L.pk32[i - 1];
+                            const uint64_t m = ballot(t);
+                            if (lane == 0) L.tmask[i >> 6] = m;
+                        }
+                    }
                 }
                 __syncthreads();
                 FD_STAMP(14);  // conflict masks
@@ -1005,14 +1010,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 if (tid < kWave) {
                     const int c = static_cast<int>(sc);
                     const uint32_t *tk = a.tie_idx_desc ? nullptr : L.pk32;
+                    const uint64_t *tm = L.tmask;
                     if (!use_grid)
-                        greedy_chunk<0>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                        greedy_chunk<0>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, tm, L.tie_prev,
                                         L.tie_has_prev);
                     else if (grid_in_lds)
-                        greedy_chunk<1>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                        greedy_chunk<1>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, tm, L.tie_prev,
                                         L.tie_has_prev);
                     else
-                        greedy_chunk<2>(a, f, c, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                        greedy_chunk<2>(a, f, c, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, tk, tm, L.tie_prev,
                                         L.tie_has_prev);
                 }
                 __syncthreads();
@@ -1131,13 +1137,13 @@ __global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs
         __syncthreads();
         if (tid < kWave) {
             if (!use_grid)
-                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr,
+                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr, nullptr,
                                 L.tie_prev, L.tie_has_prev);
             else if (grid_in_lds)
-                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr,
+                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr, nullptr,
                                 L.tie_prev, L.tie_has_prev);
             else
-                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr,
+                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr, nullptr,
                                 L.tie_prev, L.tie_has_prev);
         }
         __syncthreads();
