@@ -748,7 +748,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     }
     FD_STAMP(22);
     if (use_grid && grid_in_lds) {  // the first round's LDS-direct loads are consumed (or never used)
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load still landing in this space
+        // vmcnt(0): no load still landing in this space (only if they were issued: the wait would
+        // also hold for this thread's outstanding global stores and atomics, a memory round trip)
+        if (!a.pre_keys && !seg_mode) __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
         for (int i = tid; i < cells; i += nthr) grid_lds[i] = kEmpty;
         __syncthreads();
