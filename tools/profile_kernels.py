@@ -36,7 +36,7 @@ if a.shape == "bench":
     kind = a.kind or "harris"
     frames = noise(1, 480, 640)
     for _ in range(a.calls or 200):
-        fd.detect_points(kind, frames, 200, 20, THR[kind])
+        fd.detect_points(kind, frames, 200, 20, THR[kind] if a.thr is None else a.thr)
 elif a.shape == "northstar":
     kind = a.kind or "shi_tomasi"
     frames = noise(256, 1080, 1920)
