@@ -88,8 +88,9 @@ constexpr int kRegGather = 16;  // list responses per thread and round in the le
 template <int GRID>
 __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
                                              const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
-                                             uint32_t prior, int &s_acc, int &s_done, const uint32_t *pk32,
-                                             const uint64_t *tmask, uint32_t &tie_prev, int &tie_has_prev) {
+                                             uint32_t prior, int &s_acc, int &s_done, bool ties, const uint64_t *tmask,
+                                             const uint32_t *orig, int cfull, uint32_t key0, uint32_t keylast,
+                                             uint32_t &tie_prev, int &tie_has_prev) {
     const int lane = lane_id();
     const int d = a.dist;
     const bool pk16 = a.rows + 3 * d < 65536 && a.cols + 3 * d < 65536;  // no wrap-around in 16-bit halves
@@ -101,11 +102,10 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     bool tied = false;
     // Software pipeline: a batch's position, cell and conflict mask are loaded during the previous
     // batch's resolution (they are read-only here; only the grid is written).
-    auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C, uint64_t &T) {
+    auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C) {
         const int i = b + lane;
         const bool in = i < cnt;
         e = in ? pxy[i] : kEmpty;
-        T = pk32 ? tmask[b >> 6] : 0ull;  // (one address: a broadcast read)
         cell = gw2 + 1;
         C = 0;
         if constexpr (GRID != 0) {
@@ -115,14 +115,13 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     };
     uint32_t e_n;
     int cell_n;
-    uint64_t C_n, T_n;
-    fetch(0, e_n, cell_n, C_n, T_n);
+    uint64_t C_n;
+    int stop = -1;  // position of the append that reached `need` (scan order of pxy)
+    fetch(0, e_n, cell_n, C_n);
     for (int b0 = 0; b0 < cnt && !done; b0 += kWave) {
         const uint32_t e = e_n;
         const int cell = cell_n;
         uint64_t C = C_n;
-        const uint64_t T = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(T_n)) |
-                           (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(T_n >> 32))) << 32);
         bool ok = e != kEmpty;
         const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
         if constexpr (GRID != 0) {
@@ -149,7 +148,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                 }
             }
         }
-        if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n, T_n);
+        if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n);
         const uint64_t m = ballot(ok);
         C &= m;
         // Resolution in scan order: a lane with no earlier ok neighbour in the batch is accepted; the
@@ -173,20 +172,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
             }
             acc_m = keep;
             done = true;
-        }
-        if (pk32) {
-            // visited lanes: all of the batch, or up to the append that reached `need`; plus the next one.
-            // T (tmask): bit l = candidate b0 + l has the same response as its predecessor.
-            const int last = done ? 63 - __builtin_clzll(acc_m) : kWave - 1;
-            const uint64_t vis = last >= kWave - 1 ? ~0ull : ((2ull << last) - 1ull);
-            if (T & vis) tied = true;
-            if (b0 == 0 && t_has && pk32[0] == t_prev) tied = true;  // first candidate vs the previous chunk
-            if (done) {  // the candidate after the stop (wave-uniform)
-                const int nx = b0 + last + 1;
-                // the stop is the chunk's last candidate: its successor is not at hand, so assume a
-                // tie (a reference-order resolution then re-selects the frame, with the same result)
-                if (nx >= cnt || ((last < kWave - 1 ? (T >> (last + 1)) : tmask[(b0 >> 6) + 1]) & 1ull)) tied = true;
-            }
+            stop = b0 + 63 - __builtin_clzll(acc_m);
         }
         if ((acc_m >> lane) & 1ull) {
             const int pos = mbcnt64(acc_m, acc);
@@ -203,8 +189,26 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         acc += popc64(acc_m);
         if constexpr (GRID == 2) __builtin_amdgcn_s_waitcnt(0);
     }
-    if (pk32 && cnt > 0) {  // the chunk's last key, for the next chunk's first comparison
-        t_prev = pk32[cnt - 1];
+    if (ties && cfull > 0) {
+        // The reference's visiting order of this sub-chunk ends at the stop (or runs through it). Its
+        // prefix in the full ordered sub-chunk -- including candidates dropped before the scan
+        // (`orig` maps scan positions to full positions) -- holds a tie if any of its tie bits is set
+        // (bit i: full position i equals i - 1), if its first key equals the previous chunk's last, or
+        // if the candidate after the stop equals the stop (unknown past the sub-chunk: assumed).
+        const int last = done ? (orig ? static_cast<int>(orig[stop]) : stop) : cfull - 1;
+        bool t = false;
+        for (int w = lane; w * kWave <= last; w += kWave) {
+            uint64_t word = tmask[w];
+            if (w * kWave + kWave - 1 > last) word &= (2ull << (last & (kWave - 1))) - 1ull;
+            t = t || word != 0ull;
+        }
+        tied = ballot(t) != 0ull;
+        if (t_has && key0 == t_prev) tied = true;
+        if (done) {
+            const int nx = last + 1;
+            if (nx >= cfull || ((tmask[nx >> 6] >> (nx & (kWave - 1))) & 1ull)) tied = true;
+        }
+        t_prev = keylast;  // the chunk's last key, for the next chunk's first comparison
         t_has = true;
     }
     if (lane == 0) {
@@ -281,6 +285,7 @@ struct alignas(16) SelectLds {
     uint32_t pcell[kSelectChunk];
     uint32_t pk32[kSelectChunk];  // 32-bit response keys in scan order (tie check)
     uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor
+    uint32_t key0, keylast;                    // first / last 32-bit key of the ordered sub-chunk
     uint32_t grid_lds[kGridLdsCells];
     uint32_t tie_prev;
     int tie_has_prev;
@@ -911,6 +916,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         __syncthreads();
                     }
                     FD_STAMP(10);  // sub-chunk extract
+                    // what the greedy scans: the ordered sub-chunk, or its prefiltered part (below)
+                    int g_cnt = static_cast<int>(sc);
+                    const uint32_t *g_xy = pxy, *g_cell = pcell, *g_orig = nullptr;
                 {
                     const int c = static_cast<int>(sc);
                     // Bucket placement (every bin of the sub-chunk holds <= kBucketMax keys, the usual
@@ -994,34 +1002,120 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     __syncthreads();
                     FD_STAMP(13);  // place
                     }
-                    // conflict masks: earlier candidates of the same 64-batch within distance d
-                    if (use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
-                    if (!a.tie_idx_desc) {  // tie bits for the greedy's check (wave-aligned 64-batches)
+                    if (!a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
                         const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;
                         for (int i = tid; i < c64; i += nthr) {
                             const bool t = i > 0 && i < c && L.pk32[i] == L.pk32[i - 1];
                             const uint64_t m = ballot(t);
                             if (lane == 0) L.tmask[i >> 6] = m;
                         }
+                        if (tid == 0) {
+                            L.key0 = L.pk32[0];
+                            L.keylast = L.pk32[c - 1];
+                        }
                     }
+                    // Once the grid holds features (earlier sub-chunks, priors), the candidates it
+                    // already rules out are dropped before the conflict masks and the greedy scan: the
+                    // scan would reject them anyway (the grid only grows) and they never affect
+                    // another candidate. Order is kept (a block scan); pk32 then maps scan positions
+                    // back to the full sub-chunk for the tie check.
+                    // (WIDE instance only: the long scans of FAST and list-mode frames; small corner
+                    // frames rarely get past their first sub-chunk and keep the leaner kernel)
+                    if (WIDE && use_grid && (s_acc > 0 || prior > 0) && c > kWave) {
+                        static_assert(kSelectChunk <= 2 * NT, "two prefilter rounds cover a chunk");
+                        const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
+                        const uint32_t w2 = 2u * static_cast<uint32_t>(d);
+                        auto grid_free = [&](uint32_t e, int cell) {
+                            const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+                            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+                            bool ok = true;
+#pragma unroll
+                            for (int q = 0; q < 9; ++q) {
+                                const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
+                                const uint32_t g = grid_in_lds ? grid_lds[o]
+                                                               : __hip_atomic_load(&grid_g[o], __ATOMIC_RELAXED,
+                                                                                   __HIP_MEMORY_SCOPE_AGENT);
+                                if (g == kEmpty) continue;
+                                if (pk16) {
+                                    const u16x2 dt = __builtin_bit_cast(u16x2, g) - base;
+                                    if ((dt.x > dt.y ? dt.x : dt.y) <= w2) ok = false;
+                                } else if (abs(x - static_cast<int>(g & 0xFFFFu)) <= d &&
+                                           abs(y - static_cast<int>(g >> 16)) <= d) {
+                                    ok = false;
+                                }
+                            }
+                            return ok;
+                        };
+                        // kept candidates per (round, wave): in buf, free between the ordering and the
+                        // conflict masks
+                        uint32_t *const ctot = reinterpret_cast<uint32_t *>(buf);
+                        uint64_t km[2];
+                        uint32_t ev[2], cv[2];
+#pragma unroll
+                        for (int r = 0; r < 2; ++r) {
+                            const int p = tid + r * nthr;
+                            bool keep = false;
+                            ev[r] = kEmpty;
+                            cv[r] = 0;
+                            if (p < c) {
+                                ev[r] = pxy[p];
+                                cv[r] = pcell[p];
+                                keep = ev[r] != kEmpty && grid_free(ev[r], static_cast<int>(cv[r]));
+                            }
+                            km[r] = ballot(keep);
+                            if (lane == 0) ctot[r * (NT / kWave) + wave] = popc64(km[r]);
+                        }
+                        __syncthreads();  // totals published; the tie bits are done with pk32
+                        uint32_t *cxy = reinterpret_cast<uint32_t *>(tmp), *ccell = cxy + kSelectChunk;
+                        // items run round 0 (p < nthr) then round 1; waves in order inside a round
+                        constexpr int kW = NT / kWave;
+                        uint32_t total0 = 0, total = 0, b0 = 0, b1 = 0;
+                        for (int j = 0; j < kW; ++j) {
+                            const uint32_t t0 = ctot[j], t1 = ctot[kW + j];
+                            total0 += t0;
+                            total += t0 + t1;
+                            if (j < wave) {
+                                b0 += t0;
+                                b1 += t1;
+                            }
+                        }
+                        b1 += total0;
+#pragma unroll
+                        for (int r = 0; r < 2; ++r) {
+                            if ((km[r] >> lane) & 1ull) {
+                                const uint32_t pos =
+                                    static_cast<uint32_t>(mbcnt64(km[r], static_cast<int>(r == 0 ? b0 : b1)));
+                                cxy[pos] = ev[r];
+                                ccell[pos] = cv[r];
+                                L.pk32[pos] = static_cast<uint32_t>(tid + r * nthr);
+                            }
+                        }
+                        g_cnt = static_cast<int>(total);
+                        g_xy = cxy;
+                        g_cell = ccell;
+                        g_orig = L.pk32;
+                        __syncthreads();
+                    }
+                    // conflict masks: earlier candidates of the same 64-batch within distance d
+                    if (use_grid) conflict_masks(g_xy, g_cnt, d, rows, cols, buf, tid, nthr);
                 }
                 __syncthreads();
                 FD_STAMP(14);  // conflict masks
                 // greedy scan in order by wave 0 (SelectGoodFeatures :62-72); ties checked unless the
                 // order of equal responses is defined (SuperPoint's multimap)
                 if (tid < kWave) {
-                    const int c = static_cast<int>(sc);
-                    const uint32_t *tk = a.tie_idx_desc ? nullptr : L.pk32;
+                    const int cf = static_cast<int>(sc);
+                    const bool ties = !a.tie_idx_desc;
                     const uint64_t *tm = L.tmask;
                     if (!use_grid)
-                        greedy_chunk<0>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, tm, L.tie_prev,
-                                        L.tie_has_prev);
+                        greedy_chunk<0>(a, f, g_cnt, g_xy, g_cell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, g_orig,
+                                        cf, L.key0, L.keylast, L.tie_prev, L.tie_has_prev);
                     else if (grid_in_lds)
-                        greedy_chunk<1>(a, f, c, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, tk, tm, L.tie_prev,
-                                        L.tie_has_prev);
+                        greedy_chunk<1>(a, f, g_cnt, g_xy, g_cell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, g_orig,
+                                        cf, L.key0, L.keylast, L.tie_prev, L.tie_has_prev);
                     else
-                        greedy_chunk<2>(a, f, c, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, tk, tm, L.tie_prev,
-                                        L.tie_has_prev);
+                        greedy_chunk<2>(a, f, g_cnt, g_xy, g_cell, buf, grid_g, gw2, prior, s_acc, s_done, ties, tm, g_orig,
+                                        cf, L.key0, L.keylast, L.tie_prev, L.tie_has_prev);
                 }
                 __syncthreads();
                 FD_STAMP(5);  // greedy
@@ -1139,13 +1233,13 @@ __global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs
         __syncthreads();
         if (tid < kWave) {
             if (!use_grid)
-                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr, nullptr,
+                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, nullptr, 0, 0u, 0u,
                                 L.tie_prev, L.tie_has_prev);
             else if (grid_in_lds)
-                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr, nullptr,
+                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, nullptr, 0, 0u, 0u,
                                 L.tie_prev, L.tie_has_prev);
             else
-                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, nullptr, nullptr,
+                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, nullptr, 0, 0u, 0u,
                                 L.tie_prev, L.tie_has_prev);
         }
         __syncthreads();
