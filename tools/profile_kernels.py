@@ -19,7 +19,7 @@ import feature_detector_amd as fd  # noqa: E402
 
 THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 p = argparse.ArgumentParser()
-p.add_argument("--shape", default="bench", choices=["bench", "northstar", "fast720", "lsd"])
+p.add_argument("--shape", default="bench", choices=["bench", "northstar", "nsdetect", "fast720", "fast720r", "lsd"])
 p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast", "dense", "compact"])
 p.add_argument("--calls", type=int, default=0)
 p.add_argument("--thr", type=float, default=None, help="response threshold override (e.g. 1e30: no candidates)")
@@ -57,6 +57,22 @@ elif a.shape == "lsd":
             fd.lsd_map(frames)
         if a.kind != "dense":
             fd.lsd_lines(frames, max_lines=2048)
+elif a.shape == "nsdetect":  # north-star shape through fd_points_detect (K1 with the selection histogram)
+    kind = a.kind or "shi_tomasi"
+    frames = noise(256, 1080, 1920)
+    for _ in range(a.calls or 10):
+        try:
+            fd.detect_points(kind, frames, 200, 20, THR[kind], ties="raster")
+        except Exception as e:  # (diagnostic builds that break the selection still time the kernels)
+            print("detect:", e)
+elif a.shape == "fast720r":  # the FAST kernel alone (fd_points_response: no selection histogram)
+    kind = "fast"
+    frames = noise(64, 720, 1280)
+    cap = 720 * 1280
+    out = (torch.empty((64, cap), dtype=torch.float32, device="cuda"),
+           torch.empty((64, cap), dtype=torch.int32, device="cuda"), torch.empty((64,), dtype=torch.int32, device="cuda"))
+    for _ in range(a.calls or 10):
+        fd.point_response(kind, frames, THR[kind], out=out)
 else:
     kind = a.kind or "fast"
     frames = noise(64, 720, 1280)
