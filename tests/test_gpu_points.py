@@ -269,3 +269,14 @@ def test_sqrt_rsq_exhaustive():
     assert os.path.exists(exe), "build tools/calib first (__graft_entry__.build())"
     out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and " 0 mismatches" in out.stdout, out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("name,size", [("fast", (720, 1280)), ("shi_tomasi", (1080, 1920)), ("harris", (1080, 1920))])
+def test_priors_long_scans(fd, oracle, name, size):
+    """Prior features on the long-scan paths (FAST, and list-mode frames >= 1 Mpx): the selection's
+    grid prefilter is active from the first sub-chunk, with a dense prior lattice, dist 20 and a
+    need that forces several sub-chunks; both tie orders against the oracle."""
+    rows, cols = size
+    img = oracle.make_frame("noise", 4321, rows, cols)
+    prior = np.array([(x, y) for x in range(37, cols, 97) for y in range(41, rows, 89)], np.float32)
+    check_detect(fd, oracle, name, img, 20, THR[name], len(prior) + 150, prior)
