@@ -285,7 +285,8 @@ struct alignas(16) SelectLds {
     uint32_t pcell[kSelectChunk];
     uint32_t pk32[kSelectChunk];  // 32-bit response keys in scan order (tie check)
     uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor
-    uint32_t key0, keylast;                    // first / last 32-bit key of the ordered sub-chunk
+    uint32_t prev_min;                         // smallest 32-bit key of the previous sub-chunk (prefilter)
+    int have_prev_min;
     uint32_t grid_lds[kGridLdsCells];
     uint32_t tie_prev;
     int tie_has_prev;
@@ -384,6 +385,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         prefix[0] = 0;
         L.tie_prev = 0;
         L.tie_has_prev = 0;
+        L.have_prev_min = 0;
         atomicExch(&a.status[f], 0u);  // (atomic: the flags below are atomicOr'ed)
         a.cand_n[f] = static_cast<uint32_t>(n);
         if (a.value_flag && (__hip_atomic_load(&a.pre_count[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 31))
@@ -916,11 +918,91 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         __syncthreads();
                     }
                     FD_STAMP(10);  // sub-chunk extract
-                    // what the greedy scans: the ordered sub-chunk, or its prefiltered part (below)
-                    int g_cnt = static_cast<int>(sc);
-                    const uint32_t *g_xy = pxy, *g_cell = pcell, *g_orig = nullptr;
+                    // Once the grid holds features (earlier sub-chunks, priors), the keys it already
+                    // rules out -- and those the prior mask rejects -- are dropped before the ordering:
+                    // the reference rejects them whenever it visits them (their blocking feature has a
+                    // strictly larger response, or the mask), so they never change the result and their
+                    // place among equal responses does not matter. The one exception, a chain of equal
+                    // responses across the sub-chunk boundary, is flagged as a tie (sc_max / prev_min).
+                    // The ordering then takes the merge path (the level's suffix counts no longer
+                    // describe the kept keys). WIDE instance only (FAST, list mode).
+                    int c_sort = static_cast<int>(sc);
+                    uint64_t *keys = unsorted;
+                    bool filtered = false;
+                    if (WIDE && use_grid && (s_acc > 0 || prior > 0)) {
+                        uint64_t *const kbuf = reinterpret_cast<uint64_t *>(pxy);  // pxy + pcell: free until placed
+                        static_assert(sizeof(L.pxy) + sizeof(L.pcell) >= kSelectChunk * sizeof(uint64_t), "kbuf");
+                        const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
+                        const uint32_t w2 = 2u * static_cast<uint32_t>(d);
+                        if (tid == 0) {
+                            gcount = 0;
+                            L.seg_more[0] = 0u;
+                            L.seg_more[1] = 0xFFFFFFFFu;
+                        }
+                        __syncthreads();
+                        uint32_t kmax = 0u, kmin = 0xFFFFFFFFu;
+                        for (int b0 = wave * kWave; b0 < c_sort; b0 += nthr) {
+                            const int i = b0 + lane;
+                            const uint64_t sk = i < c_sort ? unsorted[i] : 0ull;
+                            bool keep = false;
+                            if (i < c_sort) {
+                                const uint32_t k32 = static_cast<uint32_t>(sk >> 32);
+                                kmax = max(kmax, k32);
+                                kmin = min(kmin, k32);
+                                const uint32_t idx = a.tie_idx_desc ? static_cast<uint32_t>(sk) : ~static_cast<uint32_t>(sk);
+                                keep = true;  // (an out-of-range index is kept: place() raises its guard)
+                                if (idx < static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols)) {
+                                    const uint32_t y = idx / static_cast<uint32_t>(cols);
+                                    const uint32_t x = idx - y * static_cast<uint32_t>(cols);
+                                    if (fmask && !((fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u))
+                                        keep = false;
+                                    const int cell = static_cast<int>((y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1));
+                                    const uint32_t e = (y << 16) | x;
+                                    const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+#pragma unroll
+                                    for (int q = 0; q < 9; ++q) {
+                                        const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
+                                        const uint32_t g = grid_in_lds ? grid_lds[o]
+                                                                       : __hip_atomic_load(&grid_g[o], __ATOMIC_RELAXED,
+                                                                                           __HIP_MEMORY_SCOPE_AGENT);
+                                        if (g == kEmpty) continue;
+                                        if (pk16) {
+                                            const u16x2 dt = __builtin_bit_cast(u16x2, g) - base;
+                                            if ((dt.x > dt.y ? dt.x : dt.y) <= w2) keep = false;
+                                        } else if (abs(static_cast<int>(x) - static_cast<int>(g & 0xFFFFu)) <= d &&
+                                                   abs(static_cast<int>(y) - static_cast<int>(g >> 16)) <= d) {
+                                            keep = false;
+                                        }
+                                    }
+                                }
+                            }
+                            const uint64_t m = ballot(keep);
+                            if (m) {
+                                uint32_t off = 0;
+                                if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
+                                off = __builtin_amdgcn_readfirstlane(off);
+                                if (keep) kbuf[mbcnt64(m, off)] = sk;
+                            }
+                        }
+                        for (int o = kWave / 2; o > 0; o >>= 1) {
+                            kmax = max(kmax, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmax), o)));
+                            kmin = min(kmin, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmin), o)));
+                        }
+                        if (lane == 0) {
+                            atomicMax(&L.seg_more[0], kmax);
+                            atomicMin(&L.seg_more[1], kmin);
+                        }
+                        __syncthreads();
+                        c_sort = static_cast<int>(gcount);
+                        keys = kbuf;
+                        filtered = true;
+                        if (tid == 0 && !a.tie_idx_desc && L.have_prev_min && L.seg_more[0] == L.prev_min)
+                            atomicOr(&a.status[f], FD_FRAME_TIES);
+                    }
                 {
-                    const int c = static_cast<int>(sc);
+                    const int c = c_sort;
+                    uint64_t *const unsorted = keys;
+
                     // Bucket placement (every bin of the sub-chunk holds <= kBucketMax keys, the usual
                     // case at the top of the list): a key of bin b belongs at (keys in the bins above b)
                     // + (larger keys of its own bin). The level's suffix counts give the first term; a
@@ -929,7 +1011,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     uint64_t me = 0;
                     uint32_t s_b = 0, s_b1 = 0;
                     int bin = 0;
-                    bool big = c > nthr;
+                    bool big = c > nthr || filtered;
                     if (!big && tid < c) {
                         me = unsorted[tid];
                         bin = static_cast<int>((me >> rem) & ((1ull << w) - 1ull));
@@ -1009,113 +1091,30 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                             const uint64_t m = ballot(t);
                             if (lane == 0) L.tmask[i >> 6] = m;
                         }
-                        if (tid == 0) {
-                            L.key0 = L.pk32[0];
-                            L.keylast = L.pk32[c - 1];
-                        }
-                    }
-                    // Once the grid holds features (earlier sub-chunks, priors), the candidates it
-                    // already rules out are dropped before the conflict masks and the greedy scan: the
-                    // scan would reject them anyway (the grid only grows) and they never affect
-                    // another candidate. Order is kept (a block scan); pk32 then maps scan positions
-                    // back to the full sub-chunk for the tie check.
-                    // (WIDE instance only: the long scans of FAST and list-mode frames; small corner
-                    // frames rarely get past their first sub-chunk and keep the leaner kernel)
-                    if (WIDE && use_grid && (s_acc > 0 || prior > 0) && c > kWave) {
-                        static_assert(kSelectChunk <= 2 * NT, "two prefilter rounds cover a chunk");
-                        const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
-                        const uint32_t w2 = 2u * static_cast<uint32_t>(d);
-                        auto grid_free = [&](uint32_t e, int cell) {
-                            const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
-                            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-                            bool ok = true;
-#pragma unroll
-                            for (int q = 0; q < 9; ++q) {
-                                const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
-                                const uint32_t g = grid_in_lds ? grid_lds[o]
-                                                               : __hip_atomic_load(&grid_g[o], __ATOMIC_RELAXED,
-                                                                                   __HIP_MEMORY_SCOPE_AGENT);
-                                if (g == kEmpty) continue;
-                                if (pk16) {
-                                    const u16x2 dt = __builtin_bit_cast(u16x2, g) - base;
-                                    if ((dt.x > dt.y ? dt.x : dt.y) <= w2) ok = false;
-                                } else if (abs(x - static_cast<int>(g & 0xFFFFu)) <= d &&
-                                           abs(y - static_cast<int>(g >> 16)) <= d) {
-                                    ok = false;
-                                }
-                            }
-                            return ok;
-                        };
-                        // kept candidates per (round, wave): in buf, free between the ordering and the
-                        // conflict masks
-                        uint32_t *const ctot = reinterpret_cast<uint32_t *>(buf);
-                        uint64_t km[2];
-                        uint32_t ev[2], cv[2];
-#pragma unroll
-                        for (int r = 0; r < 2; ++r) {
-                            const int p = tid + r * nthr;
-                            bool keep = false;
-                            ev[r] = kEmpty;
-                            cv[r] = 0;
-                            if (p < c) {
-                                ev[r] = pxy[p];
-                                cv[r] = pcell[p];
-                                keep = ev[r] != kEmpty && grid_free(ev[r], static_cast<int>(cv[r]));
-                            }
-                            km[r] = ballot(keep);
-                            if (lane == 0) ctot[r * (NT / kWave) + wave] = popc64(km[r]);
-                        }
-                        __syncthreads();  // totals published; the tie bits are done with pk32
-                        uint32_t *cxy = reinterpret_cast<uint32_t *>(tmp), *ccell = cxy + kSelectChunk;
-                        // items run round 0 (p < nthr) then round 1; waves in order inside a round
-                        constexpr int kW = NT / kWave;
-                        uint32_t total0 = 0, total = 0, b0 = 0, b1 = 0;
-                        for (int j = 0; j < kW; ++j) {
-                            const uint32_t t0 = ctot[j], t1 = ctot[kW + j];
-                            total0 += t0;
-                            total += t0 + t1;
-                            if (j < wave) {
-                                b0 += t0;
-                                b1 += t1;
-                            }
-                        }
-                        b1 += total0;
-#pragma unroll
-                        for (int r = 0; r < 2; ++r) {
-                            if ((km[r] >> lane) & 1ull) {
-                                const uint32_t pos =
-                                    static_cast<uint32_t>(mbcnt64(km[r], static_cast<int>(r == 0 ? b0 : b1)));
-                                cxy[pos] = ev[r];
-                                ccell[pos] = cv[r];
-                                L.pk32[pos] = static_cast<uint32_t>(tid + r * nthr);
-                            }
-                        }
-                        g_cnt = static_cast<int>(total);
-                        g_xy = cxy;
-                        g_cell = ccell;
-                        g_orig = L.pk32;
-                        __syncthreads();
                     }
                     // conflict masks: earlier candidates of the same 64-batch within distance d
-                    if (use_grid) conflict_masks(g_xy, g_cnt, d, rows, cols, buf, tid, nthr);
+                    if (use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
                 }
                 __syncthreads();
                 FD_STAMP(14);  // conflict masks
                 // greedy scan in order by wave 0 (SelectGoodFeatures :62-72); ties checked unless the
                 // order of equal responses is defined (SuperPoint's multimap)
                 if (tid < kWave) {
-                    const int cf = static_cast<int>(sc);
                     const bool ties = !a.tie_idx_desc;
                     const uint64_t *tm = L.tmask;
                     if (!use_grid)
-                        greedy_chunk<0>(a, f, g_cnt, g_xy, g_cell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, g_orig,
-                                        cf, L.key0, L.keylast, L.tie_prev, L.tie_has_prev);
+                        greedy_chunk<0>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, nullptr,
+                                        c_sort, L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
                     else if (grid_in_lds)
-                        greedy_chunk<1>(a, f, g_cnt, g_xy, g_cell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, g_orig,
-                                        cf, L.key0, L.keylast, L.tie_prev, L.tie_has_prev);
+                        greedy_chunk<1>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, nullptr,
+                                        c_sort, L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
                     else
-                        greedy_chunk<2>(a, f, g_cnt, g_xy, g_cell, buf, grid_g, gw2, prior, s_acc, s_done, ties, tm, g_orig,
-                                        cf, L.key0, L.keylast, L.tie_prev, L.tie_has_prev);
+                        greedy_chunk<2>(a, f, c_sort, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, ties, tm, nullptr,
+                                        c_sort, L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
+                }
+                if (tid == 0 && (filtered || c_sort > 0)) {  // the sub-chunk's smallest 32-bit key
+                    L.prev_min = filtered ? L.seg_more[1] : L.pk32[c_sort - 1];
+                    L.have_prev_min = 1;
                 }
                 __syncthreads();
                 FD_STAMP(5);  // greedy
