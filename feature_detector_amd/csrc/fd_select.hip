@@ -68,7 +68,12 @@ __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const Sel
 }
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
-constexpr int kSubChunk = 512;  // keys sorted per greedy sub-chunk
+// Keys ordered per greedy sub-chunk: corner frames usually stop within the first few hundred; FAST's
+// long scans drop most keys before ordering (grid prefilter), so there the whole superchunk is one
+// sub-chunk (measured at 1280x720x64: 512 -> 190 us, 768 -> 166, 2048 -> 160; the 1080p list-mode
+// corner selection prefers 512: 768 -> 78 us vs ~74).
+constexpr int kSubChunk = 512;
+constexpr int kSubChunkFast = kSelectChunk;
 constexpr int kBucketMax = 64;  // largest bin of a sub-chunk ordered by bucket placement (else merge sort)
 // k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
 // with 256 threads (4x the items per wave) the headline frame's selection measured 1.3x slower.
@@ -882,14 +887,13 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 if (use_grid) pcell[pos] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
             };
             // Sub-chunks of <= kSubChunk keys from the top bins of the superchunk (already in LDS):
+            const uint32_t sub_lim = static_cast<uint32_t>((WIDE && a.wide_eager) ? kSubChunkFast : kSubChunk);
             // the greedy usually stops within the first few hundred keys.
             int shi = hi;
             while (shi >= lo && !s_done) {
                 const uint32_t sbase = S[shi + 1];
                 // (the whole remaining range fits a sub-chunk: no search)
-                const int q0 = S[lo] - sbase <= static_cast<uint32_t>(kSubChunk)
-                                   ? lo
-                                   : first_le(S, lo, shi + 1, sbase, static_cast<uint32_t>(kSubChunk));
+                const int q0 = S[lo] - sbase <= sub_lim ? lo : first_le(S, lo, shi + 1, sbase, sub_lim);
                 const int slo = min(q0, shi);  // one bin larger than a sub-chunk is taken whole
                 const uint32_t sc = S[slo] - sbase;
                 if (sc > 0) {
