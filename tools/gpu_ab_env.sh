@@ -9,6 +9,6 @@ for v in "$@"; do
 import csv,glob
 for f in glob.glob('gpurun_out/abe/$VAR$v/**/*kernel_stats.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        if r['Name'].startswith('void fdk'): print('$VAR=$v', r['Name'][:45], r['Calls'], r['AverageNs'])
+        if 'fdk::' in r['Name']: print('$VAR=$v', r['Name'].replace('void ','')[:45], r['Calls'], r['AverageNs'])
 "
 done
