@@ -68,6 +68,10 @@ __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const Sel
 }
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
+#ifndef FD_SEQ_CONFLICTS
+#define FD_SEQ_CONFLICTS 12
+#endif
+constexpr int kSeqConflicts = FD_SEQ_CONFLICTS;  // greedy batch: ordered scalar pass up to this many conflicted lanes
 // Keys ordered per greedy sub-chunk: corner frames usually stop within the first few hundred; FAST's
 // long scans drop most keys before ordering (grid prefilter), so there the whole superchunk is one
 // sub-chunk (measured at 1280x720x64: 512 -> 190 us, 768 -> 166, 2048 -> 160; the 1080p list-mode
@@ -159,12 +163,30 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         // Resolution in scan order: a lane with no earlier ok neighbour in the batch is accepted; the
         // others (few: distance-d pairs inside 64 consecutive candidates) are decided one by one in
         // ascending order on the scalar unit -- accepted iff none of their earlier neighbours was.
+        // Many conflicted lanes (FAST's clustered top keys): a fixed point instead, where each pass
+        // decides every lane whose earlier neighbours are all decided (passes = the longest chain).
         const uint64_t conf = ballot(C != 0ull) & m;
         uint64_t acc_m = m & ~conf;
-        for (uint64_t rest = conf; rest; rest &= rest - 1ull) {
-            const int i = __builtin_ctzll(rest);
-            const uint64_t free_m = ballot((C & acc_m) == 0ull);
-            acc_m |= free_m & (1ull << i);
+        if (popc64(conf) <= kSeqConflicts) {
+            for (uint64_t rest = conf; rest; rest &= rest - 1ull) {
+                const int i = __builtin_ctzll(rest);
+                const uint64_t free_m = ballot((C & acc_m) == 0ull);
+                acc_m |= free_m & (1ull << i);
+            }
+        } else {
+            uint64_t dec_m = ~conf;  // decided: unconflicted lanes (accepted if ok) and the not-ok ones
+            bool mine = ((conf >> lane) & 1ull) == 0ull;
+            for (int pass = 0; dec_m != ~0ull; ++pass) {
+                if (pass >= kWave) {  // each pass decides the lowest undecided lane: unreachable
+                    if (lane == 0) atomicOr(&a.status[f], 0x20000000u);
+                    break;
+                }
+                const bool can = !mine && (C & ~dec_m) == 0ull;
+                const bool take = can && (C & acc_m) == 0ull;
+                dec_m |= ballot(can);
+                acc_m |= ballot(take);
+                mine = mine || can;
+            }
         }
         // need cutoff (:67-69): features.size() >= need is checked after every append
         const uint32_t have = prior + static_cast<uint32_t>(acc);
