@@ -98,7 +98,7 @@ template <int GRID>
 __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
                                              const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
                                              uint32_t prior, int &s_acc, int &s_done, bool ties, const uint64_t *tmask,
-                                             const uint32_t *orig, int cfull, uint32_t key0, uint32_t keylast,
+                                             uint32_t key0, uint32_t keylast,
                                              uint32_t &tie_prev, int &tie_has_prev) {
     const int lane = lane_id();
     const int d = a.dist;
@@ -216,13 +216,13 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         acc += popc64(acc_m);
         if constexpr (GRID == 2) __builtin_amdgcn_s_waitcnt(0);
     }
-    if (ties && cfull > 0) {
+    if (ties && cnt > 0) {
         // The reference's visiting order of this sub-chunk ends at the stop (or runs through it). Its
-        // prefix in the full ordered sub-chunk -- including candidates dropped before the scan
-        // (`orig` maps scan positions to full positions) -- holds a tie if any of its tie bits is set
-        // (bit i: full position i equals i - 1), if its first key equals the previous chunk's last, or
-        // if the candidate after the stop equals the stop (unknown past the sub-chunk: assumed).
-        const int last = done ? (orig ? static_cast<int>(orig[stop]) : stop) : cfull - 1;
+        // prefix holds a tie if any of its tie bits is set (bit i: position i equals i - 1), if its
+        // first key equals the previous sub-chunk's last, or if the candidate after the stop equals the
+        // stop (unknown past the sub-chunk: assumed). (Keys the prefilter dropped are always rejected
+        // and cannot matter, see select_frame.)
+        const int last = done ? stop : cnt - 1;
         bool t = false;
         for (int w = lane; w * kWave <= last; w += kWave) {
             uint64_t word = tmask[w];
@@ -233,7 +233,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         if (t_has && key0 == t_prev) tied = true;
         if (done) {
             const int nx = last + 1;
-            if (nx >= cfull || ((tmask[nx >> 6] >> (nx & (kWave - 1))) & 1ull)) tied = true;
+            if (nx >= cnt || ((tmask[nx >> 6] >> (nx & (kWave - 1))) & 1ull)) tied = true;
         }
         t_prev = keylast;  // the chunk's last key, for the next chunk's first comparison
         t_has = true;
@@ -1129,14 +1129,14 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     const bool ties = !a.tie_idx_desc;
                     const uint64_t *tm = L.tmask;
                     if (!use_grid)
-                        greedy_chunk<0>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, nullptr,
-                                        c_sort, L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
+                        greedy_chunk<0>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
+                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
                     else if (grid_in_lds)
-                        greedy_chunk<1>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm, nullptr,
-                                        c_sort, L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
+                        greedy_chunk<1>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
+                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
                     else
-                        greedy_chunk<2>(a, f, c_sort, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, ties, tm, nullptr,
-                                        c_sort, L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
+                        greedy_chunk<2>(a, f, c_sort, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, ties, tm,
+                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
                 }
                 if (tid == 0 && (filtered || c_sort > 0)) {  // the sub-chunk's smallest 32-bit key
                     L.prev_min = filtered ? L.seg_more[1] : L.pk32[c_sort - 1];
@@ -1258,13 +1258,13 @@ __global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs
         __syncthreads();
         if (tid < kWave) {
             if (!use_grid)
-                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, nullptr, 0, 0u, 0u,
+                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
                                 L.tie_prev, L.tie_has_prev);
             else if (grid_in_lds)
-                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, nullptr, 0, 0u, 0u,
+                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
                                 L.tie_prev, L.tie_has_prev);
             else
-                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, nullptr, 0, 0u, 0u,
+                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
                                 L.tie_prev, L.tie_has_prev);
         }
         __syncthreads();
