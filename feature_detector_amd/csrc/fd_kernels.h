@@ -18,6 +18,11 @@ constexpr int kSegHead = 64;           // selection keys kept per sorted segment
 constexpr int kWideKeys = 8192;        // keys per frame of k_select's wide first pass (SelectArgs::wide_keys)
 constexpr int kHistBins = 4096;         // level-0 digit of the selection key: top 12 bits of the mapped response
 
+// k_corner_lp tiles: px columns per lane, halo-only lanes per side so that lane 0 / 63 cover the 3
+// columns of reach (NMS + 3x3 sum + central difference): 2 lanes at px = 2, else 1.
+constexpr int lp_halo_lanes(int px) { return px == 2 ? 2 : 1; }
+constexpr int lp_tile_w(int px) { return (64 - 2 * lp_halo_lanes(px)) * px; }
+
 // A raster-mode segment entry (fd_points_candidates only).
 struct Cand {
     float resp;
@@ -43,6 +48,7 @@ struct PointsArgs {
     int batch, rows, cols;
     int tiles_x, tiles_y, tile_h;
     int blocks_per_frame;  // workgroups of 4 waves per frame (a workgroup never straddles frames)
+    int px;  // corner detect/response: columns per lane of k_corner_lp (2, 4, 8; tile width lp_tile_w), 0 = k_corner
     int aligned4;  // cols % 4 == 0 and 4-byte aligned frames: whole-dword loads are range-exact
     float thr;
     const uint32_t *mask;  // prior-feature bitmap [batch][rows][mask_wpr], bit = mask true; null = all ones
@@ -204,6 +210,7 @@ hipError_t launch_mask_boxes(const float *prior_xy, const int32_t *prior_frame, 
 hipError_t launch_fast_mask_scan(const uint32_t *mask, int mask_wpr, int batch, int rows, int cols, int32_t *row_base,
                                  int32_t *word_pref, hipStream_t s);
 hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s);
+hipError_t launch_corner_lp_any(int kind, const PointsArgs &a, hipStream_t s);  // k_corner_lp (a.px != 0)
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s);
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
 hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);

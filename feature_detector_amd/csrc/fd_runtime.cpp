@@ -316,13 +316,30 @@ struct PointGeom {
     bool empty;
 };
 
-PointGeom point_geom(int kind, int batch, int rows, int cols) {
+// Columns per lane of k_corner_lp for a corner launch in list mode (fd_points_detect /
+// fd_points_response); 0 = k_corner (FAST, negative thresholds, the raster-ordered candidate stage).
+// Large launches take wide lanes (the halo exchanges and loop control shared by more pixels), small
+// ones narrow lanes (more waves, shorter serial row chains). FD_PX overrides (A/B).
+int corner_px(int kind, int batch, int rows, int cols, float thr) {
+    if (kind == FD_FAST || !(thr >= 0.0f)) return 0;
+    if (const char *e = std::getenv("FD_PX")) {
+        const int v = std::atoi(e);
+        if (v == 0 || v == 2 || v == 4 || v == 8) return v;
+    }
+    // Measured (north-star shape, 1080p x 256): 4 columns per lane 4-5 % faster than k_corner, 8 slower
+    // (VGPR-limited to 3 waves per SIMD); at 640x480 x 1 k_corner is faster (11.4 vs 10.0 us).
+    const int64_t px = static_cast<int64_t>(batch) * rows * cols;
+    return px >= (int64_t(1) << 21) ? 4 : 0;
+}
+
+PointGeom point_geom(int kind, int batch, int rows, int cols, int px = 0) {
     PointGeom g{};
     g.border = kind == FD_FAST ? 3 : 2;
     g.out_rows = rows - 2 * g.border;
     const int out_cols = cols - 2 * g.border;
     g.empty = g.out_rows <= 0 || out_cols <= 0;
-    g.tiles_x = std::max(1, (cols - g.border + fdk::kTileW - 1) / fdk::kTileW);
+    const int tw = px ? fdk::lp_tile_w(px) : fdk::kTileW;
+    g.tiles_x = std::max(1, (cols - g.border + tw - 1) / tw);
     const int period = kind == FD_FAST ? 7 : 6;  // rows per unrolled loop iteration of the kernel
     g.tile_h = choose_tile_h(batch, g.tiles_x, std::max(g.out_rows, 1), period, kind == FD_FAST ? 9 : 100);
     g.tiles_y = std::max(1, (std::max(g.out_rows, 1) + g.tile_h - 1) / g.tile_h);
@@ -426,6 +443,13 @@ std::string hex(uint32_t v) {
 // feature_point_fast_detector.cpp:83-98), sorted here with std::sort and the reference comparator,
 // and the resulting visiting order goes back to the GPU for the greedy pass (k_select_ordered).
 int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb) {
+    // The status read below synchronises the stream, which a stream being captured into a graph cannot
+    // do (and the host sort could not be replayed): refuse before touching the capture.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    FD_HIP_TRY(c, hipStreamIsCapturing(c->stream, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+        return fail(c, FD_ERR_INVALID, "FD_TIES_REFERENCE synchronises (status read, host std::sort): not allowed "
+                                       "during stream capture; use FD_TIES_RASTER and read FD_FRAME_TIES");
     std::vector<uint32_t> st(2 * static_cast<size_t>(batch));
     FD_HIP_TRY(c, hipMemcpyAsync(st.data(), sb.status, sizeof(uint32_t) * st.size(), hipMemcpyDeviceToHost, c->stream));
     FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -798,10 +822,12 @@ int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t m
         }
     }
     FD_HIP_TRY(c, ensure(c, c->status, sizeof(uint32_t) * 2 * static_cast<size_t>(batch)));
-    const PointGeom g = point_geom(kind, batch, rows, cols);
-    if (!g.empty && use_seg_lists(g.blocks_per_frame, rows, cols)) {
-        FD_HIP_TRY(c, ensure(c, c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
-        FD_HIP_TRY(c, ensure(c, c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
+    for (const int px : {0, corner_px(kind, batch, rows, cols, 0.0f)}) {  // (either kernel's geometry)
+        const PointGeom g = point_geom(kind, batch, rows, cols, px);
+        if (!g.empty && use_seg_lists(g.blocks_per_frame, rows, cols)) {
+            FD_HIP_TRY(c, ensure(c, c->segdesc, sizeof(uint2) * static_cast<size_t>(batch) * g.blocks_per_frame));
+            FD_HIP_TRY(c, ensure(c, c->seghead, sizeof(uint64_t) * fdk::kSegHead * static_cast<size_t>(batch) * g.blocks_per_frame));
+        }
     }
     return FD_OK;
 }
@@ -820,13 +846,15 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     rc = setup_priors(c, batch, rows, cols, opts->min_feature_distance, prior_xy, prior_counts, pi);
     if (rc) return rc;
 
-    const PointGeom g = point_geom(kind, batch, rows, cols);
+    const int px = corner_px(kind, batch, rows, cols, opts->min_valid_response);
+    const PointGeom g = point_geom(kind, batch, rows, cols, px);
     const int64_t cap = detect_list_cap(kind, rows, cols);
     SelectBufs sb{};
     rc = select_buffers(c, batch, cap, sb);
     if (rc) return rc;
 
     fdk::PointsArgs a{};
+    a.px = px;
     a.frames = dframes;
     a.batch = batch;
     a.rows = rows;
@@ -900,10 +928,12 @@ static int points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch
     if (!opts || !frames || !out_resp || !out_idx || !out_counts || cand_cap < 1)
         return fail(c, FD_ERR_INVALID, "bad arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
-    const PointGeom g = point_geom(kind, batch, rows, cols);
+    const int px = corner_px(kind, batch, rows, cols, opts->min_valid_response);
+    const PointGeom g = point_geom(kind, batch, rows, cols, px);
     if (reset_counts) FD_HIP_TRY(c, hipMemsetAsync(out_counts, 0, sizeof(uint32_t) * batch, c->stream));
     if (g.empty) return FD_OK;
     fdk::PointsArgs a{};
+    a.px = px;
     a.frames = frames;
     a.batch = batch;
     a.rows = rows;

@@ -191,14 +191,18 @@ class DetectResult:
 
 
 def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_valid_response: float = 0.1,
-                  prior=None, ctx: Context | None = None, out=None, ties: str = "reference") -> DetectResult:
+                  prior=None, ctx: Context | None = None, out=None, ties: str | None = None) -> DetectResult:
     """FeaturePointDetector::DetectGoodFeatures on a batch (include/fd_hip.h fd_points_detect).
 
     Returns the NEW features per frame (x, y), in selection order, and the per-frame status words.
-    ties="reference" (default): frames whose greedy scan meets equal responses are re-selected in the
+    ties="reference": frames whose greedy scan meets equal responses are re-selected in the
     reference's std::sort order, so every frame equals the reference's DetectGoodFeatures; the call
-    then synchronises once. ties="raster": equal responses by raster index (fully asynchronous,
-    graph-capturable; identical wherever no tie reaches the scan, FD_FRAME_TIES marks the others).
+    synchronises the stream once (a status read), so it cannot run under graph capture (the library
+    refuses it there). ties="raster": equal responses by raster index, fully asynchronous and
+    graph-capturable; identical to "reference" wherever no tie reaches the scan, and FD_FRAME_TIES in
+    the status words marks the frames where one did. Default (None): "reference" for host frames
+    (the reference API's semantics), "raster" for torch device frames (asynchronous; check
+    `frame_flags() & FRAME_TIES` or pass ties="reference" to get the reference order there too).
     With torch device frames the outputs are device tensors (on the current stream); `out` may pass
     preallocated (xy, counts) or (xy, counts, status) tensors so that repeated calls allocate nothing.
     """
@@ -206,6 +210,8 @@ def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_v
     ptr, on_dev, b, r, c, keep = _frames(frames)
     ctx = _resolve_ctx(ctx, frames)
     _bind_stream(ctx, bool(on_dev))
+    if ties is None:
+        ties = "raster" if on_dev else "reference"
     ctx.set_tie_order(ties)
     opts = fd_point_opts(int(min_feature_distance), float(min_valid_response))
     pxy, pcnt, _keep2 = _priors(prior, b)

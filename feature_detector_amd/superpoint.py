@@ -219,7 +219,7 @@ class SuperPointDetector:
         if self.dtype == "fp16":
             net = net.half()
         self.net = net.to(memory_format=torch.channels_last)
-        # MIOpen solver choice (measured, tools/gpu_sp_find_probe.sh, 64x640x480 fp16): exhaustive find
+        # MIOpen solver choice (measured with tools/sp_find_probe.py, 64x640x480 fp16): exhaustive find
         # (benchmark=True) picks solvers worth 14.3 ms per 64 frames against 17.1 ms for immediate mode
         # (FD_SP_FIND_EXHAUSTIVE=0), but its first use also times the naive direct solver on every
         # conv shape (~30 s). That solver never wins, so it is left out of the search unless the caller

@@ -199,7 +199,7 @@ def test_large_batch_properties(fd, oracle):
     host = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 1000 + i, 1080, 1920)
                      for i in range(B)])
     dev = torch.from_numpy(host).cuda()
-    res = fd.detect_points("shi_tomasi", dev, 200, 20, 40.0)
+    res = fd.detect_points("shi_tomasi", dev, 200, 20, 40.0, ties="reference")
     torch.cuda.synchronize()
     counts = res.counts.cpu().numpy()
     xy = res.xy.cpu().numpy()
@@ -219,7 +219,7 @@ def test_device_tensor_path_matches_host(fd, oracle):
     frames = np.stack([oracle.make_frame("noise", s, 480, 640) for s in (21, 22, 23)])
     for name in ("harris", "shi_tomasi", "fast"):
         hres = fd.detect_points(name, frames, 200, 20, THR[name])
-        dres = fd.detect_points(name, torch.from_numpy(frames).cuda(), 200, 20, THR[name])
+        dres = fd.detect_points(name, torch.from_numpy(frames).cuda(), 200, 20, THR[name], ties="reference")
         torch.cuda.synchronize()
         assert np.array_equal(dres.counts.cpu().numpy(), hres.counts)
         for b in range(3):
@@ -280,3 +280,30 @@ def test_priors_long_scans(fd, oracle, name, size):
     img = oracle.make_frame("noise", 4321, rows, cols)
     prior = np.array([(x, y) for x in range(37, cols, 97) for y in range(41, rows, 89)], np.float32)
     check_detect(fd, oracle, name, img, 20, THR[name], len(prior) + 150, prior)
+
+
+@pytest.mark.parametrize("px", ["0", "2", "4", "8"])
+def test_lane_widths_bit_exact(fd, oracle, image_png, monkeypatch, px):
+    """Every per-pixel kernel variant (FD_PX: 0 = k_corner, 2/4/8 = k_corner_lp columns per lane; the
+    library picks one by launch size) gives the oracle's unordered candidate set and, through detect
+    (sorted-segment and list modes, with and without priors), the oracle's features."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("FD_PX", px)
+    frames = [image_png, oracle.make_frame("noise", 31, 480, 640), oracle.make_frame("checker", 32, 250, 13),
+              oracle.make_frame("noise", 33, 37, 1001)]
+    for img in frames:
+        rows, cols = img.shape
+        dev = torch.from_numpy(np.ascontiguousarray(img[None])).cuda()
+        for name in ("harris", "shi_tomasi"):
+            resp, idx, cnt = fd.point_response(name, dev, THR[name])
+            torch.cuda.synchronize()
+            n = int(cnt.cpu()[0])
+            gi = idx[0, :n].cpu().numpy().astype(np.int64)
+            gr = resp[0, :n].cpu().numpy()
+            er, ex, ey = oracle_candidates(oracle, name, img, THR[name])
+            o = np.argsort(gi, kind="stable")
+            assert np.array_equal(gi[o], ey.astype(np.int64) * cols + ex)
+            assert np.array_equal(gr[o].view(np.uint32), er.view(np.uint32))
+            check_detect(fd, oracle, name, img, 20, THR[name], 200)
+    prior = np.array([(x, y) for x in range(20, 752, 60) for y in range(15, 480, 45)], np.float32)
+    check_detect(fd, oracle, "shi_tomasi", image_png, 15, 40.0, len(prior) + 120, prior)

@@ -79,12 +79,39 @@ def test_device_frames_reference_order(fd, oracle):
     torch = pytest.importorskip("torch")
     host = np.stack([make_tie_frame(oracle, seed=s) for s in (1, 2)])
     dev = torch.from_numpy(host).cuda()
-    res = fd.detect_points("shi_tomasi", dev, 200, 20, 40.0)
+    res = fd.detect_points("shi_tomasi", dev, 200, 20, 40.0, ties="reference")
     torch.cuda.synchronize()
     for b in range(2):
         e0 = oracle.detect(1, host[b], 20, 40.0, 200, sort_mode=0)[0]
         np.testing.assert_array_equal(res.features(b), e0)
     res.check()
-    # raster order on the device is asynchronous; its status words arrive on the stream
-    ras = fd.detect_points("shi_tomasi", dev, 200, 20, 40.0, ties="raster")
+    # raster order on the device is asynchronous (the default for device frames); its status words
+    # arrive on the stream
+    ras = fd.detect_points("shi_tomasi", dev, 200, 20, 40.0)
     assert (ras.frame_flags() & fd.points.FRAME_TIES).all()
+    for b in range(2):
+        np.testing.assert_array_equal(ras.features(b), oracle.detect(1, host[b], 20, 40.0, 200, sort_mode=1)[0])
+
+
+def test_reference_order_refused_under_graph_capture(fd, oracle):
+    """ties="reference" synchronises the stream (status read + host sort): under hipGraph capture the
+    library refuses it with FD_ERR_INVALID before touching the capture; raster order captures fine."""
+    torch = pytest.importorskip("torch")
+    dev = torch.from_numpy(oracle.make_frame("noise", 5, 480, 640)[None].copy()).cuda()
+    xy = torch.empty((1, 201, 2), dtype=torch.float32, device="cuda")
+    cnt = torch.empty((1,), dtype=torch.int32, device="cuda")
+    fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt))  # warm (workspace sized outside capture)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(fd.FdError):
+        with torch.cuda.graph(g, stream=s):
+            fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt), ties="reference")
+    torch.cuda.synchronize()
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, stream=s):
+        fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt))
+    g2.replay()
+    torch.cuda.synchronize()
+    exp = oracle.detect(0, dev[0].cpu().numpy(), 20, 30.0, 200, sort_mode=1)[0]
+    np.testing.assert_array_equal(xy[0, :int(cnt[0])].cpu().numpy(), exp)
