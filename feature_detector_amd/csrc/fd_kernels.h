@@ -115,6 +115,7 @@ struct SelectArgs {
     int nseg;               // segments per frame
     uint64_t *wide_keys;  // [batch][kWideKeys] scratch of the wide pass, or null (one list pass per chunk)
     int wide_eager;       // wide pass with the first chunk (FAST) instead of at the first later list pass
+    int first_sub;     // sorted-segment corner frames: first chunk cut at one sub-chunk (kSubChunk keys)
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 

@@ -577,6 +577,8 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         s.seghead = q.seghead;
         s.nseg = q.nseg;
     }
+    s.first_sub = 1;
+    if (const char *e = std::getenv("FD_FIRST_SUB")) s.first_sub = std::atoi(e) != 0;  // (A/B switch)
     static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
         FD_HIP_TRY(c, ensure(c, c->dbg, sizeof(uint64_t) * 32 * batch));

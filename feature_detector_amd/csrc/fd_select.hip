@@ -55,6 +55,18 @@ typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));  // packed (x, y) of
         if (a.stamps && threadIdx.x == 0) L.st[(slot)] += (v);                          \
     } while (0)
 
+// n / d for quotients < 2^16 (every decode here: rows, cols, grid coordinates <= 65535) from the float
+// reciprocal of d and one correction each way: the float estimate is within 2^16 * 2^-22 < 1 of n/d,
+// so its truncation is off by at most one. (The integer division sequence costs ~30 instructions per
+// division, three per decoded key.)
+__device__ __forceinline__ uint32_t udiv16q(uint32_t n, uint32_t d, float rcp) {
+    uint32_t q = static_cast<uint32_t>(static_cast<float>(n) * rcp);
+    const int32_t r = static_cast<int32_t>(n - q * d);
+    if (r < 0) --q;
+    else if (r >= static_cast<int32_t>(d)) ++q;
+    return q;
+}
+
 // Selection key of a candidate: the response through the frame's key map (order-preserving,
 // injective on the candidates' response range; see SelectArgs::key_base), then ~idx so that equal
 // responses order by ascending raster index.
@@ -685,7 +697,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // First chunk from the sorted segments (PointsArgs::segdesc): every workgroup segment of the list
     // is ordered by level-0 bin, descending, so the keys of bins >= lo are a prefix of each segment.
     // T threads per segment read its entries T at a time while the last one read is still >= lo.
-    auto seg_gather = [&](int lo) {
+    auto seg_gather = [&](int lo, uint32_t k32hi) {  // keys of level-0 bins [lo, k32hi >> 20]
         if (tid == 0) {
             gcount = 0;
             L.seg_more[0] = 0;
@@ -696,7 +708,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         const uint32_t k32lo = static_cast<uint32_t>(lo) << 20;
         for (int r = 0;; ++r) {
             bool more = false;
-            bool hit[kSegPer] = {};
+            bool hit[kSegPer] = {}, ge[kSegPer] = {};
             uint64_t kv[kSegPer];
 #pragma unroll
             for (int k = 0; k < kSegPer; ++k) {
@@ -708,9 +720,10 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     const int64_t li = min(static_cast<int64_t>(sd.x) + e, a.list_cap - 1);
                     kv[k] = in ? make_key(lresp[li], lidx[li], a) : 0ull;
                 }
-                hit[k] = in && static_cast<uint32_t>(kv[k] >> 32) >= k32lo;
+                ge[k] = in && static_cast<uint32_t>(kv[k] >> 32) >= k32lo;
+                hit[k] = ge[k] && static_cast<uint32_t>(kv[k] >> 32) <= k32hi;  // (later chunks: skip earlier ones)
             }
-            more = hit[kSegPer - 1] && seg_j == segT - 1;
+            more = ge[kSegPer - 1] && seg_j == segT - 1;
             // one LDS reservation per wave and round for all kSegPer slots
             uint64_t bm[kSegPer];
             uint32_t wtotal = 0;
@@ -751,7 +764,13 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     bool first_ready = false;
     int first_lo = -1;  // the first chunk's cut (the main loop's first search, done here already)
     {
-        const int lo_b = first_le(suf0, 0, kHistBins, 0u, static_cast<uint32_t>(kSelectChunk));
+        // Sorted-segment frames (small, corner detectors) cut the first chunk at one sub-chunk: it is
+        // then ordered in place (no sub-chunk extract), and frames whose greedy runs past it take the
+        // next chunk through the main loop's list pass. FD_FIRST_SUB=0: the old cut (A/B).
+        int lo_b = kHistBins;
+        if (!WIDE && seg_mode && a.first_sub) lo_b = first_le(suf0, 0, kHistBins, 0u, static_cast<uint32_t>(kSubChunk));
+        if (lo_b >= kHistBins)  // (or the top bin alone exceeds a sub-chunk)
+            lo_b = first_le(suf0, 0, kHistBins, 0u, static_cast<uint32_t>(kSelectChunk));
         first_lo = lo_b;
         FD_STAMP(21);
         if (lo_b < kHistBins && suf0[lo_b] > 0) {
@@ -762,7 +781,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 if (tid == 0) gcount = want;
                 __syncthreads();
             } else if (seg_mode && seg_bad == 0) {
-                seg_gather(lo_b);
+                seg_gather(lo_b, 0xFFFFFFFFu);
             } else if (wk && a.wide_eager) {
                 // long scans expected (FAST: scores plus a slowly growing offset crowd the top bins):
                 // the first list pass already collects the bins below the first chunk
@@ -806,7 +825,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         }
         const uint32_t *S = suf(level);
         const uint32_t base = S[hi + 1];
-        const uint32_t lim = static_cast<uint32_t>(kSelectChunk);
+        // (sorted-segment corner frames: chunks of one sub-chunk, each a cheap segment-prefix gather)
+        const uint32_t lim = static_cast<uint32_t>((!WIDE && seg_mode && a.first_sub && seg_bad == 0 && level == 0)
+                                                       ? kSubChunk : kSelectChunk);
         // smallest lo in [0, hi] with S[lo] - base <= lim (S is non-increasing in b)
         // (level 0, top of the histogram: the cut computed for the first chunk above)
         int lo = (level == 0 && hi == kHistBins - 1 && first_lo >= 0) ? first_lo : first_le(S, 0, hi + 1, base, lim);
@@ -851,6 +872,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             if (first_ready && level == 0) {  // gathered before the loop (sup holds it)
                 first_ready = false;
                 if (tid == 0) gcount = cnt;
+            } else if (!WIDE && seg_mode && seg_bad == 0 && level == 0 && !a.pre_keys) {
+                seg_gather(lo, k32hi);  // a later level-0 chunk: from the sorted segments' prefixes
             } else if (level == 0 && (ensure_wide(hi), in_wide(klo))) {
                 wide_pick(klo, khi);
             } else if (in_wide(klo)) {
@@ -893,6 +916,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 atomicOr(&a.status[f], 0x04000000u);
             FD_STAMP(3);  // gather
             const uint32_t s1 = static_cast<uint32_t>(d + 1);
+            const float rcp_cols = 1.0f / static_cast<float>(cols), rcp_s1 = 1.0f / static_cast<float>(s1);
             auto place = [&](int pos, uint64_t sk) {  // decode position, prior mask, grid cell
                 uint32_t idx = a.tie_idx_desc ? static_cast<uint32_t>(sk) : ~static_cast<uint32_t>(sk);
                 bool ok = true;
@@ -901,12 +925,13 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     idx = 0;
                     atomicOr(&a.status[f], 0x80000000u);
                 }
-                const uint32_t y = idx / static_cast<uint32_t>(cols);
+                const uint32_t y = udiv16q(idx, static_cast<uint32_t>(cols), rcp_cols);
                 const uint32_t x = idx - y * static_cast<uint32_t>(cols);
                 if (fmask) ok = (fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u;
                 pxy[pos] = ok ? ((y << 16) | x) : kEmpty;
                 L.pk32[pos] = static_cast<uint32_t>(sk >> 32);
-                if (use_grid) pcell[pos] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
+                if (use_grid)
+                    pcell[pos] = (udiv16q(y, s1, rcp_s1) + 1) * static_cast<uint32_t>(gw2) + (udiv16q(x, s1, rcp_s1) + 1);
             };
             // Sub-chunks of <= kSubChunk keys from the top bins of the superchunk (already in LDS):
             const uint32_t sub_lim = static_cast<uint32_t>((WIDE && a.wide_eager) ? kSubChunkFast : kSubChunk);
