@@ -212,8 +212,9 @@ def kernel_time_ms(torch, fd, frames_pool, kind, thr, reps=50):
 
 
 def run_config(torch, fd, dev, detector, rows, cols, batch, pool, need, dist, pattern, steps, warmup, use_graph,
-               seed, barrier=None):
-    frames_pool = [make_frames(torch, pattern, batch, rows, cols, seed + 7919 * i, dev) for i in range(pool)]
+               seed, barrier=None, ties="raster", frames_pool=None):
+    if frames_pool is None:
+        frames_pool = [make_frames(torch, pattern, batch, rows, cols, seed + 7919 * i, dev) for i in range(pool)]
     thr = THR[detector]
     stride = max(need, 1) + 1
     xy = torch.empty((batch, stride, 2), dtype=torch.float32, device=dev)
@@ -222,10 +223,39 @@ def run_config(torch, fd, dev, detector, rows, cols, batch, pool, need, dist, pa
     ctx.reserve(KIND[detector], batch, rows, cols)
 
     def step(i):
-        fd.detect_points(detector, frames_pool[i % pool], need, dist, thr, out=(xy, cnt), ctx=ctx, ties="raster")
+        fd.detect_points(detector, frames_pool[i % pool], need, dist, thr, out=(xy, cnt), ctx=ctx, ties=ties)
 
     secs, done = timed_graph(torch, step, steps, warmup, use_graph, per_graph=pool, barrier=barrier)
     return secs, done, frames_pool, (xy, cnt)
+
+
+def tie_frames(fd, dev, detector, frames_pool, need, dist):
+    """Frames of a timed pool whose selection scan met equal responses (FD_FRAME_TIES after a raster-order
+    run): only those can differ from the reference's std::sort order, which ties="reference" restores
+    with a host re-selection. Returns (tied frames, frames)."""
+    ctx = fd.default_context(dev.index or 0)
+    tied = total = 0
+    for f in frames_pool:
+        fd.detect_points(detector, f, need, dist, THR[detector], ctx=ctx, ties="raster")
+        st = ctx.frame_status(f.shape[0])
+        tied += int(((st & fd.points.FRAME_TIES) != 0).sum())
+        total += f.shape[0]
+    return tied, total
+
+
+def tie_report(torch, fd, dev, detector, frames_pool, need, dist, steps=10):
+    """The leg's tie count; when nonzero the same workload is also timed with ties="reference"
+    (un-captured: the re-selection reads the status words on the host)."""
+    tied, total = tie_frames(fd, dev, detector, frames_pool, need, dist)
+    rep = {"tie_frames": tied, "frames_checked": total,
+           "timed_order": "raster (equal to the reference order on every frame without FD_FRAME_TIES)"}
+    if tied:
+        b, rows, cols = frames_pool[0].shape
+        secs, done, _, _ = run_config(torch, fd, dev, detector, rows, cols, b, len(frames_pool), need, dist, None,
+                                      steps, 2, False, 0, ties="reference", frames_pool=frames_pool)
+        rep["reference_order_ms_per_step"] = round(secs / done * 1e3, 5)
+        rep["reference_order_mpix_s"] = round(done * b * rows * cols / secs / 1e6, 1)
+    return rep
 
 
 def run_pipelined(torch, fd, dev, detector, rows, cols, need, dist, pattern, seed, nctx=2, pool=16, reps=20):
@@ -306,12 +336,15 @@ def run_config3(torch, fd, dev, seed, batch=64, rows=720, cols=1280, need=200, d
     brief_ms = e0.elapsed_time(e1) / reps
     kp = int(cnt.sum().item())
     px = batch * rows * cols
+    ties = tie_report(torch, fd, dev, "fast", pool, need, dist, steps=4)
+    if "reference_order_ms_per_step" in ties:
+        ties["reference_order_note"] = "detect + select only (no BRIEF)"
     return {
         "workload": f"fast (thr 10) + grid NMS (need {need}, dist {dist}) + BRIEF-256 (half 8, bilinear), "
                     f"{cols}x{rows} gray noise, batch {batch}/GPU (BASELINE configs[2])",
         "mpix_s": round(done * px / secs / 1e6, 1), "ms_per_step": round(secs / done * 1e3, 4),
         "keypoints_per_step": kp, "brief_kernel_ms": round(brief_ms, 4),
-        "brief_keypoints_per_s": round(kp / (brief_ms * 1e-3), 1),
+        "brief_keypoints_per_s": round(kp / (brief_ms * 1e-3), 1), "ties": ties,
     }
 
 
@@ -670,6 +703,7 @@ def main():
     traffic, traffic_src = (measured_traffic("bench_k_corner") if (args.detector == "harris" and args.rows == 480
                                                                      and args.cols == 640 and args.batch == 1)
                             else (None, None))
+    ties_headline = tie_report(torch, fd, dev, args.detector, pool, args.need, args.dist)
     roofline = {"kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "bytes_per_launch": k_bytes, "avg_launch_ms": round(k_ms, 5), "note": dominant_note}
@@ -690,6 +724,7 @@ def main():
                    "parallelism": f"frame-sharded x{world} (no collective)", "graph": not args.no_graph},
         "roofline": roofline,
         "kernels": kernels,
+        "ties": ties_headline,
     }
     if args.batch == 1 and not args.no_graph:
         with phase(torch, "headline_pipelined"):
@@ -710,6 +745,8 @@ def main():
                                           10, 2, False, seed=99 + rank)
         with phase(torch, "north_star_kernel"):
             kms = kernel_time_ms(torch, fd, pool2, "shi_tomasi", 40.0, reps=10)
+        with phase(torch, "north_star_ties"):
+            ties_ns = tie_report(torch, fd, dev, "shi_tomasi", pool2, 200, 20, steps=4)
         del pool2
         with phase(torch, "north_star_kernel_checker"):
             pool3 = [make_frames(torch, "checker", ns_batch, 1080, 1920, 199 + rank + 7919 * i, dev) for i in range(2)]
@@ -727,6 +764,7 @@ def main():
                          "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb,
                          "traffic": measured_traffic("northstar_k_corner")[0]},
             "issue": north_star_issue(),
+            "ties": ties_ns,
         }
 
     # ---- BASELINE configs[2]: FAST-12 + BRIEF-256, 1280x720 batch 64 (detect -> describe on device) --

@@ -6,12 +6,12 @@ Layers:
   feature_detector_amd      Python batch API over the C ABI (this package), used by tests and bench.py
 """
 from ._lib import FD_FAST, FD_HARRIS, FD_SHI_TOMASI, FdError, LIB_PATH, load  # noqa: F401
-from .points import Context, DetectResult, default_context, detect_points, lsd_lines, lsd_map, point_candidates, point_response  # noqa: F401
+from .points import Context, DetectResult, default_context, detect_points, lsd_lines, lsd_map, point_candidates, point_response, select_points  # noqa: F401
 from .descriptor import brief_compute, to_float, unpack_bits  # noqa: F401
 from .ingest import Ingest, load_png, png_frames, png_info  # noqa: F401
 
 __all__ = [
     "FD_HARRIS", "FD_SHI_TOMASI", "FD_FAST", "FdError", "Context", "DetectResult", "default_context",
-    "detect_points", "point_candidates", "point_response", "lsd_map", "lsd_lines", "load", "brief_compute", "unpack_bits",
+    "detect_points", "point_candidates", "point_response", "select_points", "lsd_map", "lsd_lines", "load", "brief_compute", "unpack_bits",
     "to_float", "Ingest", "load_png", "png_frames", "png_info",
 ]

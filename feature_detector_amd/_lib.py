@@ -17,7 +17,7 @@ EXPORTS = (
     "fd_ctx_create", "fd_ctx_destroy", "fd_last_error", "fd_ctx_set_stream", "fd_ctx_use_own_stream",
     "fd_ctx_get_stream",
     "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_ctx_set_tie_order", "fd_ctx_frame_status", "fd_points_detect", "fd_points_candidates", "fd_points_response",
-    "fd_points_response_append",
+    "fd_points_response_append", "fd_points_select",
     "fd_lsd_map", "fd_lsd_lines", "fd_lsd_lines_state", "fd_brief_compute", "fd_nn_select", "fd_nn_descriptors",
     "fd_build_info", "fd_png_info", "fd_png_decode", "fd_png_frames",
     "fd_ingest_create", "fd_ingest_destroy", "fd_ingest_frames", "fd_ingest_submit", "fd_ingest_wait",
@@ -91,6 +91,8 @@ def load() -> ctypes.CDLL:
                                    P, i32]),
         "fd_points_candidates": (i32, [P, i32, P, i32, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, P, P, P,
                                        i64, P, P, i32]),
+        "fd_points_select": (i32, [P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, P, P, i64, i32, P, P, u32,
+                                   P, i32, P, i32]),
         "fd_points_response": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
         "fd_points_response_append": (i32, [P, i32, P, i32, i32, i32, ctypes.POINTER(fd_point_opts), P, P, i64, P]),
         "fd_lsd_map": (i32, [P, P, i32, i32, i32, i32, f32, P, P, P, P, i64, P, i32]),

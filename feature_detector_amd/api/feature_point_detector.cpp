@@ -67,6 +67,7 @@ bool FeaturePointDetector::Fail(const std::string &what) {
 bool FeaturePointDetector::DetectGoodFeatures(const GrayImage &image, const uint32_t needed_feature_num,
                                               std::vector<Vec2> &features) {
     if (image.data() == nullptr) return false;  // RETURN_FALSE_IF(image.data() == nullptr) (:9)
+    if (KindId() < 0) return DetectWithOwnCandidates(image, needed_feature_num, features);
     fd_ctx *ctx = Context();
     if (!ctx) return Fail("no device context");
     const int32_t rows = image.rows(), cols = image.cols();
@@ -105,9 +106,68 @@ bool FeaturePointDetector::DetectGoodFeatures(const GrayImage &image, const uint
     return true;
 }
 
-// ComputeCandidates seam (feature_point_detector.h:44): raster-ordered candidates of the staged frame.
+// DetectGoodFeatures (:7-25) for a subclass with its own ComputeCandidates: the mask state of :12-16
+// (materialised on access), the subclass's candidates (:19-20), then SelectGoodFeatures (:23, :54-74)
+// on the GPU over them (fd_points_select, in the order they were pushed).
+bool FeaturePointDetector::DetectWithOwnCandidates(const GrayImage &image, const uint32_t needed_feature_num,
+                                                   std::vector<Vec2> &features) {
+    fd_ctx *ctx = Context();
+    if (!ctx) return Fail("no device context");
+    const int32_t rows = image.rows(), cols = image.cols();
+    last_prior_ = features;
+    last_new_.clear();
+    last_rows_ = rows;
+    last_cols_ = cols;
+    last_options_ = options_;
+    last_reached_need_ = false;
+    staged_frame_ = nullptr;
+    mask_valid_ = false;
+    candidates_.clear();
+    candidates_valid_ = true;
+    candidates_sorted_ = true;
+    if (!ComputeCandidates(image)) return false;  // RETURN_FALSE_IF_FALSE (:20)
+    candidates_valid_ = true;
+    candidates_sorted_ = false;
+    if (candidates_.empty()) return true;  // RETURN_TRUE_IF(candidates_.empty()) (:55)
+
+    const size_t n = candidates_.size();
+    std::vector<float> resp(n);
+    std::vector<int32_t> xs(n), ys(n);
+    for (size_t i = 0; i < n; ++i) {
+        resp[i] = candidates_[i].first;
+        xs[i] = candidates_[i].second.x();
+        ys[i] = candidates_[i].second.y();
+    }
+    std::vector<float> prior(2 * features.size());
+    for (size_t i = 0; i < features.size(); ++i) {
+        prior[2 * i] = features[i].x();
+        prior[2 * i + 1] = features[i].y();
+    }
+    const int32_t nprior = static_cast<int32_t>(features.size());
+    const fd_point_opts opts{options_.kMinFeatureDistance, options_.kMinValidResponse};
+    const int32_t stride = static_cast<int32_t>(std::max<uint32_t>(needed_feature_num, 1u)) + 1;
+    std::vector<float> out(2 * static_cast<size_t>(stride));
+    const int64_t count_in = static_cast<int64_t>(n);
+    int32_t count = 0;
+    const int rc = fd_points_select(ctx, 1, rows, cols, &opts, resp.data(), xs.data(), ys.data(), &count_in, count_in,
+                                    0, nprior ? prior.data() : nullptr, nprior ? &nprior : nullptr, needed_feature_num,
+                                    out.data(), stride, &count, 0);
+    if (rc != FD_OK) return Fail("fd_points_select");
+    for (int32_t i = 0; i < count; ++i) {
+        features.emplace_back(Vec2(out[2 * i], out[2 * i + 1]));
+        last_new_.emplace_back(Vec2(out[2 * i], out[2 * i + 1]));
+    }
+    last_reached_need_ = count > 0 && features.size() >= needed_feature_num;
+    mask_valid_ = false;
+    return true;
+}
+
+// ComputeCandidates seam (feature_point_detector.h:44) of the built-in kinds: raster-ordered
+// candidates of the staged frame. A subclass without a kind and without its own ComputeCandidates
+// has no candidates: false, as the reference's pure virtual would not have compiled.
 bool FeaturePointDetector::ComputeCandidates(const GrayImage & /*image*/) {
     candidates_.clear();
+    if (KindId() < 0) return Fail("ComputeCandidates is not overridden and KindId() names no built-in detector");
     if (!staged_frame_ || !ctx_) return false;
     const int64_t cap = static_cast<int64_t>(last_rows_) * last_cols_ / (KindId() == FD_FAST ? 1 : 2) + 16;
     std::vector<float> resp(static_cast<size_t>(cap));
@@ -131,14 +191,18 @@ bool FeaturePointDetector::ComputeCandidates(const GrayImage & /*image*/) {
 
 void FeaturePointDetector::Materialise() const {
     auto *self = const_cast<FeaturePointDetector *>(this);
+    // The reference leaves candidates_ sorted by its unstable std::sort (:58-60).
+    auto sort_ref = [this]() {
+        std::sort(candidates_.begin(), candidates_.end(),
+                  [](const std::pair<float, Pixel> &a, const std::pair<float, Pixel> &b) { return a.first > b.first; });
+    };
     if (!candidates_valid_) {
         candidates_valid_ = true;
         GrayImage none;
-        if (self->ComputeCandidates(none)) {
-            // The reference leaves candidates_ sorted by its unstable std::sort (:58-60).
-            std::sort(candidates_.begin(), candidates_.end(),
-                      [](const std::pair<float, Pixel> &a, const std::pair<float, Pixel> &b) { return a.first > b.first; });
-        }
+        if (self->ComputeCandidates(none)) sort_ref();
+    } else if (!candidates_sorted_) {
+        candidates_sorted_ = true;
+        sort_ref();
     }
     if (!mask_valid_) {
         mask_valid_ = true;

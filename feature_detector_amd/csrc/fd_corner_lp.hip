@@ -346,8 +346,10 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
                 const int ri = y0 - 3 + i0 + t;
                 lp_load_row<PX, ALIGNED>(ring[(t + 3) % 6], rs, (ri + 3) * cols + c0);
                 const uint32_t(&P_s)[NW] = ring[t];
+#if !FD_LP_FP
                 const uint32_t(&P_su)[NW] = ring[(t + 4) % 6];
                 const uint32_t(&P_sc)[NW] = ring[(t + 5) % 6];
+#endif
 
 #if FD_LP_FP
                 // row ri as floats (each row is converted once and used at three steps)

@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) void k_rgb_gray(const uint8_t *src, uint8_t *d
     if (p0 >= npx) return;
     const auto rs = make_rsrc(src, static_cast<uint32_t>(npx * C));  // (npx * C < 2^32: checked on the host)
     uint32_t out = 0;
-    if (p0 + 4 <= npx && (reinterpret_cast<uintptr_t>(src) & 3) == 0) {
+    if (p0 + 4 <= npx && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
         uint32_t w[C];
 #pragma unroll
         for (int k = 0; k < C; ++k) w[k] = buf_load_u32(rs, static_cast<int32_t>(p0 * C + 4 * k));
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(256) void k_rgb_gray(const uint8_t *src, uint8_t *d
             const uint32_t v = C <= 2 ? byte(m * C) : gray_of(byte(m * C), byte(m * C + 1), byte(m * C + 2));
             out |= v << (8 * m);
         }
-        *reinterpret_cast<uint32_t *>(dst + p0) = out;  // (dst is the frame buffer: 4-byte aligned quads)
+        *reinterpret_cast<uint32_t *>(dst + p0) = out;
         return;
     }
     for (int m = 0; m < 4 && p0 + m < npx; ++m) {

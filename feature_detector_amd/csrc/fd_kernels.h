@@ -116,6 +116,7 @@ struct SelectArgs {
     uint64_t *wide_keys;  // [batch][kWideKeys] scratch of the wide pass, or null (one list pass per chunk)
     int wide_eager;       // wide pass with the first chunk (FAST) instead of at the first later list pass
     int first_sub;     // sorted-segment corner frames: first chunk cut at one sub-chunk (kSubChunk keys)
+    int grid_at_d0;    // distance 0 still tests the grid (1-pixel cells): caller lists may name a pixel twice
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 
@@ -126,6 +127,23 @@ struct OrderedArgs {
     const int64_t *offset;  // [n_frames] start of frame j's run in `order`
     const uint32_t *count;  // [n_frames] its length
     const int32_t *frame;   // [n_frames] frame index (into SelectArgs' per-frame arrays)
+};
+
+// fd_points_select: caller candidates (response, x, y at [f * stride], counts[f]) -> list format.
+struct CandInArgs {
+    const float *resp;
+    const int32_t *x, *y;
+    const int64_t *counts;  // [batch] (device)
+    int64_t stride;
+    int batch, rows, cols;
+    float *list_resp;
+    uint32_t *list_idx;
+    int64_t list_cap;
+    uint32_t *list_count;
+    uint32_t *hist0;
+    uint32_t key_base;
+    int key_lz;
+    uint32_t *bad;  // [batch] bit 31: a candidate outside the frame, a NaN response or a bad count
 };
 
 struct CompactArgs {
@@ -215,6 +233,7 @@ hipError_t launch_corner_lp_any(int kind, const PointsArgs &a, hipStream_t s);  
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s);
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
 hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);
+hipError_t launch_cand_lists(const CandInArgs &a, int64_t max_count, hipStream_t s);
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
 hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s);    // compact mode: map (counts, row bits) + scans

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <memory>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -73,9 +74,11 @@ class FrameLines {
 public:
     FrameLines(int rows, int cols, const fd_lsd_opts &o)
         : pc_(cols - 1), words_((static_cast<int64_t>(rows - 1) * (cols - 1) + 63) / 64), o_(o),
-          min_region_(min_region_size(rows, cols, o.min_tolerance_angle_residual_rad)) {
-        entry_of_.resize(static_cast<size_t>(rows - 1) * (cols - 1));
-        mask_.resize(static_cast<size_t>(words_));
+          min_region_(min_region_size(rows, cols, o.min_tolerance_angle_residual_rad)),
+          // read only where the frame's mask bit is set, i.e. after load() wrote it: left uninitialised
+          // (a map-sized zero fill per worker per call cost more than the sparse frames touch)
+          entry_of_(new int32_t[static_cast<size_t>(rows - 1) * (cols - 1)]) {
+        mask_.assign(static_cast<size_t>(words_), 0ull);
     }
 
     // One frame: returns the number of rectangles (writes at most stride of them).
@@ -102,12 +105,12 @@ public:
         }
         if (used_out)
             for (int64_t k = 0; k < fl.n; ++k) used_out[k] = (state_[k] & kUsed) ? 1 : 0;
+        for (int64_t k = 0; k < fl.n; ++k) mask_[static_cast<size_t>(fl.idx[k]) >> 6] = 0ull;  // clean for the next frame
         return nrect;
     }
 
 private:
     void load(const FrameList &fl) {
-        std::fill(mask_.begin(), mask_.end(), 0ull);
         const size_t n = static_cast<size_t>(fl.n);
         state_.assign(n, 0);
         row_.resize(n);
@@ -240,7 +243,7 @@ private:
     const int64_t words_;
     const fd_lsd_opts o_;
     const uint32_t min_region_;
-    std::vector<int32_t> entry_of_;
+    std::unique_ptr<int32_t[]> entry_of_;
     std::vector<uint64_t> mask_;
     std::vector<uint8_t> state_;
     std::vector<int32_t> row_, col_;

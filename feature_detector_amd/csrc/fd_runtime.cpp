@@ -418,6 +418,8 @@ struct SelectCall {
     const uint2 *segdesc = nullptr;  // sorted segments of the candidate kernel (PointsArgs::segdesc)
     const uint64_t *seghead = nullptr;
     int nseg = 0;
+    bool push_order = false;  // lists hold the caller's push order (fd_points_select), not raster order
+    const char *value_msg = "a value above the declared maximum (fd_nn_opts::max_response)";
 };
 
 // Sorted-segment lists (PointsArgs::segdesc): for launches small enough that k_select can give every
@@ -442,7 +444,7 @@ std::string hex(uint32_t v) {
 // (the order ComputeCandidates pushes them, feature_point_harris_detector.cpp:120-137,
 // feature_point_fast_detector.cpp:83-98), sorted here with std::sort and the reference comparator,
 // and the resulting visiting order goes back to the GPU for the greedy pass (k_select_ordered).
-int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb) {
+int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb, bool push_order) {
     // The status read below synchronises the stream, which a stream being captured into a graph cannot
     // do (and the host sort could not be replayed): refuse before touching the capture.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -485,8 +487,10 @@ int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb) 
         std::vector<Cand> &v = lists[j];
         v.resize(resp[j].size());
         for (size_t i = 0; i < v.size(); ++i) v[i] = {resp[j][i], idx[j][i]};
-        // raster order (indices are unique), then the reference's sort (:58-60)
-        std::sort(v.begin(), v.end(), [](const Cand &a, const Cand &b) { return a.idx < b.idx; });
+        // the order ComputeCandidates pushed them in -- raster order for the built-in detectors (their
+        // indices are unique; the lists are unordered), the list order for caller-supplied candidates
+        // (fd_points_select keeps it) -- then the reference's sort (:58-60)
+        if (!push_order) std::sort(v.begin(), v.end(), [](const Cand &a, const Cand &b) { return a.idx < b.idx; });
         std::sort(v.begin(), v.end(), [](const Cand &a, const Cand &b) { return a.resp > b.resp; });
         offset[j] = static_cast<int64_t>(order.size());
         count[j] = static_cast<uint32_t>(v.size());
@@ -533,7 +537,8 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.prior_counts = pi.counts_dev;
     s.need = q.need;
     s.dist = q.dist;
-    if (s.dist >= 1) {
+    s.grid_at_d0 = q.push_order ? 1 : 0;  // caller lists may name a pixel twice: distance 0 tests it
+    if (s.dist >= 1 || (s.dist == 0 && s.grid_at_d0)) {
         s.grid_w = (cols + s.dist) / (s.dist + 1);
         s.grid_h = (rows + s.dist) / (s.dist + 1);
         const int64_t cells = static_cast<int64_t>(s.grid_w + 2) * (s.grid_h + 2);  // bordered grid
@@ -623,7 +628,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         }
     }
     if (c->tie_order == FD_TIES_REFERENCE && !q.tie_idx_desc) {
-        const int rc = resolve_ties(c, s, batch, sb);
+        const int rc = resolve_ties(c, s, batch, sb, q.push_order);
         if (rc) return rc;
     }
     if (!outputs_on_device) {
@@ -635,8 +640,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         for (int b = 0; b < batch; ++b) {
             if (st[b] & FD_FRAME_VALUE_RANGE)
-                return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": a value above the declared maximum "
-                                               "(fd_nn_opts::max_response)");
+                return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": " + q.value_msg);
             if (st[b] & FD_FRAME_GUARD)
                 return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (status 0x" + hex(st[b]) +
                                                ", frame " + std::to_string(b) + ")");
@@ -920,6 +924,98 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     sc.nseg = g.blocks_per_frame;
     sc.wide_eager = kind == FD_FAST;
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
+}
+
+// SelectGoodFeatures (feature_point_detector.cpp:54-88) over caller-supplied candidates (the
+// ComputeCandidates seam, :20): k_cand_lists puts them into the selection's list format (push order
+// kept), then the same k_select as fd_points_detect, with the full float order as key map.
+int fd_points_select(fd_ctx *c, int batch, int rows, int cols, const fd_point_opts *opts, const float *cand_resp,
+                     const int32_t *cand_x, const int32_t *cand_y, const int64_t *cand_counts, int64_t cand_cap,
+                     int cands_on_device, const float *prior_xy, const int32_t *prior_counts, uint32_t need,
+                     float *out_xy, int32_t out_stride, int32_t *out_counts, int outputs_on_device) {
+    int rc = check_shape(c, FD_HARRIS, batch, rows, cols);
+    if (rc) return rc;
+    if (!opts || !out_xy || !out_counts || out_stride < 1) return fail(c, FD_ERR_INVALID, "bad output arguments");
+    if (!cand_counts || cand_cap < 0 || cand_cap > 0xFFFFFFFFll)
+        return fail(c, FD_ERR_INVALID, "cand_counts is NULL or cand_cap out of range");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    int64_t max_n = cand_cap;
+    if (!cands_on_device) {
+        max_n = 0;
+        for (int b = 0; b < batch; ++b) {
+            if (cand_counts[b] < 0 || cand_counts[b] > cand_cap)
+                return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": candidate count outside [0, cand_cap]");
+            max_n = std::max(max_n, cand_counts[b]);
+        }
+    }
+    if (max_n > 0 && (!cand_resp || !cand_x || !cand_y)) return fail(c, FD_ERR_INVALID, "candidate arrays are NULL");
+    PriorInfo pi;
+    rc = setup_priors(c, batch, rows, cols, opts->min_feature_distance, prior_xy, prior_counts, pi);
+    if (rc) return rc;
+    const int64_t cap = std::max<int64_t>(max_n, 64);
+    SelectBufs sb{};
+    rc = select_buffers(c, batch, cap, sb);
+    if (rc) return rc;
+    fdk::CandInArgs a{};
+    a.stride = cands_on_device ? cand_cap : max_n;
+    if (cands_on_device) {
+        a.resp = cand_resp;
+        a.x = cand_x;
+        a.y = cand_y;
+        a.counts = cand_counts;
+    } else {  // pack the frames' lists at stride max_n
+        const size_t tot = static_cast<size_t>(batch) * static_cast<size_t>(std::max<int64_t>(max_n, 1));
+        FD_HIP_TRY(c, ensure(c, c->c_resp, sizeof(float) * tot));
+        FD_HIP_TRY(c, ensure(c, c->c_x, sizeof(int32_t) * tot));
+        FD_HIP_TRY(c, ensure(c, c->c_y, sizeof(int32_t) * tot));
+        FD_HIP_TRY(c, ensure(c, c->c_counts, sizeof(int64_t) * batch));
+        for (int b = 0; b < batch; ++b) {
+            const size_t n = static_cast<size_t>(cand_counts[b]);
+            if (n == 0) continue;
+            const size_t src = static_cast<size_t>(b) * static_cast<size_t>(cand_cap);
+            const size_t dst = static_cast<size_t>(b) * static_cast<size_t>(max_n);
+            FD_HIP_TRY(c, hipMemcpyAsync(as<float>(c->c_resp) + dst, cand_resp + src, sizeof(float) * n,
+                                         hipMemcpyHostToDevice, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(as<int32_t>(c->c_x) + dst, cand_x + src, sizeof(int32_t) * n,
+                                         hipMemcpyHostToDevice, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(as<int32_t>(c->c_y) + dst, cand_y + src, sizeof(int32_t) * n,
+                                         hipMemcpyHostToDevice, c->stream));
+        }
+        FD_HIP_TRY(c, hipMemcpyAsync(c->c_counts.p, cand_counts, sizeof(int64_t) * batch, hipMemcpyHostToDevice,
+                                     c->stream));
+        a.resp = as<float>(c->c_resp);
+        a.x = as<int32_t>(c->c_x);
+        a.y = as<int32_t>(c->c_y);
+        a.counts = as<int64_t>(c->c_counts);
+    }
+    a.batch = batch;
+    a.rows = rows;
+    a.cols = cols;
+    a.list_resp = as<float>(c->list_resp);
+    a.list_idx = as<uint32_t>(c->list_idx);
+    a.list_cap = cap;
+    a.list_count = sb.list_count;
+    a.hist0 = sb.hist0;
+    // any float: keys from float_key(-inf) - 1 (never 0) to float_key(+inf), the whole 32-bit range
+    a.key_base = host_float_key(-std::numeric_limits<float>::infinity()) - 1u;
+    a.key_lz = 0;
+    a.bad = sb.pre_count;
+    c->sel_dirty = true;  // until k_select is enqueued: it resets the control block
+    FD_HIP_TRY(c, fdk::launch_cand_lists(a, max_n, c->stream));
+    if (!cands_on_device) FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // caller's host arrays were the sources
+    SelectCall sc{};
+    sc.batch = batch;
+    sc.rows = rows;
+    sc.cols = cols;
+    sc.dist = opts->min_feature_distance;
+    sc.need = need;
+    sc.cap = cap;
+    sc.key_base = a.key_base;
+    sc.key_lz = a.key_lz;
+    sc.value_flag = true;
+    sc.push_order = true;
+    sc.value_msg = "a candidate outside the frame, a NaN response or a bad candidate count";
+    return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, 1);
 }
 
 static int points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch, int rows, int cols,

@@ -363,7 +363,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
     const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
     const int d = a.dist;
-    const bool use_grid = d >= 1;
+    const bool use_grid = d >= 1 || (d == 0 && a.grid_at_d0);
     // Occupancy grid of (d+1)-sized cells with a one-cell border (no bounds checks in the scan).
     const int gw2 = a.grid_w + 2;
     const int cells = gw2 * (a.grid_h + 2);
@@ -1243,7 +1243,7 @@ __global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs
     const uint32_t *ord = o.order + o.offset[j];
     const int64_t n = o.count[j];
     const int rows = a.rows, cols = a.cols, d = a.dist;
-    const bool use_grid = d >= 1;
+    const bool use_grid = d >= 1 || (d == 0 && a.grid_at_d0);
     const int gw2 = a.grid_w + 2;
     const int cells = gw2 * (a.grid_h + 2);
     const bool grid_in_lds = cells <= kGridLdsCells;

@@ -107,6 +107,10 @@ def png_frames(images, threads: int = 0, ctx: Context | None = None, out=None):
     n = len(images)
     if out is None:
         out = torch.empty((n, rows, cols), dtype=torch.uint8, device=f"cuda:{ctx.device}")
+    elif (tuple(out.shape) != (n, rows, cols) or out.dtype != torch.uint8 or out.device.type != "cuda"
+          or out.device.index != ctx.device or not out.is_contiguous()):
+        raise ValueError(f"png_frames: out must be a contiguous uint8 cuda:{ctx.device} tensor of shape "
+                         f"{(n, rows, cols)}, got {tuple(out.shape)} {out.dtype} on {out.device}")
     bufs = (ctypes.c_char_p * n)(*images)
     lens = (ctypes.c_size_t * n)(*[len(x) for x in images])
     rc = _lib.load().fd_png_frames(ctx.ptr, ctypes.cast(bufs, ctypes.c_void_p), ctypes.cast(lens, ctypes.c_void_p), n,

@@ -248,6 +248,80 @@ def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_v
     return DetectResult(xy, cnt, status)
 
 
+def select_points(candidates, rows: int, cols: int, need: int, min_feature_distance: int = 15, prior=None,
+                  ties: str | None = None, ctx: Context | None = None, out=None) -> DetectResult:
+    """SelectGoodFeatures over caller-supplied candidates (fd_points_select): the ComputeCandidates
+    seam of a detector whose candidates come from elsewhere (feature_point_detector.h:44).
+
+    candidates: a list (per frame) of (resp, x, y) arrays in the order they were pushed -- host
+    arrays, returns numpy results (ties default "reference"); or a tuple of torch device tensors
+    (resp [B, cap] float32, x [B, cap] int32, y [B, cap] int32, counts [B] int64), returns device
+    tensors asynchronously (ties default "raster"; `out` as in detect_points).
+    """
+    opts = fd_point_opts(int(min_feature_distance), 0.0)
+    L = _lib.load()
+    if isinstance(candidates, tuple) and hasattr(candidates[0], "data_ptr"):
+        import torch
+
+        resp, xs, ys, counts = candidates
+        b, cap = resp.shape
+        for t, dt in ((resp, torch.float32), (xs, torch.int32), (ys, torch.int32)):
+            if t.dtype != dt or tuple(t.shape) != (b, cap) or not t.is_cuda or not t.is_contiguous():
+                raise ValueError("device candidates: contiguous resp f32 / x, y int32 [B, cap] tensors")
+        if counts.dtype != torch.int64 or tuple(counts.shape) != (b,) or not counts.is_cuda:
+            raise ValueError("device candidates: counts int64 [B]")
+        ctx = _resolve_ctx(ctx, resp)
+        _bind_stream(ctx, True)
+        ctx.set_tie_order(ties or "raster")
+        pxy, pcnt, _keep2 = _priors(prior, b)
+        stride = max(int(need), 1) + 1
+        status = None
+        if out is None:
+            xy = torch.empty((b, stride, 2), dtype=torch.float32, device=resp.device)
+            cnt = torch.empty((b,), dtype=torch.int32, device=resp.device)
+            status = torch.empty((b,), dtype=torch.int32, device=resp.device)
+        else:
+            xy, cnt = out[0], out[1]
+            status = out[2] if len(out) > 2 else None
+            stride = xy.shape[1]
+        rc = L.fd_points_select(ctx.ptr, b, rows, cols, ctypes.byref(opts), ctypes.c_void_p(resp.data_ptr()),
+                                ctypes.c_void_p(xs.data_ptr()), ctypes.c_void_p(ys.data_ptr()),
+                                ctypes.c_void_p(counts.data_ptr()), int(cap), 1,
+                                ctypes.c_void_p(pxy.ctypes.data) if pxy is not None else None,
+                                ctypes.c_void_p(pcnt.ctypes.data) if pcnt is not None else None,
+                                int(need), ctypes.c_void_p(xy.data_ptr()), stride, ctypes.c_void_p(cnt.data_ptr()), 1)
+        _lib.check(ctx.ptr, rc)
+        if status is not None:
+            ctx.frame_status(b, out=status)
+        return DetectResult(xy, cnt, status)
+    b = len(candidates)
+    counts = np.array([len(c[0]) for c in candidates], np.int64)
+    cap = max(int(counts.max()) if b else 0, 1)
+    resp = np.zeros((b, cap), np.float32)
+    xs = np.zeros((b, cap), np.int32)
+    ys = np.zeros((b, cap), np.int32)
+    for i, (r_, x_, y_) in enumerate(candidates):
+        n = counts[i]
+        if len(x_) != n or len(y_) != n:
+            raise ValueError(f"frame {i}: resp, x and y differ in length")
+        resp[i, :n], xs[i, :n], ys[i, :n] = r_, x_, y_
+    ctx = _resolve_ctx(ctx)
+    _bind_stream(ctx, False)
+    ctx.set_tie_order(ties or "reference")
+    pxy, pcnt, _keep2 = _priors(prior, b)
+    stride = max(int(need), 1) + 1
+    xy = np.zeros((b, stride, 2), np.float32)
+    cnt = np.zeros((b,), np.int32)
+    rc = L.fd_points_select(ctx.ptr, b, rows, cols, ctypes.byref(opts), ctypes.c_void_p(resp.ctypes.data),
+                            ctypes.c_void_p(xs.ctypes.data), ctypes.c_void_p(ys.ctypes.data),
+                            ctypes.c_void_p(counts.ctypes.data), cap, 0,
+                            ctypes.c_void_p(pxy.ctypes.data) if pxy is not None else None,
+                            ctypes.c_void_p(pcnt.ctypes.data) if pcnt is not None else None,
+                            int(need), ctypes.c_void_p(xy.ctypes.data), stride, ctypes.c_void_p(cnt.ctypes.data), 0)
+    _lib.check(ctx.ptr, rc)
+    return DetectResult(xy, cnt, ctx.frame_status(b))
+
+
 def point_response(kind, frames, min_valid_response: float = 0.1, out=None, ctx: Context | None = None,
                    append: bool = False):
     """The per-pixel stage alone (fd_points_response) on torch device frames [B, R, C].

@@ -135,6 +135,26 @@ int fd_points_candidates(fd_ctx *ctx, int kind, const uint8_t *frames, int frame
                          float *out_response_map, int outputs_on_device);
 
 /*
+ * fd_points_select -- SelectGoodFeatures (feature_point_detector.cpp:54-88) over caller-supplied
+ * candidates: the ComputeCandidates seam (feature_point_detector.h:44, called at
+ * feature_point_detector.cpp:20) for a FeaturePointDetector subclass whose candidates come from
+ * elsewhere. Frame b's candidates are (cand_resp, cand_x, cand_y)[b * cand_cap + i], i < cand_counts[b],
+ * in the order ComputeCandidates pushed them; fd_points_candidates' outputs can be passed as they are.
+ * Mask from the prior features as fd_points_detect (:12-16, :90-98); then sort by response and greedy
+ * min-distance scan (the reference's SelectGoodFeatures does not filter by min_valid_response, and
+ * neither does this call). Equal responses as fd_ctx_set_tie_order says: FD_TIES_RASTER orders them
+ * by raster index, FD_TIES_REFERENCE by libstdc++'s std::sort of the pushed order. A pixel may be
+ * listed more than once. Every candidate must lie in the frame and have a non-NaN response
+ * (host outputs: FD_ERR_INVALID; device outputs: FD_FRAME_VALUE_RANGE in fd_ctx_frame_status).
+ * cand_* and cand_counts are device pointers when cands_on_device, host pointers otherwise;
+ * out_xy / out_counts as fd_points_detect.
+ */
+int fd_points_select(fd_ctx *ctx, int batch, int rows, int cols, const fd_point_opts *opts, const float *cand_resp,
+                     const int32_t *cand_x, const int32_t *cand_y, const int64_t *cand_counts, int64_t cand_cap,
+                     int cands_on_device, const float *prior_xy, const int32_t *prior_counts, uint32_t need,
+                     float *out_xy, int32_t out_stride, int32_t *out_counts, int outputs_on_device);
+
+/*
  * fd_points_response -- the per-pixel stage alone (response + NMS for Harris/Shi-Tomasi, segment test
  * + offset for FAST), i.e. ComputeCandidates without ordering: per frame, the candidates' responses
  * at out_resp[b * cand_cap] and raster indices (row * cols + col) at out_idx[b * cand_cap], in

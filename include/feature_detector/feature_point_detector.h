@@ -2,10 +2,16 @@
 // (src/feature_point_detector/feature_point_detector.h:12-53 and the subclass headers), backed by the
 // MI355X kernels of libfdhip.so through the C ABI in include/fd_hip.h.
 //
-// DetectGoodFeatures runs the whole call on the GPU (mask, candidates, ordering, greedy selection).
-// candidates() and mask() are materialised on first access after a call: candidates() recomputes the
-// raster-ordered candidates on the GPU and sorts them with the reference's std::sort comparator
-// (feature_point_detector.cpp:58-60), so it holds exactly what the reference leaves there.
+// DetectGoodFeatures keeps the reference's template method (feature_point_detector.cpp:7-25): mask,
+// ComputeCandidates, SelectGoodFeatures. For the built-in detectors (KindId() >= 0) the three run
+// fused on the GPU (fd_points_detect). A subclass that supplies its own candidates overrides
+// ComputeCandidates (pushing (response, pixel) pairs into candidates(), as the reference's subclasses
+// do) and leaves KindId() at kOwnCandidates; its candidates are then selected on the GPU by
+// fd_points_select. candidates() and mask() are materialised on first access after a call:
+// candidates() holds the candidates sorted with the reference's std::sort comparator
+// (feature_point_detector.cpp:58-60), exactly what the reference leaves there (the built-in detectors
+// recompute them on the GPU for that). mask() may be read inside ComputeCandidates (prior boxes,
+// :12-16); edits to it there are not seen by the selection, which builds the same mask on the GPU.
 #ifndef FEATURE_DETECTOR_FEATURE_POINT_DETECTOR_H_
 #define FEATURE_DETECTOR_FEATURE_POINT_DETECTOR_H_
 
@@ -59,15 +65,20 @@ public:
     const std::string &last_error() const { return error_; }
 
 protected:
-    // libfdhip detector kind (FD_HARRIS / FD_SHI_TOMASI / FD_FAST).
-    virtual int KindId() const = 0;
+    // libfdhip detector kind (FD_HARRIS / FD_SHI_TOMASI / FD_FAST): the fused GPU path. The default,
+    // kOwnCandidates, makes DetectGoodFeatures call ComputeCandidates (a subclass of a built-in
+    // detector that overrides ComputeCandidates overrides this too).
+    static constexpr int kOwnCandidates = -1;
+    virtual int KindId() const { return kOwnCandidates; }
     fd_ctx *Context();
     bool Fail(const std::string &what);
 
 private:
-    // The ComputeCandidates seam (feature_point_detector.h:44): fills candidates_ in the order the
-    // reference pushes them (raster order), from the frame staged on the device by the last call.
+    // The ComputeCandidates seam (feature_point_detector.h:44, called at feature_point_detector.cpp:20):
+    // push the image's candidates into candidates() (already cleared). The default serves the
+    // built-in kinds: the raster-ordered candidates of the frame staged by the last call.
     virtual bool ComputeCandidates(const GrayImage &image);
+    bool DetectWithOwnCandidates(const GrayImage &image, uint32_t needed_feature_num, std::vector<Vec2> &features);
     void Materialise() const;
 
 private:
@@ -76,6 +87,7 @@ private:
     mutable MatInt mask_;
     // state of the last DetectGoodFeatures call (for the lazily materialised accessors)
     mutable bool candidates_valid_ = true;
+    mutable bool candidates_sorted_ = true;  // own candidates: sorted (:58-60) on first access
     mutable bool mask_valid_ = true;
     const uint8_t *staged_frame_ = nullptr;  // device copy of the last image (owned by the context)
     int32_t last_rows_ = 0, last_cols_ = 0;

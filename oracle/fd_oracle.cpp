@@ -250,6 +250,34 @@ void orc_fast_offsets(int64_t n, float *out) {
     }
 }
 
+// SelectGoodFeatures (feature_point_detector.cpp:54-74) over `cand` in the order ComputeCandidates
+// pushed them: sort (sort_mode 0: the reference's std::sort; 1: response desc, raster index asc --
+// the HIP path's FD_TIES_RASTER order), then the greedy scan against `mask`. Returns the new features.
+static int SelectGoodFeatures(std::vector<Cand> &cand, std::vector<int32_t> &mask, int rows, int cols, int dist,
+                              uint32_t need, int n_prior, int sort_mode, float *out_xy, int out_cap) {
+    int nout = 0;
+    size_t total = static_cast<size_t>(n_prior);
+    if (cand.empty()) return 0;  // :55
+    if (sort_mode == 1)  // raster order first (a no-op for the built-in detectors' raster-pushed lists)
+        std::stable_sort(cand.begin(), cand.end(), [cols](const Cand &a, const Cand &b) {
+            return static_cast<int64_t>(a.y) * cols + a.x < static_cast<int64_t>(b.y) * cols + b.x;
+        });
+    SortCandidates(cand, sort_mode);
+    for (const Cand &c : cand) {
+        if (mask[static_cast<size_t>(c.y) * cols + c.x]) {
+            if (nout < out_cap) {
+                out_xy[2 * nout] = static_cast<float>(c.x);
+                out_xy[2 * nout + 1] = static_cast<float>(c.y);
+            }
+            ++nout;
+            ++total;
+            if (total >= need) break;  // :67-69 checked after the append
+            DrawBox(mask, rows, cols, dist, c.y, c.x);
+        }
+    }
+    return nout;
+}
+
 // -----------------------------------------------------------------------------------------------------
 // Full FeaturePointDetector::DetectGoodFeatures (feature_point_detector.cpp:7-25) for one frame.
 //   kind: 0 Harris, 1 Shi-Tomasi, 2 FAST.  sort_mode: 0 reference std::sort, 1 stable.
@@ -285,31 +313,34 @@ int64_t orc_detect(int kind, const uint8_t *img, int rows, int cols, int dist, f
             for (int64_t i = 0; i < n; ++i) cand[i] = {r[i], cx[i], cy[i]};
         }
     }
-    // SelectGoodFeatures (:54-74).
-    int nout = 0;
-    size_t total = static_cast<size_t>(n_prior);
-    if (!cand.empty()) {
-        SortCandidates(cand, sort_mode);
-        for (const Cand &c : cand) {
-            if (mask[static_cast<size_t>(c.y) * cols + c.x]) {
-                if (nout < out_cap) {
-                    out_xy[2 * nout] = static_cast<float>(c.x);
-                    out_xy[2 * nout + 1] = static_cast<float>(c.y);
-                }
-                ++nout;
-                ++total;
-                if (total >= need) break;  // :67-69 checked after the append
-                DrawBox(mask, rows, cols, dist, c.y, c.x);
-            }
-        }
-    }
-    *out_n = nout;
+    *out_n = SelectGoodFeatures(cand, mask, rows, cols, dist, need, n_prior, sort_mode, out_xy, out_cap);
     for (size_t i = 0; i < cand.size() && static_cast<int64_t>(i) < cand_cap; ++i) {
         cand_resp[i] = cand[i].response;
         cand_x[i] = cand[i].x;
         cand_y[i] = cand[i].y;
     }
     return static_cast<int64_t>(cand.size());
+}
+
+// SelectGoodFeatures alone over caller-supplied candidates (a subclass's ComputeCandidates, the
+// fd_points_select seam): mask from the prior features (:12-16, :90-98), then the sort and greedy scan
+// of SelectGoodFeatures. Candidates must lie inside the image. Returns the number of new features.
+// sorted_* (nullable, n entries): the candidates as SelectGoodFeatures leaves them sorted (candidates()).
+int orc_select(const float *resp, const int32_t *x, const int32_t *y, int64_t n, int rows, int cols, int dist,
+               uint32_t need, const float *prior_xy, int n_prior, int sort_mode, float *out_xy, int out_cap,
+               float *sorted_resp, int32_t *sorted_x, int32_t *sorted_y) {
+    std::vector<int32_t> mask;
+    BuildMask(mask, rows, cols, dist, prior_xy, n_prior);
+    std::vector<Cand> cand(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) cand[i] = {resp[i], x[i], y[i]};
+    const int nout = SelectGoodFeatures(cand, mask, rows, cols, dist, need, n_prior, sort_mode, out_xy, out_cap);
+    if (sorted_resp)
+        for (int64_t i = 0; i < n; ++i) {
+            sorted_resp[i] = cand[i].response;
+            sorted_x[i] = cand[i].x;
+            sorted_y[i] = cand[i].y;
+        }
+    return nout;
 }
 
 // Tie check for the greedy scan: returns 1 if, within the prefix of sorted candidates that the greedy

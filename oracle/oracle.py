@@ -43,6 +43,7 @@ def lib():
             "orc_fast_candidates": (i64, [_P, i32, i32, f32, _P, _P, _P, _P, i64]),
             "orc_fast_offsets": (None, [i64, _P]),
             "orc_detect": (i64, [i32, _P, i32, i32, i32, f32, u32, _P, i32, i32, _P, i32, _P, _P, _P, _P, i64]),
+            "orc_select": (i32, [_P, _P, _P, i64, i32, i32, i32, u32, _P, i32, i32, _P, i32, _P, _P, _P]),
             "orc_prefix_has_ties": (i32, [_P, i64]),
             "orc_sparsify": (None, [_P, i32, i32, i32, i32, i32, u8, u8, _P, _P]),
             "orc_lsd_map": (i64, [_P, i32, i32, f32, _P, _P, _P, _P, i64]),
@@ -136,6 +137,26 @@ def detect(kind, img, dist, thr, need, prior=None, sort_mode=0):
     n = lib().orc_detect(kind, _ptr(img), R, C, dist, thr, need, _ptr(pr), n_prior, sort_mode, _ptr(out), out_cap,
                          ctypes.byref(nout), _ptr(cr), _ptr(cx), _ptr(cy), cap)
     return out[: nout.value].copy(), (cr[:n].copy(), cx[:n].copy(), cy[:n].copy())
+
+
+def select(resp, x, y, rows, cols, dist, need, prior=None, sort_mode=0, sorted_out=False):
+    """SelectGoodFeatures (feature_point_detector.cpp:54-74) over caller-supplied candidates in push
+    order, with the prior-feature mask (:12-16, :90-98). Returns new features [n,2] float32 (x, y)
+    (and, with sorted_out, the candidates as the sort leaves them: (resp, x, y)).
+    sort_mode 0 = the reference's std::sort on the pushed order, 1 = response desc, raster index asc."""
+    resp = np.ascontiguousarray(resp, np.float32)
+    x = np.ascontiguousarray(x, np.int32)
+    y = np.ascontiguousarray(y, np.int32)
+    pr = np.zeros((1, 2), np.float32) if prior is None or len(prior) == 0 else np.ascontiguousarray(prior, np.float32)
+    n_prior = 0 if prior is None else len(prior)
+    out_cap = max(int(need) + 1, 1)
+    out = np.zeros((out_cap, 2), np.float32)
+    sr, sx, sy = (np.zeros(len(resp), np.float32), np.zeros(len(resp), np.int32),
+                  np.zeros(len(resp), np.int32)) if sorted_out else (None, None, None)
+    n = lib().orc_select(_ptr(resp), _ptr(x), _ptr(y), len(resp), rows, cols, dist, need, _ptr(pr), n_prior,
+                         sort_mode, _ptr(out), out_cap, _ptr(sr), _ptr(sx), _ptr(sy))
+    feats = out[:min(n, out_cap)].copy()
+    return (feats, (sr, sx, sy)) if sorted_out else feats
 
 
 class RefFlowDetector:

@@ -127,3 +127,31 @@ def test_descriptor_demo_matches_oracle(tmp_path, image_png, oracle, sampler):
     exp = ["".join(str((w[j >> 5] >> (j & 31)) & 1) for j in range(128)) for w in bits]
     assert b["descriptors"] == exp
     assert res["brief_false_cases"] == {"test": "brief_false_cases", "empty_uv": False, "null_image": False}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order,dist,prior", [("raster", 20, 0), ("reverse", 20, 1), ("twice", 0, 0), ("reverse", 1, 0)])
+def test_custom_subclass_candidates(tmp_path, image_png, oracle, order, dist, prior):
+    """A FeaturePointDetector subclass with its own ComputeCandidates (tests/cpp/test_custom_detector.cpp):
+    DetectGoodFeatures calls it once and selects its candidates on the GPU in the reference's order;
+    candidates() and mask() afterwards hold what the reference leaves there."""
+    from test_gpu_select_custom import PRIOR, gradient_candidates
+
+    _build()
+    r = _run("fd_demo_custom", image_png, tmp_path, order, dist, 300, prior)[0]
+    assert r["ok"] is True and r["calls"] == 1
+    rr, xx, yy = gradient_candidates(image_png, order=order)
+    pr = PRIOR if prior else None
+    feats, (sr, sx, sy) = oracle.select(rr, xx, yy, 480, 752, dist, 300, pr, sort_mode=0, sorted_out=True)
+    assert np.array_equal(np.array(r["features"], np.float32).reshape(-1, 2), feats)
+    assert r["n_candidates"] == len(rr)
+    top = np.array(r["top_candidates"], np.float64)
+    assert np.array_equal(top[:, 0].astype(np.float32), sr[:64])
+    assert np.array_equal(top[:, 1].astype(np.int32), sx[:64]) and np.array_equal(top[:, 2].astype(np.int32), sy[:64])
+    # mask_: prior boxes, then a box per new feature except the one that reached `need` (:67-70)
+    m = np.ones((480, 752), bool)
+    boxes = (list(PRIOR) if prior else []) + list(feats[:-1] if len(feats) + (81 if prior else 0) >= 300 else feats)
+    for fx, fy in boxes:
+        r0, c0 = int(fy), int(fx)
+        m[max(r0 - dist, 0):max(r0 + dist + 1, 0), max(c0 - dist, 0):max(c0 + dist + 1, 0)] = False
+    assert r["mask_zeros"] == int((~m).sum())

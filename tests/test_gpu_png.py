@@ -59,3 +59,32 @@ def test_demo_loads_png(tmp_path, image_png):
     ja = [json.loads(x) for x in a.stdout.splitlines() if x.startswith("{")]
     jb = [json.loads(x) for x in b.stdout.splitlines() if x.startswith("{")]
     assert ja == jb and len(ja) >= 4
+
+
+@pytest.mark.parametrize("ch", [1, 3])
+def test_png_frames_out_unaligned_and_checked(ch, oracle):
+    """out= may start at any byte (the converter stores dwords only when both ends are 4-byte aligned);
+    a wrong shape, dtype or device raises before any work is queued."""
+    import torch
+
+    import feature_detector_amd as fd
+
+    imgs = [oracle.make_frame("noise", 70 + i, 33, 50) for i in range(3)]
+    if ch == 3:
+        imgs = [np.stack([x, np.roll(x, 1, 0), np.roll(x, 2, 1)], -1) for x in imgs]
+    pngs = [encode_png(x) for x in imgs]
+    host = np.stack([fd.load_png(p) for p in pngs])
+    big = torch.full((host.size + 8,), 0xA5, dtype=torch.uint8, device="cuda")
+    for off in (1, 2, 3):
+        big.fill_(0xA5)
+        out = big[off:off + host.size].view(host.shape)
+        fd.png_frames(pngs, out=out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), host)
+        b = big.cpu().numpy()
+        assert (b[:off] == 0xA5).all() and (b[off + host.size:] == 0xA5).all()
+    for bad in (torch.empty((3, 33, 49), dtype=torch.uint8, device="cuda"),
+                torch.empty((3, 33, 50), dtype=torch.int32, device="cuda"),
+                torch.empty((3, 33, 50), dtype=torch.uint8)):
+        with pytest.raises(ValueError):
+            fd.png_frames(pngs, out=bad)

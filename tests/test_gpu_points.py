@@ -307,3 +307,47 @@ def test_lane_widths_bit_exact(fd, oracle, image_png, monkeypatch, px):
             check_detect(fd, oracle, name, img, 20, THR[name], 200)
     prior = np.array([(x, y) for x in range(20, 752, 60) for y in range(15, 480, 45)], np.float32)
     check_detect(fd, oracle, "shi_tomasi", image_png, 15, 40.0, len(prior) + 120, prior)
+
+
+def _full_list_check(fd, oracle, name, frames):
+    """fd_points_response's whole unordered candidate list of every frame equals the oracle's
+    candidate set (sorted by raster index), bit for bit."""
+    torch = pytest.importorskip("torch")
+    B, rows, cols = frames.shape
+    dev = torch.from_numpy(frames).cuda()
+    resp, idx, cnt = fd.point_response(name, dev, THR[name])
+    torch.cuda.synchronize()
+    cnt = cnt.cpu().numpy()
+    for b in range(B):
+        er, ex, ey = oracle_candidates(oracle, name, frames[b], THR[name])
+        assert cnt[b] == len(er), (name, b, cnt[b], len(er))
+        gi = idx[b, :cnt[b]].cpu().numpy().astype(np.int64)
+        gr = resp[b, :cnt[b]].cpu().numpy()
+        o = np.argsort(gi, kind="stable")
+        assert np.array_equal(gi[o], ey.astype(np.int64) * cols + ex)
+        assert np.array_equal(gr[o].view(np.uint32), er.view(np.uint32))
+    return dev
+
+
+@pytest.mark.parametrize("name", ["shi_tomasi", "harris"])
+def test_full_lists_north_star_shape(fd, oracle, name):
+    """The timed per-pixel kernel at the north-star frame size (1920x1080, 8 frames of noise and checker:
+    a launch large enough for the list-mode kernel and its flushes): full candidate lists against the
+    oracle, then every frame's features through detect."""
+    frames = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 900 + i, 1080, 1920) for i in range(8)])
+    dev = _full_list_check(fd, oracle, name, frames)
+    res = fd.detect_points(name, dev, 200, 20, THR[name], ties="reference")
+    for b in range(len(frames)):
+        exp, _ = oracle.detect(KIND[name], frames[b], 20, THR[name], 200, sort_mode=0)
+        assert np.array_equal(res.features(b), exp)
+
+
+def test_full_lists_fast_720p(fd, oracle):
+    """k_fast at the configs[2] frame size (1280x720, 8 noise frames: ~30 % of the pixels are candidates,
+    many staging flushes): full candidate lists against the oracle, and every frame's features."""
+    frames = np.stack([oracle.make_frame("noise", 950 + i, 720, 1280) for i in range(8)])
+    dev = _full_list_check(fd, oracle, "fast", frames)
+    res = fd.detect_points("fast", dev, 200, 20, THR["fast"], ties="reference")
+    for b in range(len(frames)):
+        exp, _ = oracle.detect(2, frames[b], 20, THR["fast"], 200, sort_mode=0)
+        assert np.array_equal(res.features(b), exp)

@@ -1,0 +1,116 @@
+"""fd_points_select (SelectGoodFeatures over caller-supplied candidates, the ComputeCandidates seam of
+feature_point_detector.h:44) against the oracle's SelectGoodFeatures restatement (oracle.select).
+
+Bar: bit-exact features in both tie orders -- "reference" (libstdc++ std::sort of the pushed sequence,
+oracle sort_mode 0) and "raster" (equal responses by raster index, oracle sort_mode 1) -- on lists with
+heavy ties (integer gradient magnitudes), in raster / reverse / duplicated push orders, with and
+without prior features, for distances 0, 1, 20 and -1."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
+PRIOR = np.array([(i * 15, j * 15) for i in range(1, 10) for j in range(1, 10)], np.float32)
+
+
+@pytest.fixture(scope="module")
+def fd():
+    import feature_detector_amd as fd
+
+    fd.load()
+    return fd
+
+
+def gradient_candidates(img, thr=40.0, order="raster"):
+    """The C++ demo's custom detector (tests/cpp/test_custom_detector.cpp): |dI/dx| + |dI/dy| > thr."""
+    I = img.astype(np.int32)
+    gx = np.abs(I[1:-1, 2:] - I[1:-1, :-2])
+    gy = np.abs(I[2:, 1:-1] - I[:-2, 1:-1])
+    v = (gx + gy).astype(np.float32)
+    yy, xx = np.nonzero(v > thr)
+    r, x, y = v[yy, xx], (xx + 1).astype(np.int32), (yy + 1).astype(np.int32)
+    if order == "reverse":
+        r, x, y = r[::-1], x[::-1], y[::-1]
+    elif order == "twice":
+        r, x, y = np.repeat(r, 2), np.repeat(x, 2), np.repeat(y, 2)
+    return np.ascontiguousarray(r), np.ascontiguousarray(x), np.ascontiguousarray(y)
+
+
+@pytest.mark.parametrize("name", ["harris", "shi_tomasi", "fast"])
+def test_builtin_candidates_through_select(fd, oracle, image_png, name):
+    """fd_points_candidates -> fd_points_select gives fd_points_detect's features (both tie orders)."""
+    cands = fd.point_candidates(name, image_png, 20, THR[name])
+    rows, cols = image_png.shape
+    for ties, sm in (("reference", 0), ("raster", 1)):
+        res = fd.select_points(cands, rows, cols, 200, 20, ties=ties)
+        exp, _ = oracle.detect({"harris": 0, "shi_tomasi": 1, "fast": 2}[name], image_png, 20, THR[name], 200,
+                               sort_mode=sm)
+        assert np.array_equal(res.features(0), exp), ties
+
+
+@pytest.mark.parametrize("order", ["raster", "reverse", "twice"])
+@pytest.mark.parametrize("dist", [0, 1, 20, -1])
+def test_custom_lists_with_ties(fd, oracle, image_png, order, dist):
+    rows, cols = image_png.shape
+    r, x, y = gradient_candidates(image_png, order=order)
+    assert len(r) > 1000
+    for prior in (None, PRIOR):
+        pr = None if prior is None else [prior]
+        for ties, sm in (("reference", 0), ("raster", 1)):
+            need = 300 if dist >= 0 else 40
+            res = fd.select_points([(r, x, y)], rows, cols, need, dist, prior=pr, ties=ties)
+            exp = oracle.select(r, x, y, rows, cols, dist, need, prior, sort_mode=sm)
+            assert np.array_equal(res.features(0), exp), (ties, prior is None)
+
+
+def test_batch_device_lists(fd, oracle):
+    """Three frames of different list lengths (one empty) as device tensors, features on the device."""
+    torch = pytest.importorskip("torch")
+    frames = [oracle.make_frame(p, s, 200, 300) for p, s in (("noise", 3), ("checker", 4), ("noise", 5))]
+    lists = [gradient_candidates(frames[0]), gradient_candidates(frames[1], order="reverse"),
+             (np.zeros(0, np.float32), np.zeros(0, np.int32), np.zeros(0, np.int32))]
+    cap = max(len(l[0]) for l in lists) + 5
+    resp = torch.zeros((3, cap), dtype=torch.float32)
+    xs = torch.zeros((3, cap), dtype=torch.int32)
+    ys = torch.zeros((3, cap), dtype=torch.int32)
+    for i, (r, x, y) in enumerate(lists):
+        resp[i, :len(r)], xs[i, :len(r)], ys[i, :len(r)] = torch.from_numpy(r), torch.from_numpy(x), torch.from_numpy(y)
+    counts = torch.tensor([len(l[0]) for l in lists], dtype=torch.int64)
+    dev = tuple(t.cuda() for t in (resp, xs, ys, counts))
+    res = fd.select_points(dev, 200, 300, 150, 7)  # ties="raster" for device lists
+    torch.cuda.synchronize()
+    for b, (r, x, y) in enumerate(lists):
+        exp = oracle.select(r, x, y, 200, 300, 7, 150, sort_mode=1)
+        assert np.array_equal(res.features(b), exp)
+    host = fd.select_points(lists, 200, 300, 150, 7)  # host lists: reference order
+    for b, (r, x, y) in enumerate(lists):
+        assert np.array_equal(host.features(b), oracle.select(r, x, y, 200, 300, 7, 150, sort_mode=0))
+
+
+def test_full_float_range(fd, oracle):
+    """Responses anywhere in the float range (negative, zero, +-inf, denormals) keep their order."""
+    rng = np.random.default_rng(3)
+    n = 5000
+    vals = np.concatenate([rng.standard_normal(n - 6).astype(np.float32) * 1e3,
+                           np.array([np.inf, -np.inf, 0.0, -0.0, 1e-42, -1e-42], np.float32)])
+    x = rng.integers(0, 640, n).astype(np.int32)
+    y = rng.integers(0, 480, n).astype(np.int32)
+    for ties, sm in (("reference", 0), ("raster", 1)):
+        res = fd.select_points([(vals, x, y)], 480, 640, 400, 3, ties=ties)
+        assert np.array_equal(res.features(0), oracle.select(vals, x, y, 480, 640, 3, 400, sort_mode=sm))
+
+
+def test_invalid_candidates_refused(fd):
+    import feature_detector_amd._lib as L
+
+    r = np.array([5.0, 4.0], np.float32)
+    for x, y in (((0, 640), (0, 0)), ((0, 1), (-1, 0)), ((0, 1), (0, 480))):
+        with pytest.raises(L.FdError):
+            fd.select_points([(r, np.array(x, np.int32), np.array(y, np.int32))], 480, 640, 10, 3)
+    with pytest.raises(L.FdError):
+        fd.select_points([(np.array([1.0, np.nan], np.float32), np.array([1, 2], np.int32),
+                           np.array([1, 2], np.int32))], 480, 640, 10, 3)
+    # the context keeps working after a refused call
+    res = fd.select_points([(r, np.array([1, 9], np.int32), np.array([1, 1], np.int32))], 480, 640, 10, 3)
+    assert np.array_equal(res.features(0), np.array([[1, 1], [9, 1]], np.float32))
