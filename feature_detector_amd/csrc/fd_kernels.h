@@ -117,6 +117,7 @@ struct SelectArgs {
     int wide_eager;       // wide pass with the first chunk (FAST) instead of at the first later list pass
     int first_sub;     // sorted-segment corner frames: first chunk cut at one sub-chunk (kSubChunk keys)
     int grid_at_d0;    // distance 0 still tests the grid (1-pixel cells): caller lists may name a pixel twice
+    int dup_keys;      // equal selection keys possible (caller lists): the orderings rank them stably
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 
@@ -144,6 +145,27 @@ struct CandInArgs {
     uint32_t key_base;
     int key_lz;
     uint32_t *bad;  // [batch] bit 31: a candidate outside the frame, a NaN response or a bad count
+    // keypoint-list models (fd_nn_select_list): (u, v) int64 pairs instead of x / y, and candidates
+    // within `border` of the frame edge dropped (CreateMask's zero rows/cols). The list is then
+    // appended to (unordered; the selection orders equal scores by raster index, tie_idx_desc).
+    const int64_t *kp;
+    int border;  // < 0: keep push order at list position i (fd_points_select)
+};
+
+// fd_nn_select_list: descriptor rows of the selected keypoints. Per (frame f, feature k), the
+// candidate at that pixel visited first by the selection (highest score, then highest index).
+struct NnPickArgs {
+    const int64_t *kp;      // [batch][stride_in][2]
+    const float *scores;    // [batch][stride_in]
+    const int64_t *counts;  // [batch]
+    int64_t stride_in;
+    const float *desc;      // [batch][stride_in][dim]
+    int dim;
+    const float *xy;        // [batch][out_stride][2] selected features
+    const int32_t *n_sel;   // [batch]
+    int out_stride;
+    int batch;
+    float *out;             // [batch][out_stride][dim]
 };
 
 struct CompactArgs {
@@ -234,6 +256,7 @@ hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off,
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
 hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);
 hipError_t launch_cand_lists(const CandInArgs &a, int64_t max_count, hipStream_t s);
+hipError_t launch_nn_pick(const NnPickArgs &a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s);
 hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s);    // compact mode: map (counts, row bits) + scans

@@ -419,6 +419,8 @@ struct SelectCall {
     const uint64_t *seghead = nullptr;
     int nseg = 0;
     bool push_order = false;  // lists hold the caller's push order (fd_points_select), not raster order
+    bool dup_keys = false;    // a pixel may be listed twice with one response (caller lists): equal keys
+    bool grid_at_d0 = false;  // distance 0 tests the grid too (1-pixel cells; set with push_order)
     const char *value_msg = "a value above the declared maximum (fd_nn_opts::max_response)";
 };
 
@@ -537,7 +539,8 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.prior_counts = pi.counts_dev;
     s.need = q.need;
     s.dist = q.dist;
-    s.grid_at_d0 = q.push_order ? 1 : 0;  // caller lists may name a pixel twice: distance 0 tests it
+    s.grid_at_d0 = (q.push_order || q.grid_at_d0) ? 1 : 0;  // caller lists may name a pixel twice: distance 0 tests it
+    s.dup_keys = q.dup_keys ? 1 : 0;
     if (s.dist >= 1 || (s.dist == 0 && s.grid_at_d0)) {
         s.grid_w = (cols + s.dist) / (s.dist + 1);
         s.grid_h = (rows + s.dist) / (s.dist + 1);
@@ -1000,6 +1003,7 @@ int fd_points_select(fd_ctx *c, int batch, int rows, int cols, const fd_point_op
     a.key_base = host_float_key(-std::numeric_limits<float>::infinity()) - 1u;
     a.key_lz = 0;
     a.bad = sb.pre_count;
+    a.border = -1;  // list position = push position
     c->sel_dirty = true;  // until k_select is enqueued: it resets the control block
     FD_HIP_TRY(c, fdk::launch_cand_lists(a, max_n, c->stream));
     if (!cands_on_device) FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // caller's host arrays were the sources
@@ -1014,6 +1018,7 @@ int fd_points_select(fd_ctx *c, int batch, int rows, int cols, const fd_point_op
     sc.key_lz = a.key_lz;
     sc.value_flag = true;
     sc.push_order = true;
+    sc.dup_keys = true;
     sc.value_msg = "a candidate outside the frame, a NaN response or a bad candidate count";
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, 1);
 }
@@ -1578,6 +1583,141 @@ int fd_nn_select(fd_ctx *c, const float *heatmap, int heatmap_on_device, int bat
     sc.tie_idx_desc = 1;
     sc.value_flag = true;
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, heatmap_on_device);
+}
+
+// DirectlySelectGoodFeaturesWithDescriptors (nn_feature_point_detector.cpp:204-230) for the
+// keypoint-list models (kSuperpointNms / kDiskNms, nn_feature_point_detector_superpoint.cpp:76-112,
+// nn_feature_point_detector_disk.cpp:76-112): k_cand_lists (border dropped) + k_select in descending
+// (score, raster index) order + k_nn_pick for the descriptor rows.
+int fd_nn_select_list(fd_ctx *c, const int64_t *keypoints, const float *scores, const int64_t *counts, int64_t cap,
+                      int inputs_on_device, int batch, int rows, int cols, const fd_nn_opts *opts,
+                      const float *prior_xy, const int32_t *prior_counts, const float *cand_desc, int desc_dim,
+                      float *out_desc, float *out_xy, int32_t out_stride, int32_t *out_counts, int outputs_on_device) {
+    int rc = check_shape(c, FD_HARRIS, batch, rows, cols);
+    if (rc) return rc;
+    if (!opts || !out_xy || !out_counts || out_stride < 1) return fail(c, FD_ERR_INVALID, "bad output arguments");
+    if (opts->invalid_boundary < 0) return fail(c, FD_ERR_INVALID, "invalid_boundary must be >= 0");
+    if (opts->max_features < 0) return fail(c, FD_ERR_INVALID, "max_features must be >= 0");
+    if (!counts || cap < 0 || cap > 0x7FFFFFFFll) return fail(c, FD_ERR_INVALID, "counts is NULL or cap out of range");
+    if (cand_desc && (desc_dim < 1 || !out_desc)) return fail(c, FD_ERR_INVALID, "descriptors need desc_dim >= 1 and out_desc");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    if (!inputs_on_device)
+        for (int b = 0; b < batch; ++b)
+            if (counts[b] < 0 || counts[b] > cap)
+                return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": keypoint count outside [0, cap]");
+    if (cap > 0 && (!keypoints || !scores)) return fail(c, FD_ERR_INVALID, "keypoints / scores are NULL");
+    const int64_t *dkp = keypoints, *dcnt = counts;
+    const float *dsc = scores, *ddesc = cand_desc;
+    if (!inputs_on_device) {  // one upload of the whole batch
+        const size_t nb = static_cast<size_t>(batch) * static_cast<size_t>(cap);
+        FD_HIP_TRY(c, ensure(c, c->c_x, sizeof(int64_t) * 2 * std::max<size_t>(nb, 1)));
+        FD_HIP_TRY(c, ensure(c, c->c_resp, sizeof(float) * std::max<size_t>(nb, 1)));
+        FD_HIP_TRY(c, ensure(c, c->c_counts, sizeof(int64_t) * batch));
+        if (nb) {
+            FD_HIP_TRY(c, hipMemcpyAsync(c->c_x.p, keypoints, sizeof(int64_t) * 2 * nb, hipMemcpyHostToDevice, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(c->c_resp.p, scores, sizeof(float) * nb, hipMemcpyHostToDevice, c->stream));
+        }
+        FD_HIP_TRY(c, hipMemcpyAsync(c->c_counts.p, counts, sizeof(int64_t) * batch, hipMemcpyHostToDevice, c->stream));
+        if (cand_desc && nb) {
+            FD_HIP_TRY(c, ensure(c, c->n_map, sizeof(float) * nb * desc_dim));
+            FD_HIP_TRY(c, hipMemcpyAsync(c->n_map.p, cand_desc, sizeof(float) * nb * desc_dim, hipMemcpyHostToDevice,
+                                         c->stream));
+            ddesc = as<float>(c->n_map);
+        }
+        dkp = as<int64_t>(c->c_x);
+        dsc = as<float>(c->c_resp);
+        dcnt = as<int64_t>(c->c_counts);
+    }
+    PriorInfo pi;
+    rc = setup_priors(c, batch, rows, cols, opts->min_feature_distance, prior_xy, prior_counts, pi);
+    if (rc) return rc;
+    const int64_t lcap = std::max<int64_t>(cap, 64);
+    SelectBufs sb{};
+    rc = select_buffers(c, batch, lcap, sb);
+    if (rc) return rc;
+    fdk::CandInArgs a{};
+    a.resp = dsc;
+    a.kp = dkp;
+    a.counts = dcnt;
+    a.stride = cap;
+    a.batch = batch;
+    a.rows = rows;
+    a.cols = cols;
+    a.border = opts->invalid_boundary;
+    a.list_resp = as<float>(c->list_resp);
+    a.list_idx = as<uint32_t>(c->list_idx);
+    a.list_cap = lcap;
+    a.list_count = sb.list_count;
+    a.hist0 = sb.hist0;
+    a.key_base = host_float_key(-std::numeric_limits<float>::infinity()) - 1u;
+    a.key_lz = 0;
+    a.bad = sb.pre_count;
+    c->sel_dirty = true;  // until k_select is enqueued: it resets the control block
+    FD_HIP_TRY(c, fdk::launch_cand_lists(a, cap, c->stream));
+    SelectCall sc{};
+    sc.batch = batch;
+    sc.rows = rows;
+    sc.cols = cols;
+    sc.dist = opts->min_feature_distance;
+    sc.need = static_cast<uint32_t>(opts->max_features);
+    sc.cap = lcap;
+    sc.key_base = a.key_base;
+    sc.key_lz = a.key_lz;
+    sc.tie_idx_desc = 1;  // equal scores: raster index descending (ArgSort walked from the back; unpinned)
+    sc.dup_keys = true;
+    sc.grid_at_d0 = true;
+    sc.value_flag = true;
+    sc.value_msg = "a keypoint outside the frame, a NaN score or a bad keypoint count";
+    // selection into device buffers first when the descriptor rows are wanted on the device
+    float *sel_xy = out_xy;
+    int32_t *sel_cnt = out_counts;
+    if (cand_desc && !outputs_on_device) {
+        FD_HIP_TRY(c, ensure(c, c->n_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch));
+        FD_HIP_TRY(c, ensure(c, c->n_counts, sizeof(int32_t) * batch));
+        sel_xy = as<float>(c->n_xy);
+        sel_cnt = as<int32_t>(c->n_counts);
+    }
+    rc = run_select(c, sc, pi, sb, sel_xy, out_stride, sel_cnt, cand_desc ? 1 : outputs_on_device, 1);
+    if (rc) return rc;
+    if (cand_desc) {
+        fdk::NnPickArgs k{};
+        k.kp = dkp;
+        k.scores = dsc;
+        k.counts = dcnt;
+        k.stride_in = cap;
+        k.desc = ddesc;
+        k.dim = desc_dim;
+        k.xy = sel_xy;
+        k.n_sel = sel_cnt;
+        k.out_stride = out_stride;
+        k.batch = batch;
+        float *dout = out_desc;
+        if (!outputs_on_device) {
+            FD_HIP_TRY(c, ensure(c, c->n_out, sizeof(float) * static_cast<size_t>(out_stride) * batch * desc_dim));
+            dout = as<float>(c->n_out);
+        }
+        k.out = dout;
+        FD_HIP_TRY(c, fdk::launch_nn_pick(k, c->stream));
+        if (!outputs_on_device) {
+            std::vector<uint32_t> st(static_cast<size_t>(batch));
+            FD_HIP_TRY(c, hipMemcpyAsync(out_xy, sel_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
+                                         hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(out_counts, sel_cnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(out_desc, dout, sizeof(float) * static_cast<size_t>(out_stride) * batch * desc_dim,
+                                         hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipMemcpyAsync(st.data(), sb.status, sizeof(uint32_t) * batch, hipMemcpyDeviceToHost, c->stream));
+            FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+            for (int b = 0; b < batch; ++b) {
+                if (st[b] & FD_FRAME_VALUE_RANGE)
+                    return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": " + sc.value_msg);
+                if (st[b] & FD_FRAME_GUARD)
+                    return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (status 0x" + hex(st[b]) +
+                                                   ", frame " + std::to_string(b) + ")");
+            }
+        }
+    }
+    if (!inputs_on_device) FD_HIP_TRY(c, hipStreamSynchronize(c->stream));  // host inputs were copy sources
+    return FD_OK;
 }
 
 int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int map_layout, int batch, int channels,

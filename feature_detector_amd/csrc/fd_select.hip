@@ -1071,8 +1071,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         big = s_b - s_b1 > static_cast<uint32_t>(kBucketMax);
                     }
                     if (!__syncthreads_or(big)) {
+                        uint32_t slot = 0;
                         if (tid < c) {
-                            const uint32_t slot = atomicAdd(const_cast<uint32_t *>(&S[bin + 1]), 1u) - sbase;
+                            slot = atomicAdd(const_cast<uint32_t *>(&S[bin + 1]), 1u) - sbase;
                             tmp[min(slot, static_cast<uint32_t>(kSelectChunk - 1))] = me;
                         }
                         __syncthreads();
@@ -1080,12 +1081,20 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         if (tid < c) {
                             const uint32_t g0 = s_b1 - sbase, gn = s_b - s_b1;
                             uint32_t r = 0;
-                            for (uint32_t j0 = 0; j0 < gn; j0 += 8) {  // 8 loads in flight (clamped to the group)
-                                uint64_t v[8];
+                            if (!a.dup_keys) {
+                                for (uint32_t j0 = 0; j0 < gn; j0 += 8) {  // 8 loads in flight (clamped to the group)
+                                    uint64_t v[8];
 #pragma unroll
-                                for (uint32_t u = 0; u < 8; ++u) v[u] = tmp[g0 + min(j0 + u, gn - 1)];
+                                    for (uint32_t u = 0; u < 8; ++u) v[u] = tmp[g0 + min(j0 + u, gn - 1)];
 #pragma unroll
-                                for (uint32_t u = 0; u < 8; ++u) r += (j0 + u < gn && v[u] > me) ? 1u : 0u;
+                                    for (uint32_t u = 0; u < 8; ++u) r += (j0 + u < gn && v[u] > me) ? 1u : 0u;
+                                }
+                            } else {  // equal keys (caller lists naming a pixel twice): ranked by group slot
+                                const uint32_t mine = slot - g0;
+                                for (uint32_t j = 0; j < gn; ++j) {
+                                    const uint64_t v = tmp[g0 + j];
+                                    r += (v > me || (v == me && j < mine)) ? 1u : 0u;
+                                }
                             }
                             place(static_cast<int>(min(g0 + r, static_cast<uint32_t>(kSelectChunk - 1))), me);
                         }
@@ -1102,10 +1111,18 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         const uint64_t me = unsorted[p];
                         const ulonglong2 *b2 = reinterpret_cast<const ulonglong2 *>(unsorted + (p & ~63));
                         int lr = 0;
+                        if (!a.dup_keys) {
     #pragma unroll 8
-                        for (int j = 0; j < 32; ++j) {
-                            const ulonglong2 q = b2[j];
-                            lr += (q.x > me) + (q.y > me);
+                            for (int j = 0; j < 32; ++j) {
+                                const ulonglong2 q = b2[j];
+                                lr += (q.x > me) + (q.y > me);
+                            }
+                        } else {  // equal keys: by position in the run (a stable order)
+                            const int mine = p & 63;
+                            for (int j = 0; j < 32; ++j) {
+                                const ulonglong2 q = b2[j];
+                                lr += (q.x > me || (q.x == me && 2 * j < mine)) + (q.y > me || (q.y == me && 2 * j + 1 < mine));
+                            }
                         }
                         tmp[(p & ~63) + lr] = me;
                     }
@@ -1118,10 +1135,14 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                             const int run = p / w;
                             const int pair = (run & ~1) * w;
                             const int sib = (run ^ 1) * w;
-                            int lo2 = 0, hi2 = max(0, min(w, c - sib));  // larger keys in the sibling run
+                            // larger keys in the sibling run (and, for the right run of a pair, equal
+                            // ones: a stable merge when keys repeat; unique keys are unaffected)
+                            const bool right = (run & 1) != 0;
+                            int lo2 = 0, hi2 = max(0, min(w, c - sib));
                             while (lo2 < hi2) {
                                 const int mid = (lo2 + hi2) >> 1;
-                                if (src[sib + mid] > me) lo2 = mid + 1; else hi2 = mid;
+                                const uint64_t o = src[sib + mid];
+                                if (o > me || (right && o == me)) lo2 = mid + 1; else hi2 = mid;
                             }
                             dst[pair + (p - run * w) + lo2] = me;
                         }

@@ -1,19 +1,25 @@
-"""SuperPoint keypoints + descriptors: the network in PyTorch-ROCm, the
-post-processing in the HIP kernels behind fd_nn_select / fd_nn_descriptors.
+"""NN keypoints + descriptors: the networks in PyTorch-ROCm, the post-processing in
+the HIP kernels behind fd_nn_select / fd_nn_select_list / fd_nn_descriptors.
 
 Mirrors feature_detector::NNFeaturePointDetector (src/nn_feature_point_detector/
-nn_feature_point_detector.h:12-86) for the kSuperpointHeatmap model:
+nn_feature_point_detector.h:12-86) for its four model types (ModelType, :15-20):
   Initialize()                          nn_feature_point_detector.cpp:10-57 (network + one warm-up run)
-  DetectGoodFeaturesWithDescriptor()    nn_feature_point_detector_superpoint.cpp:8-77
-    InferenceSession                    -> SuperPointNet (fp16 convs through MIOpen, fp32 heatmap)
-    CreateMask + candidates + selection -> fd_nn_select (GPU, std::multimap order)
-    ExtractDescriptorsForSelectedFeatures -> fd_nn_descriptors (GPU bilinear sampling)
+  DetectGoodFeaturesWithDescriptor()    nn_feature_point_detector_superpoint.cpp:8-112 / _disk.cpp:8-112
+    InferenceSession                    -> the network (fp16 convs through MIOpen, fp32 outputs); DISK
+                                           models take the gray frame as RGB (:96-99)
+    heatmap models (kSuperpointHeatmap, kDiskHeatmap):
+      CreateMask + candidates + selection -> fd_nn_select (GPU, std::multimap order)
+      ExtractDescriptorsForSelectedFeatures -> fd_nn_descriptors for the priors and the new features
+                                           (the reference describes every entry of all_pixel_uv)
+    keypoint-list models (kSuperpointNms, kDiskNms: NMS in the graph):
+      ArgSort + DirectlySelectGoodFeaturesWithDescriptors -> fd_nn_select_list (GPU selection +
+                                           descriptor-row gather; new features only, as :223-227)
 
-The reference loads trained ONNX models (onnx_models/superpoint.onnx) that are not available here
-(.MISSING_LARGE_BLOBS), and ONNX Runtime is absent: the network is the published SuperPoint
-architecture with seeded random weights, so keypoints from it are meaningful for throughput only.
-The post-processing is bit-exact to the oracle's restatement on any given network output. The
-kSuperpointNms / DISK variants are not provided (their in-graph NMS / UNet need the missing models).
+The reference loads trained ONNX models (onnx_models/*.onnx) that are not available here
+(.MISSING_LARGE_BLOBS), and ONNX Runtime is absent: the networks are the published SuperPoint
+architecture and a DISK-shaped U-Net with seeded random weights, with in-graph NMS + top-K heads for
+the list models, so keypoints from them are meaningful for throughput only. The post-processing is
+bit-exact to the oracle's restatement on any given network output.
 """
 from __future__ import annotations
 
@@ -47,6 +53,18 @@ def _opts(o: Options, max_response: float = 1.0) -> fd_nn_opts:
                       float(o.kMinResponse), float(max_response))
 
 
+def _prior_arrays(prior, b):
+    """Per-frame prior features (list of (n_i, 2) (x, y) arrays) -> (flat float32 [sum, 2], counts int32)."""
+    if prior is None:
+        return None, None
+    if len(prior) != b:
+        raise ValueError("prior must have one entry per frame")
+    pcnt = np.array([len(p) for p in prior], np.int32)
+    pflat = (np.ascontiguousarray(np.concatenate([np.asarray(p, np.float32).reshape(-1, 2) for p in prior]))
+             if pcnt.sum() > 0 else np.zeros((1, 2), np.float32))
+    return pflat, pcnt
+
+
 def nn_select(heat, options: Options | None = None, prior=None, out=None, ctx: Context | None = None,
               max_response: float = 1.0):
     """fd_nn_select on heatmaps [B, H, W] float32 (numpy, or a torch device tensor -> device outputs).
@@ -72,13 +90,7 @@ def nn_select(heat, options: Options | None = None, prior=None, out=None, ctx: C
         heat = heat[None]
     b, r, c = (int(v) for v in heat.shape)
     stride = max(int(o.kMaxNumberOfDetectedFeatures), 1) + 1
-    pflat, pcnt = None, None
-    if prior is not None:
-        if len(prior) != b:
-            raise ValueError("prior must have one entry per frame")
-        pcnt = np.array([len(p) for p in prior], np.int32)
-        pflat = (np.ascontiguousarray(np.concatenate([np.asarray(p, np.float32).reshape(-1, 2) for p in prior]))
-                 if pcnt.sum() > 0 else np.zeros((1, 2), np.float32))
+    pflat, pcnt = _prior_arrays(prior, b)
     if on_dev:
         import torch
 
@@ -100,6 +112,66 @@ def nn_select(heat, options: Options | None = None, prior=None, out=None, ctx: C
         ctypes.c_void_p(cnt_p), 1 if on_dev else 0)
     _lib.check(ctx.ptr, rc)
     return xy, cnt
+
+
+def nn_select_list(keypoints, scores, rows: int, cols: int, counts=None, options: Options | None = None, prior=None,
+                   descriptors=None, out=None, ctx: Context | None = None):
+    """fd_nn_select_list: the keypoint-list models' selection (DirectlySelectGoodFeaturesWithDescriptors).
+
+    keypoints [B, K, 2] int64 (u, v) in a rows x cols frame, scores [B, K] float32, counts [B] int64
+    (None: K each),
+    descriptors [B, K, D] float32 or None. numpy inputs give numpy outputs; torch device tensors give
+    device outputs (current stream). Returns (xy [B, max+1, 2], counts [B] int32, desc [B, max+1, D] or
+    None): the new features per frame in selection order and their descriptor rows.
+    prior: None or a list (per frame) of (n_i, 2) float arrays of (x, y), host memory.
+    """
+    o = options or Options()
+    on_dev = _is_torch_device_tensor(scores)
+    ctx = _resolve_ctx(ctx, scores)
+    opts = _opts(o, float("inf"))
+    stride = max(int(o.kMaxNumberOfDetectedFeatures), 1) + 1
+    pflat, pcnt = _prior_arrays(prior, int(scores.shape[0]))
+    if on_dev:
+        import torch
+
+        kp = keypoints.to(torch.int64).contiguous()
+        sc = scores.to(torch.float32).contiguous()
+        b, k = (int(v) for v in sc.shape)
+        cnt_in = (torch.full((b,), k, dtype=torch.int64, device=sc.device) if counts is None
+                  else counts.to(torch.int64).contiguous())
+        dd = None if descriptors is None else descriptors.to(torch.float32).contiguous()
+        dim = 0 if dd is None else int(dd.shape[2])
+        if out is None:
+            out = (torch.empty((b, stride, 2), dtype=torch.float32, device=sc.device),
+                   torch.empty((b,), dtype=torch.int32, device=sc.device),
+                   None if dd is None else torch.zeros((b, stride, dim), dtype=torch.float32, device=sc.device))
+        xy, cnt, dout = out
+        stride = xy.shape[1]
+        ptrs = (kp.data_ptr(), sc.data_ptr(), cnt_in.data_ptr(), 0 if dd is None else dd.data_ptr(),
+                0 if dout is None else dout.data_ptr(), xy.data_ptr(), cnt.data_ptr())
+    else:
+        kp = np.ascontiguousarray(keypoints, np.int64)
+        sc = np.ascontiguousarray(scores, np.float32)
+        b, k = sc.shape
+        cnt_in = np.full((b,), k, np.int64) if counts is None else np.ascontiguousarray(counts, np.int64)
+        dd = None if descriptors is None else np.ascontiguousarray(descriptors, np.float32)
+        dim = 0 if dd is None else dd.shape[2]
+        xy = np.zeros((b, stride, 2), np.float32)
+        cnt = np.zeros((b,), np.int32)
+        dout = None if dd is None else np.zeros((b, stride, dim), np.float32)
+        ptrs = (kp.ctypes.data, sc.ctypes.data, cnt_in.ctypes.data, 0 if dd is None else dd.ctypes.data,
+                0 if dout is None else dout.ctypes.data, xy.ctypes.data, cnt.ctypes.data)
+    if tuple(kp.shape) != (b, k, 2):
+        raise ValueError("keypoints must be [B, K, 2] matching scores [B, K]")
+    _bind_stream(ctx, on_dev)
+    vp = [ctypes.c_void_p(p) if p else None for p in ptrs]
+    rc = _lib.load().fd_nn_select_list(
+        ctx.ptr, vp[0], vp[1], vp[2], int(k), 1 if on_dev else 0, b, int(rows), int(cols), ctypes.byref(opts),
+        ctypes.c_void_p(pflat.ctypes.data) if pflat is not None else None,
+        ctypes.c_void_p(pcnt.ctypes.data) if pcnt is not None else None,
+        vp[3], int(dim), vp[4], vp[5], int(stride), vp[6], 1 if on_dev else 0)
+    _lib.check(ctx.ptr, rc)
+    return xy, cnt, dout
 
 
 def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = None):
@@ -141,13 +213,48 @@ def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = No
     return res
 
 
-def build_net(seed: int = 0, head_gain: float = 100.0):
+MODEL_TYPES = ("kSuperpointHeatmap", "kSuperpointNms", "kDiskHeatmap", "kDiskNms")  # ModelType (:15-20)
+DESCRIPTOR_DIM = {"superpoint": 256, "disk": 128}  # SuperpointDescriptorType / DiskDescriptorType
+
+
+def simple_nms(heat, radius: int):
+    """In-graph NMS of the keypoint-list models (the max-pool suppression SuperPoint/DISK exports use):
+    a score survives where it is the maximum of its (2r+1)^2 window, twice refined around the kept ones."""
+    import torch
+    import torch.nn.functional as F
+
+    def mp(x):
+        return F.max_pool2d(x, kernel_size=2 * radius + 1, stride=1, padding=radius)
+
+    x = heat[:, None]
+    zeros = torch.zeros_like(x)
+    keep = x == mp(x)
+    for _ in range(2):
+        supp = mp(keep.float()) > 0
+        supp_x = torch.where(supp, zeros, x)
+        keep = keep | ((supp_x == mp(supp_x)) & ~supp)
+    return torch.where(keep, x, zeros)[:, 0]
+
+
+def top_k_keypoints(heat, k: int):
+    """heat [B, H, W] -> (keypoints [B, k, 2] int64 (u, v), scores [B, k] float32), best first."""
+    import torch
+
+    b, h, w = heat.shape
+    sc, idx = heat.reshape(b, -1).topk(min(k, h * w), dim=1)
+    kp = torch.stack([idx % w, idx // w], dim=2).to(torch.int64)
+    return kp, sc.float()
+
+
+def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k: int = 1024):
     """SuperPoint (DeTone et al. 2018): shared VGG encoder (1/8 resolution, 128 channels), detector
     head (65-way cell softmax -> full-resolution heatmap) and descriptor head (256-d, L2-normalised).
     Seeded random weights (the trained model is not available offline). With default init the
     65-way softmax is nearly uniform (every value ~1/65 < kMinResponse), so the detector head's
     logits are scaled by head_gain: at 100, ~5 % of a noise frame's pixels exceed 0.1 (a few
-    thousand candidates per 640x480 frame), so that selection does the work a trained model gives it."""
+    thousand candidates per 640x480 frame), so that selection does the work a trained model gives it.
+    nms=True (kSuperpointNms): the heatmap goes through simple_nms (radius 4) and top_k keypoints are
+    returned with their scores and bilinearly sampled, normalised descriptors."""
     import torch
     from torch import nn
 
@@ -171,7 +278,8 @@ def build_net(seed: int = 0, head_gain: float = 100.0):
             self.convDb = nn.Conv2d(c5, d1, 1, 1, 0)
 
         def forward(self, x):
-            """x: [B, 1, H, W] in [0, 1] -> (heatmap [B, H, W] f32, descriptors [B, 256, H/8, W/8] f32)."""
+            """x: [B, 1, H, W] in [0, 1] -> (heatmap [B, H, W] f32, descriptors [B, 256, H/8, W/8] f32), or
+            with nms (keypoints [B, K, 2] int64, scores [B, K] f32, descriptors [B, K, 256] f32)."""
             r = self.relu
             x = r(self.conv1b(r(self.conv1a(x))))
             x = self.pool(x)
@@ -185,7 +293,15 @@ def build_net(seed: int = 0, head_gain: float = 100.0):
             heat = torch.nn.functional.pixel_shuffle(prob, 8)[:, 0]
             desc = self.convDb(r(self.convDa(x))).float()
             desc = desc / desc.norm(dim=1, keepdim=True).clamp_min(1e-12)
-            return heat, desc
+            if not nms:
+                return heat, desc
+            kp, sc = top_k_keypoints(simple_nms(heat, 4), top_k)
+            h, w = heat.shape[1:]
+            # descriptor at each keypoint: bilinear on the 1/8 map at the cell-centred position
+            grid = torch.stack([(kp[..., 0].float() + 0.5) / w * 2 - 1, (kp[..., 1].float() + 0.5) / h * 2 - 1], -1)
+            d = torch.nn.functional.grid_sample(desc, grid[:, None], mode="bilinear", align_corners=False)[:, :, 0]
+            d = d / d.norm(dim=1, keepdim=True).clamp_min(1e-12)
+            return kp, sc, d.transpose(1, 2).contiguous()
 
     torch.manual_seed(seed)
     net = SuperPointNet()
@@ -195,27 +311,104 @@ def build_net(seed: int = 0, head_gain: float = 100.0):
     return net
 
 
-class SuperPointDetector:
-    """NNFeaturePointDetector for the SuperPoint heatmap model, batched, on one GPU."""
+def build_disk(seed: int = 0, nms: bool = False, top_k: int = 1024, head_gain: float = 8.0):
+    """DISK-shaped network (Tyszkiewicz et al. 2020): a U-Net on the RGB frame whose full-resolution
+    output holds 128 descriptor channels and one detection channel. Seeded random weights (the
+    trained disk.onnx is not available); the detection logits are scaled by head_gain and pass a
+    sigmoid, so a few percent of a noise frame's pixels exceed kMinResponse. nms=True (kDiskNms):
+    simple_nms (radius 2) + top_k keypoints with the descriptor rows at their pixels."""
+    import torch
+    from torch import nn
 
-    def __init__(self, options: Options | None = None, device: int = 0, dtype: str = "fp16", seed: int = 0):
+    def block(ci, co):
+        return nn.Sequential(nn.Conv2d(ci, co, 3, 1, 1), nn.ReLU(inplace=True), nn.Conv2d(co, co, 3, 1, 1),
+                             nn.ReLU(inplace=True))
+
+    class DiskNet(nn.Module):
+        def __init__(self):
+            super().__init__()
+            ch = (32, 64, 64, 128)
+            self.enc = nn.ModuleList([block(3, ch[0]), block(ch[0], ch[1]), block(ch[1], ch[2]), block(ch[2], ch[3])])
+            self.up = nn.ModuleList([nn.ConvTranspose2d(ch[3], ch[2], 2, 2), nn.ConvTranspose2d(ch[2], ch[1], 2, 2),
+                                     nn.ConvTranspose2d(ch[1], ch[0], 2, 2)])
+            self.dec = nn.ModuleList([block(2 * ch[2], ch[2]), block(2 * ch[1], ch[1]), block(2 * ch[0], ch[0])])
+            self.head = nn.Conv2d(ch[0], 129, 1)
+            self.pool = nn.MaxPool2d(2, 2)
+
+        def forward(self, x):
+            """x: [B, 3, H, W] in [0, 1] -> (heatmap [B, H, W] f32, descriptors [B, 128, H, W] f32), or
+            with nms (keypoints [B, K, 2] int64, scores [B, K] f32, descriptors [B, K, 128] f32)."""
+            skips = []
+            for i, e in enumerate(self.enc):
+                x = e(x if i == 0 else self.pool(x))
+                skips.append(x)
+            for u, d, sk in zip(self.up, self.dec, reversed(skips[:-1])):
+                x = d(torch.cat([u(x), sk], dim=1))
+            out = self.head(x).float()
+            heat = torch.sigmoid(out[:, 128] * head_gain)
+            desc = out[:, :128]
+            desc = desc / desc.norm(dim=1, keepdim=True).clamp_min(1e-12)
+            if not nms:
+                return heat, desc
+            kp, sc = top_k_keypoints(simple_nms(heat, 2), top_k)
+            b = torch.arange(desc.shape[0], device=desc.device)[:, None]
+            d = desc.permute(0, 2, 3, 1)[b, kp[..., 1], kp[..., 0]]
+            return kp, sc, d.contiguous()
+
+    torch.manual_seed(seed)
+    return DiskNet()
+
+
+@dataclass
+class NNResult:
+    """DetectGoodFeaturesWithDescriptor's outputs for a batch: xy [B, S, 2] / counts [B] (the new
+    features), descriptors [B, S, D] (their rows), prior_descriptors [B, P, D] (heatmap models: the
+    reference's descriptors of the incoming features, all_pixel_uv[0..P), per frame counts as the
+    priors given; None for the keypoint-list models, whose reference returns new rows only). Unpacks as
+    (xy, counts, descriptors)."""
+    xy: object
+    counts: object
+    descriptors: object
+    prior_descriptors: object = None
+
+    def __iter__(self):
+        return iter((self.xy, self.counts, self.descriptors))
+
+
+class NNFeaturePointDetector:
+    """NNFeaturePointDetector (nn_feature_point_detector.h:12-86), batched, on one GPU."""
+
+    def __init__(self, options: Options | None = None, device: int = 0, dtype: str = "fp16", seed: int = 0,
+                 top_k: int = 1024):
         self._options = options or Options()
         self.device = device
         self.dtype = dtype
         self.seed = seed
+        self.top_k = top_k
         self.net = None
 
     def options(self) -> Options:
         return self._options
 
+    @property
+    def is_disk(self) -> bool:
+        return self._options.kModelType.startswith("kDisk")
+
+    @property
+    def is_list_model(self) -> bool:
+        return self._options.kModelType.endswith("Nms")
+
     def Initialize(self) -> bool:
-        """nn_feature_point_detector.cpp:10-57: build the network, run it once on an all-ones image."""
+        """nn_feature_point_detector.cpp:10-57: build the model's network, run it once on an all-ones image."""
         import torch
 
-        if self._options.kModelType != "kSuperpointHeatmap":
-            raise NotImplementedError("only kSuperpointHeatmap is provided (see module docstring)")
+        mt = self._options.kModelType
+        if mt not in MODEL_TYPES:
+            raise ValueError(f"unknown kModelType {mt!r} (one of {MODEL_TYPES})")
         dev = torch.device("cuda", self.device)
-        net = build_net(self.seed).to(dev).eval()
+        net = (build_disk(self.seed, nms=self.is_list_model, top_k=self.top_k) if self.is_disk
+               else build_net(self.seed, nms=self.is_list_model, top_k=self.top_k))
+        net = net.to(dev).eval()
         if self.dtype == "fp16":
             net = net.half()
         self.net = net.to(memory_format=torch.channels_last)
@@ -231,22 +424,46 @@ class SuperPointDetector:
         return True
 
     def InferenceSession(self, frames):
-        """frames: u8 [B, H, W] device tensor -> (heatmap f32 [B, H, W], descriptors f32 [B, 256, H/8, W/8])."""
+        """frames: u8 [B, H, W] device tensor (H, W multiples of 8) -> the network's outputs: heatmap
+        models (heatmap f32 [B, H, W], descriptor map f32 [B, D, h, w]); list models (keypoints
+        int64 [B, K, 2], scores f32 [B, K], descriptors f32 [B, K, D]). DISK models see the gray frame as
+        RGB (OnnxRuntime::ConvertGrayImageToRgbTensor, nn_feature_point_detector.cpp:96-99)."""
         import torch
 
         x = frames.unsqueeze(1).to(torch.float16 if self.dtype == "fp16" else torch.float32) / 255.0
+        if self.is_disk:
+            x = x.expand(-1, 3, -1, -1)
         x = x.contiguous(memory_format=torch.channels_last)
         with torch.inference_mode():
             return self.net(x)
 
-    def DetectGoodFeaturesWithDescriptor(self, frames, prior=None):
-        """nn_feature_point_detector_superpoint.cpp:8-77 for a batch of device frames [B, H, W] (H, W
-        multiples of 8). Returns (xy [B, S, 2], counts [B], descriptors [B, S, 256]) on the device:
-        the new features of each frame and, when kComputeDescriptors, their descriptors (the
-        reference also describes the priors: pass them through nn_descriptors)."""
+    def DetectGoodFeaturesWithDescriptor(self, frames, prior=None) -> NNResult:
+        """nn_feature_point_detector_superpoint.cpp:8-112 / nn_feature_point_detector_disk.cpp:8-112 for a
+        batch of device frames [B, H, W]. prior: None or a list (per frame) of (n_i, 2) (x, y) arrays
+        (the incoming all_pixel_uv). Returns an NNResult on the device."""
+        import torch
+
         if self.net is None:
             raise RuntimeError("Initialize() first")
-        heat, desc = self.InferenceSession(frames)
-        xy, cnt = nn_select(heat, self._options, prior)
-        d = nn_descriptors(desc, xy, cnt) if self._options.kComputeDescriptors else None
-        return xy, cnt, d
+        o = self._options
+        out = self.InferenceSession(frames)
+        if self.is_list_model:
+            kp, sc, dl = out
+            xy, cnt, d = nn_select_list(kp, sc, int(frames.shape[1]), int(frames.shape[2]), None, o, prior, dl)
+            return NNResult(xy, cnt, d, None)
+        heat, desc = out
+        xy, cnt = nn_select(heat, o, prior)
+        d = nn_descriptors(desc, xy, cnt)
+        pd = None
+        if prior is not None:  # ExtractDescriptorsForSelectedFeatures runs over all_pixel_uv (priors first)
+            p = max(max((len(q) for q in prior), default=0), 1)
+            pxy = np.zeros((len(prior), p, 2), np.float32)
+            for i, q in enumerate(prior):
+                q = np.asarray(q, np.float32).reshape(-1, 2)
+                pxy[i, :len(q)] = q
+            pcnt = torch.tensor([len(q) for q in prior], dtype=torch.int32, device=desc.device)
+            pd = nn_descriptors(desc, torch.from_numpy(pxy).to(desc.device), pcnt)
+        return NNResult(xy, cnt, d, pd)
+
+
+SuperPointDetector = NNFeaturePointDetector  # (kSuperpointHeatmap by default)

@@ -303,6 +303,25 @@ int fd_nn_select(fd_ctx *ctx, const float *heatmap, int heatmap_on_device, int b
                  int32_t out_stride, int32_t *out_counts, int outputs_on_device);
 
 /*
+ * fd_nn_select_list -- the keypoint-list models (kSuperpointNms / kDiskNms, whose networks run NMS
+ * in-graph): CreateMask + ArgSort + DirectlySelectGoodFeaturesWithDescriptors
+ * (nn_feature_point_detector.cpp:59-73, 204-230; nn_feature_point_detector_superpoint.cpp:106-109,
+ * nn_feature_point_detector_disk.cpp:106-109). Per frame b, counts[b] keypoints (u = x, v = y as int64
+ * pairs, [b * cap + i]) with scores [b * cap + i] and optionally descriptor rows
+ * cand_desc [(b * cap + i) * desc_dim ...]. Keypoints are visited by descending score; equal scores
+ * by descending raster index, then descending list index (SlamOperation::ArgSort is un-vendored: its
+ * order of equal scores is parity-unpinned). Masked ones (border, prior boxes) are skipped,
+ * the rest kept until max_features (priors included) with the min_feature_distance box rule.
+ * out_xy / out_counts as fd_nn_select; out_desc [b * out_stride + k][desc_dim] = the descriptor row
+ * of new feature k (new features only, as the reference's `descriptors`). Inputs (keypoints, scores,
+ * counts, cand_desc) are device pointers when inputs_on_device; outputs when outputs_on_device.
+ */
+int fd_nn_select_list(fd_ctx *ctx, const int64_t *keypoints, const float *scores, const int64_t *counts, int64_t cap,
+                      int inputs_on_device, int batch, int rows, int cols, const fd_nn_opts *opts,
+                      const float *prior_xy, const int32_t *prior_counts, const float *cand_desc, int desc_dim,
+                      float *out_desc, float *out_xy, int32_t out_stride, int32_t *out_counts, int outputs_on_device);
+
+/*
  * fd_nn_descriptors -- ExtractDescriptorsForSelectedFeatures (nn_feature_point_detector.cpp:163-193):
  * per feature (x, y) in xy [batch][stride][2] (counts as fd_brief_compute), bilinear samples at
  * (y / 8, x / 8) of each of the `channels` planes of the descriptor map (zero outside

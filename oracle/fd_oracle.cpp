@@ -550,6 +550,55 @@ int orc_nn_select(const float *heat, int rows, int cols, int border, int dist, i
     return n;
 }
 
+// ArgSort + DirectlySelectGoodFeaturesWithDescriptors (nn_feature_point_detector.cpp:204-230) for the
+// keypoint-list models (nn_feature_point_detector_superpoint.cpp:106-109): keypoints kp[i] = (u, v)
+// (int64, cast to int32 as :215), scores[i]. SlamOperation::ArgSort (un-vendored) is restated as an
+// ascending argsort; its order of equal scores is unpinned: taken here as ascending raster index,
+// then ascending list index, so the walk from the back (:213) visits equal scores by descending
+// raster index (the heatmap path's multimap order), then descending list index. Mask as
+// orc_nn_select (CreateMask, :59-73). Returns the number of new features; out_index receives the
+// list index of each (the descriptor rows gathered at :224-227).
+int orc_nn_select_list(const int64_t *kp, const float *scores, int64_t n, int rows, int cols, int border, int dist,
+                       int max_features, const float *prior_xy, int n_prior, float *out_xy, int32_t *out_index,
+                       int out_cap) {
+    std::vector<int32_t> mask(static_cast<size_t>(rows) * cols, 1);
+    auto draw = [&](int32_t row, int32_t col, int32_t radius) {  // DrawRectangleInMask (:75-82)
+        const int32_t r0 = std::max(0, row - radius), r1 = std::min(rows - 1, row + radius);
+        const int32_t c0 = std::max(0, col - radius), c1 = std::min(cols - 1, col + radius);
+        for (int32_t r = r0; r <= r1; ++r)
+            for (int32_t c = c0; c <= c1; ++c) mask[static_cast<size_t>(r) * cols + c] = 0;
+    };
+    for (int r = 0; r < rows; ++r)
+        for (int c = 0; c < cols; ++c)
+            if (r < border || r >= rows - border || c < border || c >= cols - border) mask[static_cast<size_t>(r) * cols + c] = 0;
+    for (int i = 0; i < n_prior; ++i) draw(static_cast<int32_t>(prior_xy[2 * i + 1]), static_cast<int32_t>(prior_xy[2 * i]), dist);
+    std::vector<int32_t> sorted(static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) sorted[i] = static_cast<int32_t>(i);
+    auto raster = [&](int32_t i) { return kp[2 * i + 1] * cols + kp[2 * i]; };
+    std::sort(sorted.begin(), sorted.end(), [&](int32_t a, int32_t b) {
+        if (scores[a] != scores[b]) return scores[a] < scores[b];
+        if (raster(a) != raster(b)) return raster(a) < raster(b);
+        return a < b;
+    });
+    size_t size = static_cast<size_t>(n_prior);
+    int nout = 0;
+    for (auto it = sorted.rbegin(); it != sorted.rend(); ++it) {
+        const int32_t index = *it;
+        const int32_t u = static_cast<int32_t>(kp[2 * index]), v = static_cast<int32_t>(kp[2 * index + 1]);
+        if (!mask[static_cast<size_t>(v) * cols + u]) continue;  // :216
+        if (nout < out_cap) {
+            out_xy[2 * nout] = static_cast<float>(u);
+            out_xy[2 * nout + 1] = static_cast<float>(v);
+            out_index[nout] = index;
+        }
+        ++nout;
+        ++size;
+        if (size >= static_cast<size_t>(max_features)) break;  // :219
+        draw(v, u, dist);
+    }
+    return nout;
+}
+
 // ExtractDescriptorsForSelectedFeatures (:163-193): map is [channels][map_rows][map_cols].
 void orc_nn_descriptors(const float *map, int channels, int map_rows, int map_cols, const float *xy, int n, float *out) {
     for (int i = 0; i < n; ++i) {

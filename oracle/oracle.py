@@ -52,6 +52,7 @@ def lib():
             "orc_make_frame": (None, [i32, u32, i32, i32, i32, _P]),
             "orc_brief": (None, [_P, i32, i32, _P, i32, i32, i32, i32, _P, _P, _P, _P]),
             "orc_nn_select": (i32, [_P, i32, i32, i32, i32, i32, f32, _P, i32, _P, i32]),
+            "orc_nn_select_list": (i32, [_P, _P, i64, i32, i32, i32, i32, i32, _P, i32, _P, _P, i32]),
             "orc_nn_descriptors": (None, [_P, i32, i32, i32, _P, i32, _P]),
             "orc_lsd_lines": (i64, [_P, i32, i32, _P, u32, _P, i64]),
             "orc_ref_state_new": (_P, []),
@@ -281,6 +282,22 @@ def nn_select(heat, border=3, dist=15, max_features=240, thr=0.1, prior=None):
     n = lib().orc_nn_select(_ptr(heat), R, C, border, dist, max_features, np.float32(thr), _ptr(pr), n_prior,
                             _ptr(out), cap)
     return out[:min(n, cap)].copy()
+
+
+def nn_select_list(kp, scores, rows, cols, border=3, dist=15, max_features=240, prior=None):
+    """ArgSort + DirectlySelectGoodFeaturesWithDescriptors (nn_feature_point_detector.cpp:204-230) on one
+    frame's keypoint list (kp [n, 2] int64 (u, v), scores [n]); returns (new features (m, 2) (x, y),
+    their list indices (m,)). Equal scores: see orc_nn_select_list (ArgSort unpinned)."""
+    kp = np.ascontiguousarray(kp, np.int64).reshape(-1, 2)
+    scores = np.ascontiguousarray(scores, np.float32)
+    pr = np.zeros((1, 2), np.float32) if prior is None or len(prior) == 0 else np.ascontiguousarray(prior, np.float32)
+    n_prior = 0 if prior is None else len(prior)
+    cap = max(max_features, 1) + 1
+    out = np.zeros((cap, 2), np.float32)
+    idx = np.zeros(cap, np.int32)
+    n = lib().orc_nn_select_list(_ptr(kp), _ptr(scores), len(scores), rows, cols, border, dist, max_features, _ptr(pr),
+                                 n_prior, _ptr(out), _ptr(idx), cap)
+    return out[:min(n, cap)].copy(), idx[:min(n, cap)].copy()
 
 
 def nn_descriptors(desc_map, xy):

@@ -133,3 +133,109 @@ def test_nn_descriptors_channels_last_in_place(sp, oracle):
     for f, n in ((0, 40), (1, 17)):
         exp = oracle.nn_descriptors(m[f], xy[f, :n])
         assert np.array_equal(b[f, :n].cpu().numpy().view(np.uint32), exp.view(np.uint32))
+
+
+# ------------------------------------------------------------------ keypoint-list models (kSuperpointNms / kDiskNms)
+def random_lists(rng, b, k, rows, cols, levels=16):
+    """Keypoint lists with many equal scores and some repeated pixels."""
+    kp = np.stack([rng.integers(0, cols, (b, k)), rng.integers(0, rows, (b, k))], -1).astype(np.int64)
+    kp[:, 1::7] = kp[:, 0::7][:, :kp[:, 1::7].shape[1]]  # repeats
+    sc = (rng.integers(0, levels, (b, k)) / levels).astype(np.float32)
+    return kp, sc
+
+
+@pytest.mark.parametrize("border,dist,maxf", [(3, 15, 240), (0, 4, 300), (5, 0, 50), (3, 6, 1), (2, 1, 5000)])
+def test_nn_select_list_matches_oracle(sp, oracle, border, dist, maxf):
+    rng = np.random.default_rng(border * 31 + dist)
+    rows, cols, b, k = 120, 160, 3, 2000
+    kp, sc = random_lists(rng, b, k, rows, cols)
+    counts = np.array([k, 700, 0], np.int64)
+    desc = rng.standard_normal((b, k, 64)).astype(np.float32)
+    prior = [np.array([(10.5, 20.7), (100.0, 50.0)], np.float32), np.zeros((0, 2), np.float32),
+             np.array([(5.0, 5.0)], np.float32)]
+    o = sp.Options(kInvalidBoundary=border, kMinFeatureDistance=dist, kMaxNumberOfDetectedFeatures=maxf)
+    for pr in (None, prior):
+        xy, cnt, d = sp.nn_select_list(kp, sc, rows, cols, counts, o, pr, desc)
+        for f in range(b):
+            p = None if pr is None or len(pr[f]) == 0 else pr[f]
+            exp, idx = oracle.nn_select_list(kp[f, :counts[f]], sc[f, :counts[f]], rows, cols, border, dist, maxf, p)
+            assert np.array_equal(features(xy, cnt, f), exp), (f, pr is None)
+            assert np.array_equal(d[f, :cnt[f]], desc[f, idx])
+
+
+def test_nn_select_list_device_and_checks(sp, oracle):
+    torch = pytest.importorskip("torch")
+    import feature_detector_amd as fd
+
+    rng = np.random.default_rng(5)
+    rows, cols, b, k = 96, 128, 2, 900
+    kp, sc = random_lists(rng, b, k, rows, cols, levels=1000)
+    desc = rng.standard_normal((b, k, 32)).astype(np.float32)
+    o = sp.Options(kMaxNumberOfDetectedFeatures=100, kMinFeatureDistance=5)
+    xy, cnt, d = sp.nn_select_list(torch.from_numpy(kp).cuda(), torch.from_numpy(sc).cuda(), rows, cols, None, o,
+                                   None, torch.from_numpy(desc).cuda())
+    torch.cuda.synchronize()
+    for f in range(b):
+        exp, idx = oracle.nn_select_list(kp[f], sc[f], rows, cols, 3, 5, 100)
+        assert np.array_equal(features(xy, cnt, f), exp)
+        assert np.array_equal(d[f, :len(idx)].cpu().numpy(), desc[f, idx])
+    bad = kp.copy()
+    bad[1, 3] = (cols, 0)  # outside the frame
+    with pytest.raises(fd.FdError):
+        sp.nn_select_list(bad, sc, rows, cols, None, o)
+    xy2, cnt2, _ = sp.nn_select_list(kp, sc, rows, cols, None, o)  # the context is clean after the refusal
+    assert np.array_equal(features(xy2, cnt2, 0), features(xy, cnt, 0))
+
+
+@pytest.mark.parametrize("model", ["kSuperpointHeatmap", "kSuperpointNms", "kDiskHeatmap", "kDiskNms"])
+def test_model_types_end_to_end(sp, oracle, model):
+    """Each ModelType on device frames (random weights): the GPU post-processing equals the oracle's on
+    the same network outputs; heatmap models also describe the prior features (all_pixel_uv)."""
+    torch = pytest.importorskip("torch")
+    rows, cols, n = 96, 128, 2
+    o = sp.Options(kModelType=model, kMaxImageRows=rows, kMaxImageCols=cols, kMaxNumberOfDetectedFeatures=60)
+    det = sp.NNFeaturePointDetector(o, top_k=400)
+    assert det.Initialize()
+    frames = torch.from_numpy(np.stack([oracle.make_frame("noise", 70 + i, rows, cols) for i in range(n)])).cuda()
+    prior = [np.array([(20.0, 30.0), (64.5, 40.2)], np.float32), np.zeros((0, 2), np.float32)]
+    out = det.InferenceSession(frames)
+    dim = 128 if "Disk" in model else 256
+    if model.endswith("Nms"):
+        kp, sc, dl = (t.float().cpu().numpy() if t.dtype != torch.int64 else t.cpu().numpy() for t in out)
+        xy, cnt, d = sp.nn_select_list(out[0], out[1], rows, cols, None, o, prior, out[2])
+        torch.cuda.synchronize()
+        assert tuple(d.shape) == (n, 61, dim)
+        for f in range(n):
+            p = prior[f] if len(prior[f]) else None
+            exp, idx = oracle.nn_select_list(kp[f], sc[f], rows, cols, 3, 15, 60, p)
+            assert len(exp) > 0
+            assert np.array_equal(features(xy, cnt, f), exp)
+            assert np.array_equal(d[f, :len(idx)].cpu().numpy(), dl[f, idx])
+    else:
+        heat, desc = out
+        heat_h, desc_h = heat.float().cpu().numpy(), desc.float().cpu().numpy()
+        assert desc_h.shape[1] == dim
+        xy, cnt = sp.nn_select(heat, o, prior)
+        d = sp.nn_descriptors(desc, xy, cnt)
+        torch.cuda.synchronize()
+        for f in range(n):
+            p = prior[f] if len(prior[f]) else None
+            exp = oracle.nn_select(heat_h[f], 3, 15, 60, 0.1, p)
+            assert len(exp) > 0
+            got = features(xy, cnt, f)
+            assert np.array_equal(got, exp)
+            assert np.array_equal(d[f, :len(got)].cpu().numpy().view(np.uint32),
+                                  oracle.nn_descriptors(desc_h[f], got).view(np.uint32))
+    res = det.DetectGoodFeaturesWithDescriptor(frames, prior)
+    xy_r, cnt_r, d_r = res
+    torch.cuda.synchronize()
+    assert tuple(d_r.shape)[2] == dim and int(cnt_r.min()) > 0
+    if model.endswith("Nms"):
+        assert res.prior_descriptors is None
+    else:  # descriptors of the incoming features too (all_pixel_uv), rows 0.. of each frame
+        pd = res.prior_descriptors.cpu().numpy()
+        assert pd.shape == (n, 2, dim) and not pd[1].any() and np.abs(pd[0]).sum() > 0
+        exp = oracle.nn_descriptors(desc_h[0], prior[0])
+        pxy = torch.from_numpy(np.stack([prior[0], np.zeros((2, 2), np.float32)])).cuda()
+        got = sp.nn_descriptors(desc, pxy, torch.tensor([2, 0], dtype=torch.int32, device="cuda"))
+        assert np.array_equal(got[0].cpu().numpy().view(np.uint32), exp.view(np.uint32))
