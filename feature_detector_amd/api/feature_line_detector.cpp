@@ -1,11 +1,11 @@
 // FeatureLineDetector over libfdhip.so (reference: src/feature_line_detector/feature_line_detector.cpp).
 //
-// DetectGoodFeatures (:12-54) is one fd_lsd_lines call for the frame: the GPU level-line map in compact
-// form and the library's host region-growing stage (fd_lines.cpp), which returns the accepted
-// rectangles. The members the reference exposes are then filled as it leaves them: pixels_ and
-// sorted_pixels_ from the dense GPU map (fd_lsd_map: bit-exact norm / validity / angle and the
-// scan-ordered valid list, :56-97) with each listed pixel's final is_used flag from
-// fd_lsd_lines_state, and rectangles_ from the segments.
+// DetectGoodFeatures (:12-54) is one fd_lsd_lines call for the frame (staged on the device once): the
+// GPU level-line map in compact form and the library's host region-growing stage (fd_lines.cpp),
+// which returns the accepted rectangles (rectangles_, features). The other members the reference
+// exposes are materialised on first access, as it leaves them: pixels_ and sorted_pixels_ from a dense
+// GPU map of the staged frame (fd_lsd_map: bit-exact norm / validity / angle and the scan-ordered
+// valid list, :56-97), with each listed pixel's final is_used flag from fd_lsd_lines_state.
 #include "feature_detector/feature_line_detector.h"
 
 #include <algorithm>
@@ -56,10 +56,16 @@ bool FeatureLineDetector::DetectGoodFeatures(const GrayImage &image, const uint3
 
     const fd_lsd_opts opts{options_.kMinValidGradientNorm, options_.kMinToleranceAngleResidualInRad,
                            options_.kMinValidLineLengthInPixel, options_.kMaxToleranceInlierRation};
+    const uint8_t *dframe = nullptr;
+    if (fd_ctx_stage(ctx_, image.data(), static_cast<int64_t>(image.rows()) * image.cols(), &dframe) != FD_OK) {
+        error_ = std::string("fd_ctx_stage: ") + fd_last_error(ctx_);
+        std::fprintf(stderr, "[feature_detector] %s\n", error_.c_str());
+        return false;
+    }
     std::vector<fd_lsd_rect> rects(256);
     int32_t count = 0;
     for (;;) {
-        const int rc = fd_lsd_lines(ctx_, image.data(), 0, 1, image.rows(), image.cols(), &opts, needed_feature_num,
+        const int rc = fd_lsd_lines(ctx_, dframe, 1, 1, image.rows(), image.cols(), &opts, needed_feature_num,
                                     rects.data(), static_cast<int32_t>(rects.size()), &count, 1);
         if (rc != FD_OK) {
             error_ = std::string("fd_lsd_lines: ") + fd_last_error(ctx_);
@@ -69,17 +75,11 @@ bool FeatureLineDetector::DetectGoodFeatures(const GrayImage &image, const uint3
         if (count <= static_cast<int32_t>(rects.size())) break;
         rects.resize(static_cast<size_t>(count));  // more segments than slots: run again with room for all
     }
-    if (!ComputeLineLevelAngleMap(image)) return false;
-
-    // is_used as the reference's regions leave it (every listed pixel; unlisted ones are invalid)
-    int64_t n = 0;
-    fd_lsd_lines_state(ctx_, nullptr, nullptr, nullptr, nullptr, 0, &n);
-    std::vector<int32_t> idx(static_cast<size_t>(n));
-    std::vector<float> nv(static_cast<size_t>(n)), av(static_cast<size_t>(n));
-    std::vector<uint8_t> used(static_cast<size_t>(n));
-    if (n > 0) fd_lsd_lines_state(ctx_, idx.data(), nv.data(), av.data(), used.data(), n, &n);
-    const int32_t pc = image.cols() - 1;
-    for (int64_t k = 0; k < n; ++k) pixels_(idx[k] / pc, idx[k] % pc).is_used = used[k] != 0;
+    staged_ = dframe;
+    last_rows_ = image.rows();
+    last_cols_ = image.cols();
+    last_min_norm_ = options_.kMinValidGradientNorm;
+    members_valid_ = false;
 
     rectangles_.clear();
     for (int32_t k = 0; k < count; ++k) {
@@ -101,17 +101,51 @@ bool FeatureLineDetector::DetectGoodFeatures(const GrayImage &image, const uint3
     return true;
 }
 
-// ComputeLineLevelAngleMap (feature_line_detector.cpp:56-97): map on the GPU, std::sort on the host.
-bool FeatureLineDetector::ComputeLineLevelAngleMap(const GrayImage &image) {
-    const int32_t rows = image.rows(), cols = image.cols();
+void FeatureLineDetector::Materialise() const {
+    if (members_valid_) return;
+    members_valid_ = true;
+    if (!ComputeLineLevelAngleMap()) return;
+    // is_used as the reference's regions leave it (every listed pixel; unlisted ones are invalid)
+    int64_t n = 0;
+    fd_lsd_lines_state(ctx_, nullptr, nullptr, nullptr, nullptr, 0, &n);
+    std::vector<int32_t> idx(static_cast<size_t>(n));
+    std::vector<float> nv(static_cast<size_t>(n)), av(static_cast<size_t>(n));
+    std::vector<uint8_t> used(static_cast<size_t>(n));
+    if (n > 0) fd_lsd_lines_state(ctx_, idx.data(), nv.data(), av.data(), used.data(), n, &n);
+    const int32_t pc = last_cols_ - 1;
+    for (int64_t k = 0; k < n; ++k) pixels_(idx[k] / pc, idx[k] % pc).is_used = used[k] != 0;
+}
+
+FeatureLineDetector::PixelMatrix &FeatureLineDetector::pixels() {
+    Materialise();
+    return pixels_;
+}
+const FeatureLineDetector::PixelMatrix &FeatureLineDetector::pixels() const {
+    Materialise();
+    return pixels_;
+}
+std::vector<FeatureLineDetector::PixelParam *> &FeatureLineDetector::sorted_pixels() {
+    Materialise();
+    return sorted_pixels_;
+}
+const std::vector<FeatureLineDetector::PixelParam *> &FeatureLineDetector::sorted_pixels() const {
+    Materialise();
+    return sorted_pixels_;
+}
+
+// ComputeLineLevelAngleMap (feature_line_detector.cpp:56-97): map on the GPU (the frame staged by the
+// last call), std::sort on the host.
+bool FeatureLineDetector::ComputeLineLevelAngleMap() const {
+    const int32_t rows = last_rows_, cols = last_cols_;
     const int32_t pr = rows - 1, pc = cols - 1;
     const size_t n = static_cast<size_t>(pr) * pc;
     std::vector<float> norm(n), angle(n);
     std::vector<uint8_t> valid(n);
     std::vector<int32_t> idx(n);
     int64_t count = 0;
-    const int rc = fd_lsd_map(ctx_, image.data(), 0, 1, rows, cols, options_.kMinValidGradientNorm, norm.data(),
-                              angle.data(), valid.data(), idx.data(), static_cast<int64_t>(n), &count, 0);
+    ++map_passes_;
+    const int rc = fd_lsd_map(ctx_, staged_, 1, 1, rows, cols, last_min_norm_, norm.data(), angle.data(), valid.data(),
+                              idx.data(), static_cast<int64_t>(n), &count, 0);
     if (rc != FD_OK) {
         error_ = std::string("fd_lsd_map: ") + fd_last_error(ctx_);
         std::fprintf(stderr, "[feature_detector] %s\n", error_.c_str());

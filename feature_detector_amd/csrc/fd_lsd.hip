@@ -15,6 +15,7 @@
 // host atan2f bit for bit over the whole LSD input domain (every half-integer (gx, gy) pair).
 #include "fd_device.h"
 #include "fd_kernels.h"
+#include "fd_corner_common.h"  // logical_block
 
 namespace fdk {
 
@@ -113,20 +114,25 @@ __device__ __forceinline__ void lsd_tile(const LsdArgs &a, int &f, int &strip, i
     f = w / a.chunks;
 }
 
-constexpr int kLsdGroup = 4;
-
 // Pass 1: maps + per (column, row-chunk) valid counts and valid-row bitmasks. A wave owns a strip of
 // 256 map columns (4 per lane, read as one dword per lane and row; the fifth column comes from the
 // right neighbour lane by DPP, lane 63 loads it) and walks chunk_h rows. Every map entry is written
-// exactly once per call (dword-per-lane stores of 4 columns); the angle map first gets 0 for the whole
-// row, then the valid pixels' angles: their (gx, gy) are queued in LDS and atan2f runs on full waves
-// of 64 queued pixels (on ~3 % of the pixels of a structured frame a per-row branch would run the
-// whole atan2f for most rows, VALU-bound; compacted it is a small fraction of the row work).
+// exactly once per call (dword-per-lane stores of 4 columns). Angles: the valid pixels' (gx, gy) are
+// queued in LDS and atan2f runs on waves of up to 64 queued pixels (on ~3 % of the pixels of a
+// structured frame a per-row branch would run the whole atan2f for most rows, VALU-bound; compacted it
+// is a small fraction of the row work), writing into the group's angle rows in LDS (0 elsewhere);
+// after each group of kLsdGroup rows the queue is drained and the rows go to the map as whole rows
+// (scattered 4-byte stores into the map would cost partial-line writes and their read-modify-write).
+// Workgroups are placed XCD-aware (logical_block): an XCD holds consecutive strips and row chunks of
+// one frame, so the column (strip edge) and row (chunk edge) neighbours a wave reads come from its
+// own L2.
 constexpr int kLsdQueue = 64 + 256;  // queued valid pixels per wave: < 64 left + one row (256 columns)
+constexpr int kLsdGroup = 4;         // rows per group (row loads in flight; angle rows buffered in LDS)
 
 struct LsdQueue {
     uint32_t sd[4][kLsdQueue];   // (s = ad + bc, d = ad - bc) as two int16
-    uint32_t idx[4][kLsdQueue];  // map index in the frame
+    uint32_t idx[4][kLsdQueue];  // position in the wave's angle rows (row in group * 256 + column)
+    float ang[4][kLsdGroup][256];  // the group's angle rows, stored to the map whole once drained
 };
 
 template <bool ALIGNED>
@@ -139,7 +145,7 @@ __device__ __forceinline__ uint32_t lsd_load4(__amdgpu_buffer_rsrc_t r, int32_t 
 // atan2f(gx, -gy) (:85) of the queued pixels, 64 at a time while at least `keep_below` remain (0 at
 // the end: all), written into the angle map. One out-of-line copy: the atan2f body (correctly rounded
 // divisions included) is large, and a copy per unrolled row would not fit the instruction cache.
-__device__ __noinline__ int lsd_drain(const uint32_t *qsd, const uint32_t *qidx, int qn, int keep_below, float *amap) {
+__device__ __noinline__ int lsd_drain(const uint32_t *qsd, const uint32_t *qidx, int qn, int keep_below, float *arow) {
     const int lane = lane_id();
     while (qn >= keep_below && qn > 0) {
         const int take = min(qn, kWave);
@@ -148,7 +154,7 @@ __device__ __noinline__ int lsd_drain(const uint32_t *qsd, const uint32_t *qidx,
             const int sv = static_cast<int16_t>(e & 0xFFFFu), dv = static_cast<int16_t>(e >> 16);
             const float gx = static_cast<float>(sv) / 2.0f;  // :80-81
             const float gy = static_cast<float>(dv) / 2.0f;
-            amap[qidx[qn - take + lane]] = fd_atan2f(gx, -gy);
+            arow[qidx[qn - take + lane]] = fd_atan2f(gx, -gy);
         }
         qn -= take;
     }
@@ -182,25 +188,40 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     const auto ra = make_rsrc(amap, amap ? 4 * mbytes : 0u);
     const auto rv = make_rsrc(a.valid ? a.valid + mbase : nullptr, a.valid ? mbytes : 0u);
 
-    auto put = [&](int r, const float (&nv)[4], const float (&av)[4], uint32_t vb) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    struct alignas(4) F4 { float x, y, z, w; };
+    // one map row's 4 angle entries of this lane
+    auto put_angle = [&](int r, const float (&av)[4]) {
+        if constexpr (INTERIOR) {
+            __builtin_amdgcn_raw_buffer_store_b128(
+                u4{__float_as_uint(av[0]), __float_as_uint(av[1]), __float_as_uint(av[2]), __float_as_uint(av[3])}, ra,
+                4 * (r * mc + c0), 0, 0);
+            return;
+        }
+        if (!a.angle) return;
+        const int64_t i = mbase + static_cast<int64_t>(r) * mc + c0;
+        if (full) {
+            *reinterpret_cast<F4 *>(a.angle + i) = F4{av[0], av[1], av[2], av[3]};
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                if (colw[m]) a.angle[i + m] = av[m];
+        }
+    };
+    // norm and valid of one map row (the angles follow per group, put_angle)
+    auto put = [&](int r, const float (&nv)[4], uint32_t vb) {
         if constexpr (INTERIOR) {
             // (null maps: a zero-range resource drops the stores)
             const int o = r * mc + c0;  // < 2^31: checked on the host
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
             __builtin_amdgcn_raw_buffer_store_b128(
                 u4{__float_as_uint(nv[0]), __float_as_uint(nv[1]), __float_as_uint(nv[2]), __float_as_uint(nv[3])}, rn,
-                4 * o, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                u4{__float_as_uint(av[0]), __float_as_uint(av[1]), __float_as_uint(av[2]), __float_as_uint(av[3])}, ra,
                 4 * o, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(vb, rv, o, 0, 0);
             return;
         }
         const int64_t i = mbase + static_cast<int64_t>(r) * mc + c0;
         if (full) {
-            struct alignas(4) F4 { float x, y, z, w; };
             if (a.norm) *reinterpret_cast<F4 *>(a.norm + i) = F4{nv[0], nv[1], nv[2], nv[3]};
-            if (a.angle) *reinterpret_cast<F4 *>(a.angle + i) = F4{av[0], av[1], av[2], av[3]};
             typedef uint32_t u32a1 __attribute__((aligned(1)));
             if (a.valid) *reinterpret_cast<u32a1 *>(a.valid + i) = vb;
         } else {
@@ -208,7 +229,6 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
             for (int m = 0; m < 4; ++m)
                 if (colw[m]) {
                     if (a.norm) a.norm[i + m] = nv[m];
-                    if (a.angle) a.angle[i + m] = av[m];
                     if (a.valid) a.valid[i + m] = static_cast<uint8_t>(vb >> (8 * m));
                 }
         }
@@ -216,8 +236,14 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     // Map rows 0 and rows-2 lie outside the scan (:71): zeros, written by the first / last chunk.
     {
         const float z[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (chunk == 0) put(0, z, z, 0u);
-        if (r1 == rows - 2) put(rows - 2, z, z, 0u);
+        if (chunk == 0) {
+            put(0, z, 0u);
+            put_angle(0, z);
+        }
+        if (r1 == rows - 2) {
+            put(rows - 2, z, 0u);
+            put_angle(rows - 2, z);
+        }
     }
     // I(r, c0 .. c0+3) and I(r, c0+4): lane 63 loads the next dword (the others take byte 0 of the
     // right lane's dword). Rows/columns past the frame read 0 and only feed unscanned entries.
@@ -232,9 +258,10 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     int cnt[4] = {0, 0, 0, 0};
     uint32_t word[4] = {0, 0, 0, 0};
     int qn = 0;  // wave-uniform queue length
-    auto row = [&](int rr, uint32_t t, uint32_t te, uint32_t b, uint32_t be) {
+    float *const arows = &Q.ang[wv][0][0];  // [kLsdGroup][256]
+    auto row = [&](int rr, int slot, uint32_t t, uint32_t te, uint32_t b, uint32_t be) {
         const uint32_t t4 = fifth(t, te), b4 = fifth(b, be);
-        float nv[4], av[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        float nv[4];
         int sv[4], dv[4];
         bool vv[4];
         uint32_t vb = 0;
@@ -260,13 +287,14 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
             cnt[m] += vv[m] ? 1 : 0;
             word[m] |= static_cast<uint32_t>(vv[m]) << ((rr - r0) & 31);
         }
-        put(rr, nv, av, vb);
-        if (amap) {  // queue the valid pixels' (s, d) and map index
+        put(rr, nv, vb);
+        if (amap) {  // zero angle row in LDS; queue the valid pixels' (s, d) and row position
+            *reinterpret_cast<F4 *>(arows + slot * 256 + 4 * lane) = F4{0.0f, 0.0f, 0.0f, 0.0f};
             const uint64_t b0 = ballot(vv[0]), b1 = ballot(vv[1]), b2 = ballot(vv[2]), b3 = ballot(vv[3]);
             const int tot = popc64(b0) + popc64(b1) + popc64(b2) + popc64(b3);
             if (tot) {
                 int pos = mbcnt64(b3, mbcnt64(b2, mbcnt64(b1, mbcnt64(b0, qn))));
-                const uint32_t i0 = static_cast<uint32_t>(rr) * static_cast<uint32_t>(mc) + static_cast<uint32_t>(c0);
+                const uint32_t i0 = static_cast<uint32_t>(slot * 256 + 4 * lane);
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
                     if (vv[m]) {
@@ -279,7 +307,7 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    qn = __builtin_amdgcn_readfirstlane(lsd_drain(qsd, qidx, qn, kWave, amap));
+                    qn = __builtin_amdgcn_readfirstlane(lsd_drain(qsd, qidx, qn, kWave, arows));
                 }
             }
         }
@@ -289,7 +317,23 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
 #pragma unroll
         for (int i = 0; i < kLsdGroup; ++i) {
             if (r + i >= r1) break;  // uniform
-            row(r + i, P[i], E[i], P[i + 1], E[i + 1]);
+            row(r + i, i, P[i], E[i], P[i + 1], E[i + 1]);
+        }
+        if (amap) {  // the group's angles: drain the queue into the LDS rows, then store the rows whole
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (qn > 0) qn = __builtin_amdgcn_readfirstlane(lsd_drain(qsd, qidx, qn, 0, arows));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int i = 0; i < kLsdGroup; ++i) {
+                if (r + i >= r1) break;  // uniform
+                const F4 v = *reinterpret_cast<const F4 *>(arows + i * 256 + 4 * lane);
+                const float av[4] = {v.x, v.y, v.z, v.w};
+                put_angle(r + i, av);
+            }
         }
         // rows r0 + 32k .. r0 + 32k + 31 share a bitmask word (kLsdGroup divides 32)
         const int done = r + kLsdGroup - r0;
@@ -317,12 +361,6 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
         for (int i = 0; i <= kLsdGroup; ++i) ld(r + 2 * kLsdGroup + i, A[i], AE[i]);
         group(r + kLsdGroup, B, BE);
     }
-    if (amap && qn > 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        lsd_drain(qsd, qidx, qn, 0, amap);
-    }
 #pragma unroll
     for (int m = 0; m < 4; ++m)
         if (INTERIOR || colv[m]) a.col_cnt[(static_cast<int64_t>(f) * a.chunks + chunk) * mc + c0 + m] = cnt[m];
@@ -331,7 +369,7 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
 template <bool ALIGNED>
 __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
     __shared__ LsdQueue Q;
-    int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    int w = __builtin_amdgcn_readfirstlane(logical_block() * 4 + (threadIdx.x >> 6));
     const int strip = w % a.strips4;
     w /= a.strips4;
     const int chunk = w % a.chunks;

@@ -334,6 +334,7 @@ struct alignas(16) SelectLds {
     uint32_t wtot[16];
     uint32_t gcount;
     uint32_t seg_more[2];
+    uint32_t lb_rng[2];  // local-digit bucket sort: the sub-chunk's smallest / largest 32-bit key
     int ff_res[2];  // first_le results (alternating slots)
     int s_done, s_acc;
     uint64_t st[32];  // diagnostic phase clocks (a.stamps only); 16..31 free for ad-hoc probes
@@ -1003,11 +1004,12 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                                 const uint32_t idx = a.tie_idx_desc ? static_cast<uint32_t>(sk) : ~static_cast<uint32_t>(sk);
                                 keep = true;  // (an out-of-range index is kept: place() raises its guard)
                                 if (idx < static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols)) {
-                                    const uint32_t y = idx / static_cast<uint32_t>(cols);
+                                    const uint32_t y = udiv16q(idx, static_cast<uint32_t>(cols), rcp_cols);
                                     const uint32_t x = idx - y * static_cast<uint32_t>(cols);
                                     if (fmask && !((fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u))
                                         keep = false;
-                                    const int cell = static_cast<int>((y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1));
+                                    const int cell = static_cast<int>((udiv16q(y, s1, rcp_s1) + 1) * static_cast<uint32_t>(gw2) +
+                                                                      (udiv16q(x, s1, rcp_s1) + 1));
                                     const uint32_t e = (y << 16) | x;
                                     const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
 #pragma unroll
@@ -1101,7 +1103,82 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         __syncthreads();
                         FD_STAMP(13);  // bucket rank + place
                     } else {
-                    // Merge sort of unique keys, descending: rank inside runs of 64 by counting larger
+                    // Local-digit bucket placement (the level's digit left a bin of more than kBucketMax
+                    // keys, or the prefilter dropped keys: FAST's clustered top responses): the same
+                    // placement on a digit of the sub-chunk's own 32-bit key range, kLocalBins buckets.
+                    // Falls back to the merge sort below when a bucket still holds more than kBucketMax.
+                    constexpr int kLocalBins = 1024;
+                    constexpr int kPer = (kSelectChunk + NT - 1) / NT;
+                    uint32_t *const lcnt = L.pk32;  // [kLocalBins + 1] counts, then suffix sums (place rewrites pk32)
+                    if (tid == 0) {
+                        L.lb_rng[0] = 0xFFFFFFFFu;
+                        L.lb_rng[1] = 0u;
+                    }
+                    for (int b = tid; b <= kLocalBins; b += nthr) lcnt[b] = 0u;
+                    uint64_t kk[kPer];
+                    uint32_t kmn = 0xFFFFFFFFu, kmx = 0u;
+#pragma unroll
+                    for (int j = 0; j < kPer; ++j) {
+                        const int p = tid + j * nthr;
+                        kk[j] = p < c ? unsorted[p] : 0ull;
+                        if (p < c) {
+                            kmn = min(kmn, static_cast<uint32_t>(kk[j] >> 32));
+                            kmx = max(kmx, static_cast<uint32_t>(kk[j] >> 32));
+                        }
+                    }
+                    for (int o = kWave / 2; o > 0; o >>= 1) {
+                        kmn = min(kmn, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmn), o)));
+                        kmx = max(kmx, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmx), o)));
+                    }
+                    __syncthreads();  // (lb_rng, lcnt initialised)
+                    if (lane == 0 && kmn <= kmx) {
+                        atomicMin(&L.lb_rng[0], kmn);
+                        atomicMax(&L.lb_rng[1], kmx);
+                    }
+                    __syncthreads();
+                    const uint32_t lo32 = L.lb_rng[0], rng = L.lb_rng[1] - L.lb_rng[0];
+                    const int lsh = rng < static_cast<uint32_t>(kLocalBins) ? 0 : (32 - __builtin_clz(rng)) - 10;
+                    uint32_t dg[kPer], sl[kPer];
+#pragma unroll
+                    for (int j = 0; j < kPer; ++j) {
+                        dg[j] = (static_cast<uint32_t>(kk[j] >> 32) - lo32) >> lsh;
+                        sl[j] = 0;
+                        if (tid + j * nthr < c) sl[j] = atomicAdd(&lcnt[dg[j]], 1u);
+                    }
+                    __syncthreads();
+                    FD_STAMP(10);
+                    suffix(lcnt, kLocalBins);  // lcnt[b] = keys of digits >= b (descending placement)
+                    bool lbig = false;
+#pragma unroll
+                    for (int j = 0; j < kPer; ++j)
+                        if (tid + j * nthr < c) lbig = lbig || lcnt[dg[j]] - lcnt[dg[j] + 1] > static_cast<uint32_t>(kBucketMax);
+                    if (!__syncthreads_or(lbig)) {
+#pragma unroll
+                        for (int j = 0; j < kPer; ++j)
+                            if (tid + j * nthr < c) tmp[min(lcnt[dg[j] + 1] + sl[j], static_cast<uint32_t>(kSelectChunk - 1))] = kk[j];
+                        __syncthreads();
+                        FD_STAMP(11);  // local bucket scatter
+                        uint32_t pos[kPer];
+#pragma unroll
+                        for (int j = 0; j < kPer; ++j) {
+                            pos[j] = 0;
+                            if (tid + j * nthr >= c) continue;
+                            const uint32_t g0 = lcnt[dg[j] + 1], gn = lcnt[dg[j]] - g0;
+                            uint32_t r = 0;
+                            for (uint32_t q = 0; q < gn; ++q) {
+                                const uint64_t v = tmp[g0 + q];
+                                r += (v > kk[j] || (v == kk[j] && q < sl[j])) ? 1u : 0u;
+                            }
+                            pos[j] = g0 + r;
+                        }
+                        __syncthreads();  // lcnt (pk32) is read above, rewritten by place
+#pragma unroll
+                        for (int j = 0; j < kPer; ++j)
+                            if (tid + j * nthr < c) place(static_cast<int>(min(pos[j], static_cast<uint32_t>(kSelectChunk - 1))), kk[j]);
+                        __syncthreads();
+                        FD_STAMP(13);  // local bucket rank + place
+                    } else {
+                    // Merge sort, descending: rank inside runs of 64 by counting larger
                     // keys (broadcast LDS reads), then log2 merge levels where each key moves to
                     // (its offset in its run) + (number of larger keys in the sibling run, by binary search).
                     const int c64 = (c + 63) & ~63;
@@ -1155,6 +1232,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     for (int i = tid; i < c; i += nthr) place(i, src[i]);
                     __syncthreads();
                     FD_STAMP(13);  // place
+                    }
                     }
                     if (!a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
                         const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;

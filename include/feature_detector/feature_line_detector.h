@@ -77,37 +77,49 @@ public:
 
     bool DetectGoodFeatures(const GrayImage &image, const uint32_t needed_feature_num, std::vector<Vec4> &features);
 
-    // Reference for member variables.
+    // Reference for member variables. pixels() and sorted_pixels() are materialised on first access
+    // after a call (one dense GPU map of the frame staged by that call): DetectGoodFeatures itself is a
+    // single fd_lsd_lines pass.
     Options &options() { return options_; }
-    PixelMatrix &pixels() { return pixels_; }
-    std::vector<PixelParam *> &sorted_pixels() { return sorted_pixels_; }
+    PixelMatrix &pixels();
+    std::vector<PixelParam *> &sorted_pixels();
     std::vector<RectangleParam> &rectangles() { return rectangles_; }
 
     // Const reference for member variables.
     const Options &options() const { return options_; }
-    const PixelMatrix &pixels() const { return pixels_; }
-    const std::vector<PixelParam *> &sorted_pixels() const { return sorted_pixels_; }
+    const PixelMatrix &pixels() const;
+    const std::vector<PixelParam *> &sorted_pixels() const;
     const std::vector<RectangleParam> &rectangles() const { return rectangles_; }
 
-    // MI355X extensions.
+    // MI355X extensions: GPU ordinal, last libfdhip error, and the number of dense map passes run so
+    // far to materialise pixels() / sorted_pixels().
     void set_device(int device);
     const std::string &last_error() const { return error_; }
+    int map_passes() const { return map_passes_; }
 
 private:
     bool EnsureContext();
-    // pixels_ / sorted_pixels_ as the reference leaves them (:56-97), from the GPU level-line map
-    bool ComputeLineLevelAngleMap(const GrayImage &image);
+    // pixels_ / sorted_pixels_ as the reference leaves them (:56-97), from the GPU level-line map of
+    // the frame staged by the last call, with each listed pixel's final is_used flag
+    bool ComputeLineLevelAngleMap() const;
+    void Materialise() const;
 
 private:
     Options options_;
 
-    PixelMatrix pixels_;
-    std::vector<PixelParam *> sorted_pixels_;
+    mutable PixelMatrix pixels_;
+    mutable std::vector<PixelParam *> sorted_pixels_;
     std::vector<RectangleParam> rectangles_;
+    // state of the last call, for the lazily materialised members
+    mutable bool members_valid_ = true;
+    const uint8_t *staged_ = nullptr;  // device copy of the last frame (owned by the context)
+    int32_t last_rows_ = 0, last_cols_ = 0;
+    float last_min_norm_ = 0.0f;
+    mutable int map_passes_ = 0;
 
     fd_ctx *ctx_ = nullptr;
     int device_ = -1;
-    std::string error_;
+    mutable std::string error_;
 };
 
 }  // namespace feature_detector

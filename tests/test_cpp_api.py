@@ -100,6 +100,10 @@ def test_line_demo_reference_counts(tmp_path, image_png, oracle, ref_counts):
     assert r["ok"] is True
     assert r["n_valid"] == ref_counts["image_png"]["lsd_valid"] == r["n_sorted"]
     assert len(r["lines"]) == ref_counts["image_png"]["lsd_lines"]
+    assert r["map_passes"] == 1  # pixels() / sorted_pixels() materialised once, on first access
+    # members never read: DetectGoodFeatures is the single fd_lsd_lines pass, same segments
+    (q,) = _run("fd_demo_lines", image_png, tmp_path, 1)
+    assert q["ok"] is True and q["map_passes"] == 0 and q["lines"] == r["lines"]
 
 
 @pytest.mark.gpu
