@@ -35,8 +35,8 @@ MFMA_PEAK_TFLOPS_FP16 = 2500.0  # dense BF16/FP16 MFMA (MI355X_MICROARCH.md: ~2.
 # HBM traffic per launch measured with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) and
 # corrected by the calibrated gfx950 factor (tools/gpu_traffic.sh, tools/calib/fetch_calib.hip).
 # (tools/gpu_round_pmc.sh + tools/make_round_profiles.py write both files)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r02_traffic.json")
-SQ_FILE = os.path.join(ROOT, "profiles", "r02_sq.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_traffic.json")
+SQ_FILE = os.path.join(ROOT, "profiles", "r03_sq.json")
 
 
 def north_star_issue():
@@ -47,12 +47,14 @@ def north_star_issue():
     except (OSError, KeyError, ValueError):
         return None
     return {"source": os.path.relpath(SQ_FILE, ROOT),
+            "valu_issue_slot_busy": q.get("valu_issue_slot_busy"),
             "simd_valu_utilisation": q["simd_valu_utilisation"],
             "waves_resident_per_simd": q["waves_resident_per_simd"],
             "wave_time_issue_stalled": q["wave_time_issue_stalled"],
-            "note": ("neither HBM nor VALU issue saturates: SIMD VALU utilisation = SQ_INSTS_VALU x 2 cycles / "
-                     "(1024 SIMDs x kernel cycles); the rest is dependency latency at ~3 resident waves per SIMD "
-                     "(LDS-limited occupancy) -- DESIGN.md section 4")}
+            "note": ("VALU issue-slot bound: one quad-cycle issue slot per wave64 VALU instruction (dual-issued "
+                     "pairs share one; measured per opcode class in profiles/r03_valu_probe.txt), busy = "
+                     "(SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) x 4 / (1024 SIMDs x kernel cycles); HBM is ~10 % "
+                     "-- DESIGN.md section 5")}
 
 
 def measured_traffic(key):
@@ -357,6 +359,7 @@ class phase:
 
     def __enter__(self):
         self.torch.cuda.synchronize()
+        print(f"[bench] {self.name}", file=sys.stderr, flush=True)  # progress (stdout keeps the one JSON line)
         try:
             self.torch.cuda.nvtx.range_push("fdbench:" + self.name)
         except Exception:
@@ -754,16 +757,19 @@ def main():
             del pool3
         kb = ns_batch * 1080 * 1920
         ach = kb / (kms * 1e-3) / 1e9
+        ns_issue = north_star_issue()
         out["north_star"] = {
             "workload": "shi_tomasi response+NMS + grid NMS, 1920x1080 gray, batch 256/GPU, noise",
             "mpix_s_per_gpu": round(d2 * kb / s2 / 1e6, 1), "ms_per_step": round(s2 / d2 * 1e3, 4),
-            "kernel": "k_corner<ShiTomasi>", "kernel_ms": round(kms, 4),
+            "kernel": "k_corner_lp<ShiTomasi, 4 px/lane>", "kernel_ms": round(kms, 4),
             "kernel_mpix_s": round(kb / (kms * 1e-3) / 1e6, 1),
             "kernel_ms_checker": round(kms_checker, 4),
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb,
-                         "traffic": measured_traffic("northstar_k_corner")[0]},
-            "issue": north_star_issue(),
+                         "traffic": measured_traffic("northstar_k_corner")[0],
+                         # the bound that binds: VALU issue slots (SQ pass of the same kernel, profiles/)
+                         "valu_frac": ns_issue["valu_issue_slot_busy"] if ns_issue else None},
+            "issue": ns_issue,
             "ties": ties_ns,
         }
 

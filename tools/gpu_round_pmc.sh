@@ -2,7 +2,7 @@
 # shapes' kernels and SQ counters of the north-star kernel. usage: bash tools/gpu_round_pmc.sh <tag>
 set -e
 cd $GRAFT_REPO_ROOT
-TAG=${1:-r02}
+TAG=${1:-r03}
 export TMPDIR=/tmp
 O=gpurun_out/$TAG/pmc
 mkdir -p $O
@@ -21,8 +21,8 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   run lsdd_$ctr $ctr -- python3 tools/profile_kernels.py --shape lsd --kind dense --calls 2
   run lsdc_$ctr $ctr -- python3 tools/profile_kernels.py --shape lsd --kind compact --calls 2
 done
-run ns_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- python3 tools/profile_kernels.py --shape northstar --kind shi_tomasi --calls 3
-run fast_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -- python3 tools/profile_kernels.py --shape fast720 --calls 3
+run ns_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -- python3 tools/profile_kernels.py --shape northstar --kind shi_tomasi --calls 3
+run fast_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -- python3 tools/profile_kernels.py --shape fast720 --calls 3
 rm -rf $O/raw
 python3 tools/make_round_profiles.py $O/summary.csv $TAG > $O/sq_summary.json
 echo ok
