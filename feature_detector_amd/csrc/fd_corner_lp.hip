@@ -163,19 +163,21 @@ __device__ __forceinline__ void lp_flush(uint32_t &n, const uint32_t *sl, const 
     uint32_t base = 0;
     if (lane_id() == 0) base = atomicAdd(&a.list_count[f], tot);
     base = __builtin_amdgcn_readfirstlane(base);
-    float *dr = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
-    uint32_t *di = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    // The frame's list as two buffer resources of list_cap entries: a position past the capacity is
+    // outside the range and its store is dropped by the hardware (no compare, no 64-bit address math;
+    // the launch keeps list_cap * 4 < 2^32, lp_list_ok).
+    const uint32_t cap_b = static_cast<uint32_t>(a.list_cap) * 4u;
+    const auto rr = make_rsrc(a.list_resp + static_cast<int64_t>(f) * a.list_cap, cap_b);
+    const auto ri = make_rsrc(a.list_idx + static_cast<int64_t>(f) * a.list_cap, cap_b);
     uint32_t off = base;
     for (int j = 0; j < jmax; ++j) {
         const uint64_t b = ballot(n > static_cast<uint32_t>(j));
         if (n > static_cast<uint32_t>(j)) {
             const float r = lp_resp<KIND>(sl, j);
             if (hist) atomicAdd(&hist[((float_key(r) - a.key_base) << a.key_lz) >> 20], 1u);
-            const int64_t pos = static_cast<int64_t>(mbcnt64(b, static_cast<int>(off)));
-            if (pos < a.list_cap) {
-                dr[pos] = r;
-                di[pos] = sl[j * 128 + 64];
-            }
+            const uint32_t pos4 = static_cast<uint32_t>(mbcnt64(b, static_cast<int>(off))) << 2;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rr, static_cast<int>(pos4), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(sl[j * 128 + 64], ri, static_cast<int>(pos4), 0, 0);
         }
         off += static_cast<uint32_t>(popc64(b));
     }
@@ -313,6 +315,11 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
 #endif
         float rsp[3][PX];
 #if FD_LP_FP
+        // vertical pair sums shared by two consecutive output rows: an even step forms
+        // h(ri-2) + h(ri-1) and adds h(ri-3), the next step adds h(ri) to the same pair (exact integers)
+        f2 pxx[PX / 2], pyy[PX / 2], pxy[PX / 2];
+#endif
+#if FD_LP_FP
 #pragma unroll
         for (int s = 0; s < 3; ++s)
 #pragma unroll
@@ -428,9 +435,20 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
                 for (int m = 0; m < PX; m += 2) {
 #if FD_LP_FP
                     const int k = m / 2;
-                    const f2 v = corner_response_fp<KIND>((hxx[s][k] + hxx[su][k]) + hxx[sc][k],
-                                                          (hyy[s][k] + hyy[su][k]) + hyy[sc][k],
-                                                          (hxy[s][k] + hxy[su][k]) + hxy[sc][k], a.thr);
+                    f2 sxx, syy, sxy;
+                    if constexpr (t % 2 == 0) {
+                        pxx[k] = hxx[su][k] + hxx[sc][k];
+                        pyy[k] = hyy[su][k] + hyy[sc][k];
+                        pxy[k] = hxy[su][k] + hxy[sc][k];
+                        sxx = hxx[s][k] + pxx[k];
+                        syy = hyy[s][k] + pyy[k];
+                        sxy = hxy[s][k] + pxy[k];
+                    } else {
+                        sxx = pxx[k] + hxx[sc][k];
+                        syy = pyy[k] + hyy[sc][k];
+                        sxy = pxy[k] + hxy[sc][k];
+                    }
+                    const f2 v = corner_response_fp<KIND>(sxx, syy, sxy, a.thr);
 #else
                     const f2 v = corner_response_lp<KIND>(
                         add3u(hxx[s][m], hxx[su][m], hxx[sc][m]), add3u(hxx[s][m + 1], hxx[su][m + 1], hxx[sc][m + 1]),

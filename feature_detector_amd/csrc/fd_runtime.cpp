@@ -322,6 +322,8 @@ struct PointGeom {
 // ones narrow lanes (more waves, shorter serial row chains). FD_PX overrides (A/B).
 int corner_px(int kind, int batch, int rows, int cols, float thr) {
     if (kind == FD_FAST || !(thr >= 0.0f)) return 0;
+    // k_corner_lp addresses a frame's list through a buffer resource: list_cap * 4 bytes < 2^32
+    if (static_cast<int64_t>(rows) * cols >= (int64_t(1) << 30)) return 0;
     if (const char *e = std::getenv("FD_PX")) {
         const int v = std::atoi(e);
         if (v == 0 || v == 2 || v == 4 || v == 8) return v;
