@@ -167,6 +167,19 @@ __global__ __launch_bounds__(256) void probe(uint64_t *cyc, uint32_t *sink, uint
         if constexpr (CLASS == 67) { BODY4(R8(X67)) }
         if constexpr (CLASS == 68) { BODY4(R8(X68)) }
         if constexpr (CLASS == 69) { BODY4(R8(X69)) }
+        // mixes: does a dual-capable op (v_add/mul_f32) issue beside a packed / 3-operand one?
+#define M70(i) PK(i) X28(i)
+#define M71(i) PK(i) X27(i) X28(i)
+#define M72(i) MAX3(i) X28(i)
+#define M73(i) X27(i) X28(i)
+#define M74(i) X36(i) X28(i) X52(i)
+#define M75(i) PK(i) X41(i)
+        if constexpr (CLASS == 70) { BODY4(R8(M70)) }
+        if constexpr (CLASS == 71) { BODY4(R8(M71)) }
+        if constexpr (CLASS == 72) { BODY4(R8(M72)) }
+        if constexpr (CLASS == 73) { BODY4(R8(M73)) }
+        if constexpr (CLASS == 74) { BODY4(R8(M74)) }
+        if constexpr (CLASS == 75) { BODY4(R8(M75)) }
         // big loop bodies (instruction-fetch test): 64x the 32-instruction block, 1/64 of the iterations
         if constexpr (CLASS == 13) { if (it % 64 == 0) { BIG64(BODY4(R8(A3))) } }
         if constexpr (CLASS == 14) { if (it % 64 == 0) { BIG64(BODY4(R8(ADD))) } }
@@ -179,7 +192,7 @@ __global__ __launch_bounds__(256) void probe(uint64_t *cyc, uint32_t *sink, uint
 static const char *kNames[] = {"v_add3_u32", "v_add_u32_e32", "v_mad_i32_i24", "v_fma_f32", "v_pk_fma_f32",
                                "dpp wave_shr", "dpp row_shr", "v_sub_u32_sdwa", "v_rsq_f32", "v_max3_f32",
                                "cmp+addc (2)", "cmp_e64+cndmask (2)", "pk_fma+add3 (2)",
-                               "v_add3 16KB body", "v_add_e32 8KB body", "v_pk_add_u16", "v_pk_mad_u16", "v_pk_mul_lo_u16", "v_dot2_u32_u16", "v_dot2_i32_i16", "v_dot4_u32_u8", "v_perm_b32", "v_bfe_u32", "v_lshl_add_u32", "v_cndmask_b32_e32", "v_cmp_gt_f32_e32", "v_max_f32_e32", "v_mul_f32_e32", "v_add_f32_e32", "v_mul_u32_u24_e32", "v_mad_u32_u24", "v_addc_co_u32_e32", "v_alignbyte_b32", "v_mov_b32_e32", "dpp quad_perm", "v_add_u32_dpp", "v_pk_add_f32", "v_sqrt_f32", "rsq+fma (2)", "v_sad_u16", "v_add_u16_e32", "v_and_b32_e32", "v_lshrrev_b32_e32", "v_sub_u32_e32", "v_fmac_f32_e32", "v_pk_fma_f32 2-reg", "v_add3 distinct", "v_cvt_f32_ubyte0", "v_cvt_f32_ubyte3", "v_cvt_f32_i32", "v_rsq_f32 div:2", "v_mul_f32 mul:2", "v_sub_f32_e32", "v_fma_f32 neg", "cndmask_e64 s-pair", "cmp_e64 only", "v_add_u32_e64", "v_min_f32_e32", "v_max_u32_e32", "v_med3_f32", "v_mul_legacy_f32", "v_add_co_u32_e32", "v_or3_b32", "v_xor_b32_e32", "v_cvt_f32_u32", "v_lshlrev_b32_e32", "v_cndmask_e32 after cmp", "cmp_e64+cndmask+add (3)", "v_mov_b32_dpp wave_shl dep", "ds_write2st64_b32"};
+                               "v_add3 16KB body", "v_add_e32 8KB body", "v_pk_add_u16", "v_pk_mad_u16", "v_pk_mul_lo_u16", "v_dot2_u32_u16", "v_dot2_i32_i16", "v_dot4_u32_u8", "v_perm_b32", "v_bfe_u32", "v_lshl_add_u32", "v_cndmask_b32_e32", "v_cmp_gt_f32_e32", "v_max_f32_e32", "v_mul_f32_e32", "v_add_f32_e32", "v_mul_u32_u24_e32", "v_mad_u32_u24", "v_addc_co_u32_e32", "v_alignbyte_b32", "v_mov_b32_e32", "dpp quad_perm", "v_add_u32_dpp", "v_pk_add_f32", "v_sqrt_f32", "rsq+fma (2)", "v_sad_u16", "v_add_u16_e32", "v_and_b32_e32", "v_lshrrev_b32_e32", "v_sub_u32_e32", "v_fmac_f32_e32", "v_pk_fma_f32 2-reg", "v_add3 distinct", "v_cvt_f32_ubyte0", "v_cvt_f32_ubyte3", "v_cvt_f32_i32", "v_rsq_f32 div:2", "v_mul_f32 mul:2", "v_sub_f32_e32", "v_fma_f32 neg", "cndmask_e64 s-pair", "cmp_e64 only", "v_add_u32_e64", "v_min_f32_e32", "v_max_u32_e32", "v_med3_f32", "v_mul_legacy_f32", "v_add_co_u32_e32", "v_or3_b32", "v_xor_b32_e32", "v_cvt_f32_u32", "v_lshlrev_b32_e32", "v_cndmask_e32 after cmp", "cmp_e64+cndmask+add (3)", "v_mov_b32_dpp wave_shl dep", "ds_write2st64_b32", "pk_fma+add_f32 (2)", "pk_fma+mul+add_f32 (3)", "max3+add_f32 (2)", "mul_f32+add_f32 (2)", "pk_add+add+sub_f32 (3)", "pk_fma+and_b32 (2)"};
 
 template <int C>
 static int run(int cus, uint64_t *dcyc, uint32_t *dsink) {
@@ -200,7 +213,7 @@ static int run(int cus, uint64_t *dcyc, uint32_t *dsink) {
         std::vector<uint64_t> c(blocks * 4);
         CHECK(hipMemcpy(c.data(), dcyc, c.size() * 8, hipMemcpyDeviceToHost));
         std::sort(c.begin(), c.end());
-        const int per_iter = (C == 67) ? 96 : (((C >= 10 && C <= 12) || C == 38 || C == 68) ? 64 : 32);  // wave-instructions per loop iteration (average)
+        const int per_iter = (C == 67 || C == 71 || C == 74) ? 96 : (((C >= 10 && C <= 12) || C == 38 || C == 68 || C == 70 || C == 72 || C == 73 || C == 75) ? 64 : 32);  // wave-instructions per loop iteration (average)
         const double instr = double(kIters) * per_iter;
         // waves per SIMD = w (a 256-thread block puts one wave on each SIMD of its CU)
         printf("%-22s waves/SIMD %d  cycles/instr/SIMD (median wave) %.2f  (max wave) %.2f  wall %.3f ms -> %.2f GHz-equiv\n",
@@ -229,7 +242,7 @@ int main(int argc, char **argv) {
     CHECK(hipMalloc(&dsink, sizeof(uint32_t) * cus * 8 * 256));
     printf("CUs %d, clock %d kHz\n", cus, p.clockRate);
     const int only = argc > 1 ? atoi(argv[1]) : -1;
-    if (run_all(cus, dcyc, dsink, only, std::make_integer_sequence<int, 70>())) return 1;
+    if (run_all(cus, dcyc, dsink, only, std::make_integer_sequence<int, 76>())) return 1;
     printf("valu_probe done\n");
     return 0;
 }
