@@ -46,6 +46,14 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
     return r;
 }
 
+// a + (lane i+1's b; 0 for lane 63) as one v_add_f32_dpp (the compiler leaves a v_mov_b32_dpp when
+// the halo's source register is reused before the add)
+__device__ __forceinline__ float add_from_right_f(float a, float b) {
+    float r;
+    asm("v_add_f32_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(r) : "v"(b), "v"(a));
+    return r;
+}
+
 // The same responses from float tensor sums (exact integers < 2^24 held as floats, FD_LP_FP), G1 form,
 // gate test as a sign mask (thr - gate < 0 <=> gate > thr): full-rate float ops only.
 // Shi-Tomasi: sqrt_rn_rsq2 (fd_device.h), verified exhaustively. (Folding its halving into rsq's output
@@ -209,11 +217,7 @@ __device__ __forceinline__ void lp_seg_flush(uint32_t &n, const uint32_t *sl, co
     uint32_t v[kPer], sum = 0;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) sum += (v[k] = L.hist[kHistBins - 1 - (tid * kPer + k)]);
-    uint32_t incl = sum;
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
+    const uint32_t incl = wave_incl_add(sum);
     if (lane == kWave - 1) wtot[wv] = incl;
     __syncthreads();
     uint32_t run = incl - sum, total = 0;
@@ -384,9 +388,6 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
                 qxx[0] = from_left_f(qxx[PX]);
                 qyy[0] = from_left_f(qyy[PX]);
                 qxy[0] = from_left_f(qxy[PX]);
-                qxx[PX + 1] = from_right_f(qxx[1]);
-                qyy[PX + 1] = from_right_f(qyy[1]);
-                qxy[PX + 1] = from_right_f(qxy[1]);
                 // 3-tap row sums, two columns at a time sharing the middle pair (exact: integers < 2^24)
 #pragma unroll
                 for (int m = 0; m < PX; m += 2) {
@@ -394,9 +395,15 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
                     hxx[sc][m / 2].x = qxx[m] + txx;
                     hyy[sc][m / 2].x = qyy[m] + tyy;
                     hxy[sc][m / 2].x = qxy[m] + txy;
-                    hxx[sc][m / 2].y = txx + qxx[m + 3];
-                    hyy[sc][m / 2].y = tyy + qyy[m + 3];
-                    hxy[sc][m / 2].y = txy + qxy[m + 3];
+                    if (m + 3 <= PX) {
+                        hxx[sc][m / 2].y = txx + qxx[m + 3];
+                        hyy[sc][m / 2].y = tyy + qyy[m + 3];
+                        hxy[sc][m / 2].y = txy + qxy[m + 3];
+                    } else {  // the right halo column's products
+                        hxx[sc][m / 2].y = add_from_right_f(txx, qxx[1]);
+                        hyy[sc][m / 2].y = add_from_right_f(tyy, qyy[1]);
+                        hxy[sc][m / 2].y = add_from_right_f(txy, qxy[1]);
+                    }
                 }
 #else
                 // gradients of row ri-1 (feature_point_harris_detector.cpp:35-62) and biased products at

@@ -57,6 +57,25 @@ __device__ __forceinline__ uint32_t add3u(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
+// Inclusive prefix sum over the wave (lane i: lanes 0..i) by DPP: row_shr 1/2/4/8 within each row of
+// 16 lanes, then row_bcast:15 / row_bcast:31 carry the row totals up (GFX9 DPP). Six dependent VALU
+// ops instead of six ds_bpermute round trips (__shfl_up), which chain LDS latency.
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xF, 0xF, false));  // row_shr:1
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xF, 0xF, false));  // row_shr:2
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xF, 0xF, false));  // row_shr:4
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xF, 0xF, false));  // row_shr:8
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xA, 0xF, false));  // row_bcast:15
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return x;
+}
+// Inclusive suffix sum over the wave (lane i: lanes i..63) = wave total - exclusive prefix.
+__device__ __forceinline__ uint32_t wave_suffix_add(uint32_t x) {
+    const uint32_t p = wave_incl_add(x);
+    const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(p), 63));
+    return tot - p + x;
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 __device__ __forceinline__ uint64_t lanes_below() {

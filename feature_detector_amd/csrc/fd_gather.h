@@ -60,11 +60,7 @@ __device__ __forceinline__ void gather_first_chunk(const GatherView &v, int g, i
         uint32_t val[kBpt], sacc = 0;
 #pragma unroll
         for (int q = 0; q < kBpt; ++q) sacc += (val[q] = L.S[b0 + q]);
-        uint32_t incl = sacc;
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint32_t t = __shfl_down(incl, o);
-            if (lane + o < kWave) incl += t;
-        }
+        const uint32_t incl = wave_suffix_add(sacc);
         if (lane == 0) L.wtot[wave] = incl;
         __syncthreads();
         uint32_t after = 0;
@@ -96,11 +92,7 @@ __device__ __forceinline__ void gather_first_chunk(const GatherView &v, int g, i
             hm |= static_cast<uint32_t>(i < s1 && sel_key32(r[k], v.key_base, v.key_lz) >= k32lo) << k;
         }
         const uint32_t cntt = __popc(hm);
-        uint32_t incl = cntt;
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
-        }
+        const uint32_t incl = wave_incl_add(cntt);
         if (lane == kWave - 1) L.wtot[wave] = incl;
         __syncthreads();
         uint32_t before = 0, total = 0;

@@ -147,11 +147,7 @@ __device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, 
     uint32_t v[kPer], sum = 0;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) sum += (v[k] = L.hist[kHistBins - 1 - (tid * kPer + k)]);
-    uint32_t incl = sum;
-    for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (lane >= o) incl += t;
-    }
+    const uint32_t incl = wave_incl_add(sum);
     if (lane == kWave - 1) wtot[wv] = incl;
     __syncthreads();
     uint32_t run = incl - sum, total = 0;

@@ -443,11 +443,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         uint32_t sacc = 0;
         for (int b = b0; b < b1; ++b) sacc += S[b];
         // suffix over threads: wave-level, then across the waves
-        uint32_t incl = sacc;
-        for (int o = 1; o < kWave; o <<= 1) {
-            const uint32_t t = __shfl_down(incl, o);
-            if (lane + o < kWave) incl += t;
-        }
+        const uint32_t incl = wave_suffix_add(sacc);
         if (lane == 0) wtot[wave] = incl;
         __syncthreads();
         uint32_t after = 0;
