@@ -46,7 +46,10 @@ def north_star_issue():
             q = json.load(fh)["ns_sq"]
     except (OSError, KeyError, ValueError):
         return None
+    c = q.get("counters", {})
+    slots = c.get("SQ_INSTS_VALU", 0.0) - c.get("SQ_ACTIVE_INST_VALU2", 0.0)  # dual-issued pairs share a slot
     return {"source": os.path.relpath(SQ_FILE, ROOT),
+            "valu_issue_slots_per_launch": slots or None,
             "valu_issue_slot_busy": q.get("valu_issue_slot_busy"),
             "simd_valu_utilisation": q["simd_valu_utilisation"],
             "waves_resident_per_simd": q["waves_resident_per_simd"],
@@ -55,6 +58,25 @@ def north_star_issue():
                      "pairs share one; measured per opcode class in profiles/r03_valu_probe.txt), busy = "
                      "(SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) x 4 / (1024 SIMDs x kernel cycles); HBM is ~10 % "
                      "-- DESIGN.md section 5")}
+
+
+SIMDS, CLOCK_GHZ = 1024, 2.4  # 256 CUs x 4 SIMDs; peak engine clock (MI355X_MICROARCH.md)
+
+
+def valu_floor(issue, pixels, kernel_ms):
+    """The north-star kernel against its VALU issue-slot floor: one quad-cycle slot per wave64 VALU
+    instruction (dual-issued pairs one), all SIMDs at the peak clock; and the slot budget per pixel that
+    70 % of the HBM read roofline (1 B/px) would leave."""
+    if not issue or not issue.get("valu_issue_slots_per_launch"):
+        return None
+    slots = issue["valu_issue_slots_per_launch"]
+    floor_ms = slots * 4 / SIMDS / (CLOCK_GHZ * 1e9) * 1e3
+    slot_rate = SIMDS * CLOCK_GHZ * 1e9 / 4
+    return {"issue_slots_per_px": round(slots / pixels, 4), "lane_slots_per_px": round(64 * slots / pixels, 1),
+            "floor_ms": round(floor_ms, 4), "frac": round(floor_ms / kernel_ms, 4),
+            "hbm70_slots_per_px": round(slot_rate / (0.7 * HBM_PEAK_GBS * 1e9), 4),
+            "note": "VALU issue-slot floor at the peak clock vs the measured kernel time; 70 % of the HBM read "
+                    "roofline would need <= hbm70_slots_per_px wave issue slots per pixel (DESIGN.md section 5)"}
 
 
 def measured_traffic(key):
@@ -768,7 +790,8 @@ def main():
                          "frac": round(ach / HBM_PEAK_GBS, 4), "bytes_per_launch": kb,
                          "traffic": measured_traffic("northstar_k_corner")[0],
                          # the bound that binds: VALU issue slots (SQ pass of the same kernel, profiles/)
-                         "valu_frac": ns_issue["valu_issue_slot_busy"] if ns_issue else None},
+                         "valu_frac": ns_issue["valu_issue_slot_busy"] if ns_issue else None,
+                         "valu": valu_floor(ns_issue, kb, kms)},
             "issue": ns_issue,
             "ties": ties_ns,
         }

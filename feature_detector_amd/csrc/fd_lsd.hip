@@ -381,8 +381,9 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
 
 // Pass 2: per-frame exclusive scan of the counts in column-major order (col outer, chunk inner).
 __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
-    __shared__ int64_t wsum[16];
-    __shared__ int64_t carry;
+    constexpr int kPer = 4;  // consecutive scan entries per thread and round
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t carry;
     const int f = blockIdx.x;
     const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
     const int mc = a.cols - 1;
@@ -391,25 +392,31 @@ __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
     int32_t *base = a.col_base + static_cast<int64_t>(f) * n;
     if (tid == 0) carry = 0;
     __syncthreads();
-    for (int64_t s0 = 0; s0 < n; s0 += 1024) {
-        const int64_t s = s0 + tid;
-        // entries of columns outside [1, cols-3] were never written: treat them as 0
-        const int col = static_cast<int>(s / a.chunks), chunk = static_cast<int>(s - static_cast<int64_t>(col) * a.chunks);
-        const int64_t at = static_cast<int64_t>(chunk) * mc + col;  // (chunk, column) layout
-        const int c = (s < n && col >= 1 && col <= a.cols - 3) ? cnt[at] : 0;
-        int64_t incl = c;
-        for (int o = 1; o < kWave; o <<= 1) {
-            const int64_t t = __shfl_up(incl, o);
-            if (lane >= o) incl += t;
+    // (a frame's count < 2^29: 32-bit sums)
+    for (int64_t s0 = 0; s0 < n; s0 += kPer * 1024) {
+        uint32_t c[kPer], sum = 0;
+        int64_t at[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int64_t s = s0 + kPer * tid + k;
+            // entries of columns outside [1, cols-3] were never written: treat them as 0
+            const int col = static_cast<int>(s / a.chunks), chunk = static_cast<int>(s - static_cast<int64_t>(col) * a.chunks);
+            at[k] = s < n ? static_cast<int64_t>(chunk) * mc + col : -1;  // (chunk, column) layout
+            c[k] = (s < n && col >= 1 && col <= a.cols - 3) ? static_cast<uint32_t>(cnt[at[k]]) : 0u;
+            sum += c[k];
         }
-        if (lane == 63) wsum[wv] = incl;
+        const uint32_t incl = wave_incl_add(sum);
+        if (lane == kWave - 1) wsum[wv] = incl;
         __syncthreads();
-        int64_t wpre = 0;
-        for (int q = 0; q < wv; ++q) wpre += wsum[q];
-        const int64_t start = carry + wpre + incl - c;
-        __syncthreads();
-        if (s < n) base[at] = static_cast<int32_t>(start);
-        if (tid == 1023) carry = start + c;
+        uint32_t run = carry + incl - sum;
+        for (int q = 0; q < wv; ++q) run += wsum[q];
+        __syncthreads();  // everyone has read carry and wsum
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            if (at[k] >= 0) base[at[k]] = static_cast<int32_t>(run);
+            run += c[k];
+        }
+        if (tid == 1023) carry = run;
         __syncthreads();
     }
     if (tid == 0) a.counts[f] = carry;

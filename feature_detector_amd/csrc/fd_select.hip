@@ -111,8 +111,16 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                                              const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
                                              uint32_t prior, int &s_acc, int &s_done, bool ties, const uint64_t *tmask,
                                              uint32_t key0, uint32_t keylast,
-                                             uint32_t &tie_prev, int &tie_has_prev) {
+                                             uint32_t &tie_prev, int &tie_has_prev, uint64_t *st = nullptr) {
     const int lane = lane_id();
+    // diagnostic clocks (a.stamps): per-batch phases into slots 26-28 (st[15]: the running clock)
+    auto gst = [&](int slot) {
+        if (st && lane == 0) {
+            const uint64_t now = __builtin_readcyclecounter();
+            st[slot] += now - st[15];
+            st[15] = now;
+        }
+    };
     const int d = a.dist;
     const bool pk16 = a.rows + 3 * d < 65536 && a.cols + 3 * d < 65536;  // no wrap-around in 16-bit halves
     const uint32_t w2 = 2u * static_cast<uint32_t>(d);
@@ -171,6 +179,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         }
         if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n);
         const uint64_t m = ballot(ok);
+        gst(26);  // grid test
         C &= m;
         // Resolution in scan order: a lane with no earlier ok neighbour in the batch is accepted; the
         // others (few: distance-d pairs inside 64 consecutive candidates) are decided one by one in
@@ -200,6 +209,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                 mine = mine || can;
             }
         }
+        gst(27);  // resolution
         // need cutoff (:67-69): features.size() >= need is checked after every append
         const uint32_t have = prior + static_cast<uint32_t>(acc);
         const int allow = have < a.need ? static_cast<int>(a.need - have) : 1;
@@ -227,6 +237,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         }
         acc += popc64(acc_m);
         if constexpr (GRID == 2) __builtin_amdgcn_s_waitcnt(0);
+        gst(28);  // output + grid update
     }
     if (ties && cnt > 0) {
         // The reference's visiting order of this sub-chunk ends at the stop (or runs through it). Its
@@ -1250,13 +1261,16 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     const uint64_t *tm = L.tmask;
                     if (!use_grid)
                         greedy_chunk<0>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
-                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
+                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev,
+                                        a.stamps ? L.st : nullptr);
                     else if (grid_in_lds)
                         greedy_chunk<1>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
-                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
+                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev,
+                                        a.stamps ? L.st : nullptr);
                     else
                         greedy_chunk<2>(a, f, c_sort, pxy, pcell, buf, grid_g, gw2, prior, s_acc, s_done, ties, tm,
-                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
+                                        L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev,
+                                        a.stamps ? L.st : nullptr);
                 }
                 if (tid == 0 && (filtered || c_sort > 0)) {  // the sub-chunk's smallest 32-bit key
                     L.prev_min = filtered ? L.seg_more[1] : L.pk32[c_sort - 1];
