@@ -37,15 +37,42 @@ constexpr float kZeroFloat = 1e-6f;        // Slam_Utility kZeroFloat (un-vendor
                                            // integer keypoints, so any value in (0, 1) gives the same bits)
 constexpr float kPatternMaxBound = 19.0f;  // descriptor_brief.cpp:13
 
+// Pixel source. Global: one byte load per sample from the frame (a sample pattern spreads a wave's 64
+// loads over ~30 rows: ~one cache line per lane, the TA's limit). Staged (STAGED = true, the usual
+// case): the keypoint's patch -- every pixel a sample of this keypoint can touch -- was copied once into
+// the wave's LDS with coalesced row loads, and samples read it there.
+constexpr int kStageSide = 64;  // largest staged patch side (one lane per column)
+constexpr int kPatchR = 20;     // sample reach: |rot(p)| <= sqrt(13^2 + 13^2) < 18.4 (pattern coordinates
+                                // in [-13, 12]) plus the bilinear neighbour, around floor(u), floor(v)
+
 struct Frame {
     __amdgpu_buffer_rsrc_t rsrc;
     int cols;
+    const uint8_t *lds;  // staged patch [side][side] (null: global loads)
+    int r0, c0, side;    // frame coordinates of lds[0]
 };
 
 __device__ __forceinline__ float pixel(const Frame &fr, int32_t r, int32_t c) {
+    if (fr.lds) return static_cast<float>(fr.lds[(r - fr.r0) * fr.side + (c - fr.c0)]);
     // Linear index as the row-major NoCheck accessor; out of the frame -> 0 (buffer range check).
     const int32_t idx = r * fr.cols + c;
     return static_cast<float>(buf_load_u8(fr.rsrc, idx));
+}
+
+// Copy rows [r0, r0 + side) x columns [c0, c0 + side) -- as linear indices r * cols + c, exactly the bytes
+// the global path would read (0 outside the frame's byte range) -- into the wave's LDS, one row per
+// load instruction (lane = column).
+__device__ __forceinline__ void stage_patch(Frame &fr, uint8_t *lds, int r0, int c0, int side) {
+    const int lane = lane_id();
+    for (int pr = 0; pr < side; ++pr)
+        if (lane < side) lds[pr * side + lane] = static_cast<uint8_t>(buf_load_u8(fr.rsrc, (r0 + pr) * fr.cols + c0 + lane));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    fr.lds = lds;
+    fr.r0 = r0;
+    fr.c0 = c0;
+    fr.side = side;
 }
 
 template <int SAMPLER>
@@ -65,15 +92,16 @@ __device__ __forceinline__ float sample(const Frame &fr, float row, float col) {
     }
 }
 
+// Sum over the wave (every lane gets it): DPP prefix sum + lane 63 (six dependent VALU ops instead of
+// six ds_bpermute round trips).
 __device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    const uint32_t p = wave_incl_add(static_cast<uint32_t>(v));
+    return __builtin_amdgcn_readlane(static_cast<int>(p), 63);
 }
 
 template <int SAMPLER>
-__device__ void brief_one(const BriefArgs &a, const Frame &fr, float u, float v, uint32_t *out, uint8_t *valid,
-                          float *stage) {
+__device__ void brief_one(const BriefArgs &a, Frame &fr, float u, float v, uint32_t *out, uint8_t *valid,
+                          float *stage, uint8_t *patch) {
     const int lane = lane_id();
     const int nw = (a.length + 31) >> 5;
     const int h = a.half;
@@ -87,6 +115,13 @@ __device__ void brief_one(const BriefArgs &a, const Frame &fr, float u, float v,
         if (lane < nw) out[lane] = 0u;
         if (valid && lane == 0) *valid = 0;
         return;
+    }
+    {  // stage the patch: moments reach h (+1 bilinear), the pattern kPatchR, around floor(u), floor(v)
+        const int reach = max(kPatchR, h + 1);
+        if (2 * reach + 1 <= kStageSide) {
+            const int u0 = static_cast<int>(floorf(u)), v0 = static_cast<int>(floorf(v));
+            stage_patch(fr, patch, v0 - reach, u0 - reach, 2 * reach + 1);
+        }
     }
     const int side = 2 * h + 1;
     const int npatch = side * side;
@@ -173,6 +208,7 @@ __device__ void brief_one(const BriefArgs &a, const Frame &fr, float u, float v,
 template <int SAMPLER>
 __global__ __launch_bounds__(256) void k_brief(BriefArgs a) {
     __shared__ float stage[4][kWave];
+    __shared__ uint8_t patch[4][kStageSide * kStageSide];
     const int wave = static_cast<int>(threadIdx.x >> 6);
     const int64_t slot = static_cast<int64_t>(blockIdx.x) * 4 + wave;
     if (slot >= static_cast<int64_t>(a.batch) * a.stride) return;
@@ -189,7 +225,10 @@ __global__ __launch_bounds__(256) void k_brief(BriefArgs a) {
     fr.rsrc = make_rsrc(a.frames + static_cast<int64_t>(f) * a.rows * a.cols,
                         static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols));
     fr.cols = a.cols;
-    brief_one<SAMPLER>(a, fr, u, v, a.out_bits + slot * nw, a.out_valid ? a.out_valid + slot : nullptr, stage[wave]);
+    fr.lds = nullptr;
+    fr.r0 = fr.c0 = fr.side = 0;
+    brief_one<SAMPLER>(a, fr, u, v, a.out_bits + slot * nw, a.out_valid ? a.out_valid + slot : nullptr, stage[wave],
+                       patch[wave]);
 }
 
 }  // namespace

@@ -69,6 +69,10 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
     x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xC, 0xF, false));  // row_bcast:31
     return x;
 }
+// Sum over the wave, in every lane.
+__device__ __forceinline__ uint32_t wave_total_add(uint32_t x) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wave_incl_add(x)), 63));
+}
 // Inclusive suffix sum over the wave (lane i: lanes i..63) = wave total - exclusive prefix.
 __device__ __forceinline__ uint32_t wave_suffix_add(uint32_t x) {
     const uint32_t p = wave_incl_add(x);

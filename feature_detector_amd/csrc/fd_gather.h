@@ -64,7 +64,7 @@ __device__ __forceinline__ void gather_first_chunk(const GatherView &v, int g, i
         if (lane == 0) L.wtot[wave] = incl;
         __syncthreads();
         uint32_t after = 0;
-        for (int q = wave + 1; q < NT / kWave; ++q) after += L.wtot[q];
+        after = wave_total_add((lane > wave && lane < NT / kWave) ? L.wtot[lane] : 0u);
         uint32_t run = incl - sacc + after;
 #pragma unroll
         for (int q = kBpt - 1; q >= 0; --q) {

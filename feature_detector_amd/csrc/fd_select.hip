@@ -458,7 +458,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         if (lane == 0) wtot[wave] = incl;
         __syncthreads();
         uint32_t after = 0;
-        for (int q = wave + 1; q < nthr / kWave; ++q) after += wtot[q];
+        // the later waves' totals: one LDS read per lane and a wave sum (not a chain of up to 15 reads)
+        after = wave_total_add((lane > wave && lane < nthr / kWave) ? wtot[lane] : 0u);
         uint32_t run = incl - sacc + after;
         for (int b = b1 - 1; b >= b0; --b) {  // (a thread's own bins: read before written)
             run += S[b];

@@ -5,6 +5,7 @@ fixed number of times, on seeded uniform-noise frames generated on the GPU.
   --shape northstar  fd_points_response (per-pixel kernel alone), 1920x1080 batch 256, 10 calls
                      (--kind shi_tomasi by default: the north-star kernel)
   --shape fast720    fd_points_detect, FAST, 1280x720 batch 64 (BASELINE configs[2]), 10 calls
+  --shape fastbrief  the same + BRIEF-256 on the detected keypoints (fd_brief_compute), 10 calls
   --shape lsd        fd_lsd_map (dense) and fd_lsd_lines (compact map + host stage), 1920x1080 batch 256,
                      64-px checker + noise (BASELINE configs[3]), 3 calls each (--kind dense / compact: one)
 """
@@ -19,7 +20,7 @@ import feature_detector_amd as fd  # noqa: E402
 
 THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 p = argparse.ArgumentParser()
-p.add_argument("--shape", default="bench", choices=["bench", "northstar", "nsdetect", "fast720", "fast720r", "lsd"])
+p.add_argument("--shape", default="bench", choices=["bench", "northstar", "nsdetect", "fast720", "fast720r", "fastbrief", "lsd"])
 p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast", "dense", "compact"])
 p.add_argument("--calls", type=int, default=0)
 p.add_argument("--thr", type=float, default=None, help="response threshold override (e.g. 1e30: no candidates)")
@@ -73,6 +74,12 @@ elif a.shape == "fast720r":  # the FAST kernel alone (fd_points_response: no sel
            torch.empty((64, cap), dtype=torch.int32, device="cuda"), torch.empty((64,), dtype=torch.int32, device="cuda"))
     for _ in range(a.calls or 10):
         fd.point_response(kind, frames, THR[kind], out=out)
+elif a.shape == "fastbrief":  # BASELINE configs[2]: FAST detect + BRIEF-256 on the device output
+    kind = "fast"
+    frames = noise(64, 720, 1280)
+    for _ in range(a.calls or 10):
+        res = fd.detect_points(kind, frames, 200, 20, THR[kind])
+        fd.brief_compute(frames, res.xy, res.counts, length=256, half_patch_size=8)
 else:
     kind = a.kind or "fast"
     frames = noise(64, 720, 1280)
