@@ -265,6 +265,8 @@ hipError_t launch_brief(const BriefArgs &a, hipStream_t s);
 hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s);
 int heat_blocks_per_frame(int64_t npx);
 hipError_t launch_nn_desc(const NnDescArgs &a, hipStream_t s);
+hipError_t launch_bias_relu(const void *x, const void *bias, void *y, int n, int h, int w, int c, int pool,
+                            hipStream_t s);
 // Interleaved 8-bit samples (channels 1-4) of npx pixels -> gray frames (fd_gray.hip).
 hipError_t launch_rgb_gray(const uint8_t *src, int channels, uint8_t *dst, int64_t npx, hipStream_t s);
 

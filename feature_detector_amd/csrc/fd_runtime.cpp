@@ -1733,6 +1733,18 @@ int fd_nn_select_list(fd_ctx *c, const int64_t *keypoints, const float *scores, 
     return FD_OK;
 }
 
+int fd_nn_bias_relu(fd_ctx *c, const void *x, const void *bias, void *y, int n, int h, int w, int ch, int pool) {
+    if (!c) return FD_ERR_INVALID;
+    if (!x || !bias || !y) return fail(c, FD_ERR_INVALID, "bad arguments");
+    if (n < 0 || h < 0 || w < 0 || ch <= 0 || ch % 8) return fail(c, FD_ERR_INVALID, "need n, h, w >= 0, c a multiple of 8");
+    if (pool && ((h | w) & 1)) return fail(c, FD_ERR_INVALID, "pooling needs even h and w");
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(y)) & 15)
+        return fail(c, FD_ERR_INVALID, "pointers must be 16-byte aligned");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    FD_HIP_TRY(c, fdk::launch_bias_relu(x, bias, y, n, h, w, ch, pool, c->stream));
+    return FD_OK;
+}
+
 int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int map_layout, int batch, int channels,
                       int map_rows, int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
                       int io_on_device) {

@@ -174,6 +174,29 @@ def nn_select_list(keypoints, scores, rows: int, cols: int, counts=None, options
     return xy, cnt, dout
 
 
+def bias_relu(x, bias, pool: bool = False, out=None, ctx: Context | None = None):
+    """fd_nn_bias_relu: relu(x + bias) (and the 2x2 max pool when pool) of a channels-last fp16
+    activation [N, C, H, W] on the device, in one pass (torch's current stream). x is the output of a
+    bias-free convolution; the result equals PyTorch's conv-with-bias -> ReLU (-> MaxPool2d(2, 2)) in
+    half precision bit for bit. out: preallocated result (may be x itself when not pooling)."""
+    import torch
+
+    if not (_is_torch_device_tensor(x) and x.dtype == torch.float16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("bias_relu: x must be a channels-last float16 [N, C, H, W] device tensor")
+    n, c, h, w = x.shape
+    if out is None:
+        shape = (n, c, h // 2, w // 2) if pool else (n, c, h, w)
+        out = torch.empty(shape, dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
+    b = bias.detach().to(torch.float16).contiguous()
+    ctx = _resolve_ctx(ctx, x)
+    _bind_stream(ctx, True)
+    rc = _lib.load().fd_nn_bias_relu(ctx.ptr, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                                      ctypes.c_void_p(out.data_ptr()), int(n), int(h), int(w), int(c), 1 if pool else 0)
+    _lib.check(ctx.ptr, rc)
+    return out
+
+
 def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = None):
     """fd_nn_descriptors: desc_map [B, C, h, w] float32, xy [B, S, 2] -> descriptors [B, S, C].
 
@@ -277,21 +300,32 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             self.convDa = nn.Conv2d(c4, c5, 3, 1, 1)
             self.convDb = nn.Conv2d(c5, d1, 1, 1, 0)
 
+        def cbr(self, conv, x, pool=False):
+            """conv -> ReLU (-> MaxPool2d(2, 2)): fp16 channels-last activations run the convolution
+            without its bias and fd_nn_bias_relu for bias, ReLU and pooling in one pass (PyTorch would make
+            three or four elementwise passes over the activation); other inputs take the torch modules."""
+            if x.dtype == torch.float16 and x.is_cuda and x.is_contiguous(memory_format=torch.channels_last) \
+                    and conv.out_channels % 8 == 0 and not os.environ.get("FD_SP_UNFUSED"):  # (A/B switch)
+                y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding)
+                if y.is_contiguous(memory_format=torch.channels_last):
+                    return bias_relu(y, conv.bias, pool, out=None if pool else y)
+                x = y + conv.bias.view(1, -1, 1, 1)
+                x = self.relu(x)
+                return self.pool(x) if pool else x
+            x = self.relu(conv(x))
+            return self.pool(x) if pool else x
+
         def forward(self, x):
             """x: [B, 1, H, W] in [0, 1] -> (heatmap [B, H, W] f32, descriptors [B, 256, H/8, W/8] f32), or
             with nms (keypoints [B, K, 2] int64, scores [B, K] f32, descriptors [B, K, 256] f32)."""
-            r = self.relu
-            x = r(self.conv1b(r(self.conv1a(x))))
-            x = self.pool(x)
-            x = r(self.conv2b(r(self.conv2a(x))))
-            x = self.pool(x)
-            x = r(self.conv3b(r(self.conv3a(x))))
-            x = self.pool(x)
-            x = r(self.conv4b(r(self.conv4a(x))))
-            semi = self.convPb(r(self.convPa(x))).float()
+            x = self.cbr(self.conv1b, self.cbr(self.conv1a, x), pool=True)
+            x = self.cbr(self.conv2b, self.cbr(self.conv2a, x), pool=True)
+            x = self.cbr(self.conv3b, self.cbr(self.conv3a, x), pool=True)
+            x = self.cbr(self.conv4b, self.cbr(self.conv4a, x))
+            semi = self.convPb(self.cbr(self.convPa, x)).float()
             prob = torch.softmax(semi, dim=1)[:, :-1]
             heat = torch.nn.functional.pixel_shuffle(prob, 8)[:, 0]
-            desc = self.convDb(r(self.convDa(x))).float()
+            desc = self.convDb(self.cbr(self.convDa, x)).float()
             desc = desc / desc.norm(dim=1, keepdim=True).clamp_min(1e-12)
             if not nms:
                 return heat, desc

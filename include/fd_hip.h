@@ -335,6 +335,16 @@ int fd_nn_descriptors(fd_ctx *ctx, const float *map, int map_on_device, int map_
                       int map_rows, int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
                       int io_on_device);
 
+/*
+ * fd_nn_bias_relu -- the NN detectors' bias + ReLU after a bias-free convolution, and with pool = 1 the
+ * 2x2 / stride-2 max pool that follows (nn.MaxPool2d(2, 2)), in one pass over an NHWC (channels-last)
+ * fp16 activation x [n][h][w][c] on the device: y = relu(x + bias[c]) ([n][h][w][c]; may alias x), or
+ * its pooled [n][h/2][w/2][c]. Arithmetic as PyTorch's half ops (the add in float, rounded to half).
+ * bias: c fp16 values on the device; c a multiple of 8; pool needs even h and w; 16-byte aligned
+ * pointers. Runs on the context's stream.
+ */
+int fd_nn_bias_relu(fd_ctx *ctx, const void *x, const void *bias, void *y, int n, int h, int w, int c, int pool);
+
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);
 

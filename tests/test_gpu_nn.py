@@ -239,3 +239,54 @@ def test_model_types_end_to_end(sp, oracle, model):
         pxy = torch.from_numpy(np.stack([prior[0], np.zeros((2, 2), np.float32)])).cuda()
         got = sp.nn_descriptors(desc, pxy, torch.tensor([2, 0], dtype=torch.int32, device="cuda"))
         assert np.array_equal(got[0].cpu().numpy().view(np.uint32), exp.view(np.uint32))
+
+
+def _reference_forward(net, x):
+    """SuperPointNet.forward with PyTorch's own modules only (biased convolution, ReLU, MaxPool2d)."""
+    import torch
+
+    r, p = net.relu, net.pool
+    x = p(r(net.conv1b(r(net.conv1a(x)))))
+    x = p(r(net.conv2b(r(net.conv2a(x)))))
+    x = p(r(net.conv3b(r(net.conv3a(x)))))
+    x = r(net.conv4b(r(net.conv4a(x))))
+    semi = net.convPb(r(net.convPa(x))).float()
+    heat = torch.nn.functional.pixel_shuffle(torch.softmax(semi, dim=1)[:, :-1], 8)[:, 0]
+    desc = net.convDb(r(net.convDa(x))).float()
+    return heat, desc / desc.norm(dim=1, keepdim=True).clamp_min(1e-12)
+
+
+@pytest.mark.gpu
+def test_bias_relu_matches_torch(sp):
+    """fd_nn_bias_relu (bias + ReLU, and + 2x2 max pool, on channels-last fp16) equals PyTorch's separate
+    half-precision ops bit for bit. The fused SuperPoint forward runs the convolutions without their bias,
+    which is not bit-identical to PyTorch's biased convolution (MIOpen may apply the bias before the
+    fp16 rounding of the convolution's output), so the network is compared within fp16 tolerance
+    (the network has seeded random weights: no reference output exists for it)."""
+    import torch
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    for c in (8, 64, 256):
+        x = (torch.randn(3, c, 34, 50, generator=g, device="cuda") * 8).half().contiguous(memory_format=torch.channels_last)
+        b = (torch.randn(c, generator=g, device="cuda") * 4).half()
+        ref = torch.relu(x + b.view(1, -1, 1, 1))
+        got = sp.bias_relu(x, b)
+        assert torch.equal(got, ref), c
+        refp = torch.nn.functional.max_pool2d(ref, 2, 2)
+        assert torch.equal(sp.bias_relu(x, b, pool=True), refp), c
+        inplace = x.clone(memory_format=torch.channels_last)
+        sp.bias_relu(inplace, b, out=inplace)
+        assert torch.equal(inplace, ref), c
+    with pytest.raises(ValueError):
+        sp.bias_relu(torch.zeros(1, 8, 4, 4, device="cuda"), torch.zeros(8, device="cuda"))  # fp32, not fp16
+    net = sp.build_net(0).cuda().eval().half().to(memory_format=torch.channels_last)
+    frames = torch.randint(0, 256, (2, 1, 96, 128), generator=g, device="cuda", dtype=torch.int32)
+    x = (frames.half() / 255.0).contiguous(memory_format=torch.channels_last)
+    with torch.inference_mode():
+        heat, desc = net(x)
+        rheat, rdesc = _reference_forward(net, x)
+    dh = (heat - rheat).abs().max().item()
+    dd = (desc - rdesc).abs().max().item()
+    print(f"fused vs module forward: max |d heat| {dh:.3g} (max heat {rheat.max().item():.3g}), max |d desc| {dd:.3g}")
+    assert torch.allclose(heat, rheat, rtol=2e-2, atol=2e-3) and torch.allclose(desc, rdesc, rtol=2e-2, atol=2e-3)

@@ -1,0 +1,40 @@
+"""A/B of the SuperPoint forward (BASELINE configs[4] shape: 64 x 640x480 fp16, channels last): the fused
+bias + ReLU (+ pool) kernel (fd_nn_bias_relu) against PyTorch's separate elementwise passes
+(FD_SP_UNFUSED=1), interleaved in one process; prints ms per 64-frame forward."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+import feature_detector_amd as fd  # noqa: E402
+from feature_detector_amd import superpoint as sp  # noqa: E402
+
+fd.load()
+det = sp.NNFeaturePointDetector(sp.Options(kMaxImageRows=480, kMaxImageCols=640))
+det.Initialize()
+g = torch.Generator(device="cuda")
+g.manual_seed(1)
+frames = torch.randint(0, 256, (64, 480, 640), generator=g, device="cuda", dtype=torch.int32).to(torch.uint8)
+
+
+def timed(reps=10):
+    det.InferenceSession(frames)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        det.InferenceSession(frames)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+for rnd in range(2):
+    for mode in ("fused", "unfused"):
+        if mode == "unfused":
+            os.environ["FD_SP_UNFUSED"] = "1"
+        else:
+            os.environ.pop("FD_SP_UNFUSED", None)
+        print(f"round {rnd} {mode}: {timed():.3f} ms per 64-frame forward", flush=True)
