@@ -267,6 +267,12 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
             const int ri = y0 - 3 + i0 + t;                            // row consumed this step
             ring[(t + 3) % 6] = load_px4<ALIGNED>(rs, (ri + 3) * cols + c0);
             const uint32_t P_s = ring[t], P_su = ring[(t + 4) % 6], P_sc = ring[(t + 5) % 6];
+            // Pipeline fill: step i0+t computes the gradients of row y0-4+(i0+t) (needed from row y0-2:
+            // steps >= 2) and the responses of row y0-5+(i0+t) (needed from row y0-1: steps >= 4). The
+            // first steps only load (wave-uniform; compile-time true for i0 > 0 or the later t).
+            // Short tiles (batch 1: 3 output rows in 9 steps) drop 2 of 9 gradient and 4 of 9 response
+            // evaluations. Skipped slots keep their zero initialisation and are never read.
+            if (!(t >= 2 || i0 > 0)) continue;
 
             // Gradients of centre row ri-1 at the lane's 4 columns (feature_point_harris_detector.cpp:
             // 35-62); the two halo bytes of row ri-1 come from the neighbour lanes. Products carry the
@@ -298,6 +304,7 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
                 hxy[sc][m] = add3u(qxy[m], qxy[m + 1], qxy[m + 2]);
             }
 
+            if (!(t >= 4 || i0 > 0)) continue;
             // Response of row rr = ri-2: vertical 3-row sums are exact integers (< 2^23).
             const int rr = ri - 2;
             const bool rowv = rr >= 2 && rr <= rows - 3;
