@@ -37,6 +37,12 @@ constexpr int kLevels = 8;
 __device__ __forceinline__ int lvl_width(int l) { return l == 0 ? 12 : (l == 7 ? 4 : 8); }
 __device__ __forceinline__ int lvl_top(int l) { return l == 7 ? 64 : 12 + 8 * l; }  // bits consumed through l
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+// Empty occupancy-grid cell. Frames with rows, cols + 3d < 2^15 use 0x7FFF7FFF: in the packed-halves
+// distance test (dt = g - (e - d) per 16-bit half, conflict iff both halves <= 2d) it lies more than d
+// from every pixel without wrapping (0x7FFF - x + d is in (2d, 2^16) for x < cols), so the greedy's grid
+// test needs no empty check; larger frames use 0xFFFFFFFF (coordinates stay below 65535) and check.
+__device__ __forceinline__ bool grid_pk15(int rows, int cols, int d) { return rows + 3 * d < 32768 && cols + 3 * d < 32768; }
+__device__ __forceinline__ uint32_t grid_empty(int rows, int cols, int d) { return grid_pk15(rows, cols, d) ? 0x7FFF7FFFu : kEmpty; }
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));  // packed (x, y) of a (y << 16) | x position
 
 // Diagnostic phase clocks (only when a.stamps is set), accumulated by thread 0 in LDS (L.st) and
@@ -123,6 +129,8 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     };
     const int d = a.dist;
     const bool pk16 = a.rows + 3 * d < 65536 && a.cols + 3 * d < 65536;  // no wrap-around in 16-bit halves
+    const bool pk15 = grid_pk15(a.rows, a.cols, d);
+    const uint32_t gempty = grid_empty(a.rows, a.cols, d);
     const uint32_t w2 = 2u * static_cast<uint32_t>(d);
     int acc = s_acc;
     bool done = false;
@@ -132,14 +140,22 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     // Software pipeline: a batch's position, cell and conflict mask are loaded during the previous
     // batch's resolution (they are read-only here; only the grid is written).
     auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C) {
+        // unconditional LDS reads at a clamped index (in the array: cnt <= kSelectChunk), masked after:
+        // no exec-masked branch per array
         const int i = b + lane;
         const bool in = i < cnt;
-        e = in ? pxy[i] : kEmpty;
+        const int ic = min(i, kSelectChunk - 1);
+        e = pxy[ic];
         cell = gw2 + 1;
         C = 0;
         if constexpr (GRID != 0) {
-            cell = in ? static_cast<int>(pcell[i]) : gw2 + 1;
-            C = in ? cmask[i] : 0ull;
+            cell = static_cast<int>(pcell[ic]);
+            C = cmask[ic];
+        }
+        if (!in) {
+            e = kEmpty;
+            cell = gw2 + 1;
+            C = 0;
         }
     };
     uint32_t e_n;
@@ -161,19 +177,28 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                 if constexpr (GRID == 1) g[q] = grid[o];
                 else g[q] = __hip_atomic_load(&grid[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (pk16) {  // packed halves, as in the conflict masks (select_frame)
+            if (pk15) {  // packed halves; the empty cell tests far (grid_empty): min over the 9 cells
+                const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+                uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
+                    mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
+                }
+                ok = ok && mn > w2;
+            } else if (pk16) {  // packed halves, as in the conflict masks (select_frame)
                 const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
                     const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
                     const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
-                    if (g[q] != kEmpty && m <= w2) ok = false;
+                    if (g[q] != gempty && m <= w2) ok = false;
                 }
             } else {
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
                     const int gx = static_cast<int>(g[q] & 0xFFFFu), gy = static_cast<int>(g[q] >> 16);
-                    if (g[q] != kEmpty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
+                    if (g[q] != gempty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
                 }
             }
         }
@@ -429,7 +454,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     }
 
     if (use_grid && !grid_in_lds)
-        for (int i = tid; i < cells; i += nthr) grid_g[i] = kEmpty;
+        for (int i = tid; i < cells; i += nthr) grid_g[i] = grid_empty(rows, cols, d);
     if (tid == 0) {
         s_done = 0;
         s_acc = 0;
@@ -814,7 +839,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         // also hold for this thread's outstanding global stores and atomics, a memory round trip)
         if (!a.pre_keys && !seg_mode) __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
-        for (int i = tid; i < cells; i += nthr) grid_lds[i] = kEmpty;
+        for (int i = tid; i < cells; i += nthr) grid_lds[i] = grid_empty(rows, cols, d);
         __syncthreads();
     }
     FD_STAMP(3);
@@ -1026,7 +1051,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                                         const uint32_t g = grid_in_lds ? grid_lds[o]
                                                                        : __hip_atomic_load(&grid_g[o], __ATOMIC_RELAXED,
                                                                                            __HIP_MEMORY_SCOPE_AGENT);
-                                        if (g == kEmpty) continue;
+                                        if (g == grid_empty(rows, cols, d)) continue;
                                         if (pk16) {
                                             const u16x2 dt = __builtin_bit_cast(u16x2, g) - base;
                                             if ((dt.x > dt.y ? dt.x : dt.y) <= w2) keep = false;
@@ -1364,7 +1389,7 @@ __global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs
     const uint32_t npx = static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols);
     const uint32_t s1 = static_cast<uint32_t>(d + 1);
     if (use_grid)
-        for (int i = tid; i < cells; i += NT) grid[i] = kEmpty;
+        for (int i = tid; i < cells; i += NT) grid[i] = grid_empty(rows, cols, d);
     if (tid == 0) {
         L.s_done = 0;
         L.s_acc = 0;
