@@ -48,13 +48,16 @@ __device__ __forceinline__ uint32_t load_px4(__amdgpu_buffer_rsrc_t r, int32_t o
            (buf_load_u8(r, off + 3) << 24);
 }
 
+// (the per-pixel kernels run 256-thread workgroups: a constant stride, no blockDim load -- whose wait
+// would also hold for every vector-memory operation in flight, e.g. seg_flush's returning atomic)
+constexpr int kPixWg = 256;
 __device__ __forceinline__ void hist_clear(uint32_t *h) {
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) h[b] = 0;
+    for (int b = threadIdx.x; b < kHistBins; b += kPixWg) h[b] = 0;
     __syncthreads();
 }
 __device__ __forceinline__ void hist_flush(const uint32_t *h, uint32_t *g) {
     __syncthreads();
-    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) {
+    for (int b = threadIdx.x; b < kHistBins; b += kPixWg) {
         const uint32_t v = h[b];
         if (v) atomicAdd(&g[b], v);
     }

@@ -130,13 +130,19 @@ template <class LdsT>
 __device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, bool active, LdsT &L,
                                           uint32_t (&wtot)[4], uint32_t &wg_base) {
     const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+    const int n = active ? sk.n : 0;
+    if (lane == 0) wtot[wv] = static_cast<uint32_t>(n);
     __syncthreads();
     if (*sk.ovf) {  // part of the workgroup's list is already out unsorted: plain flush (frame marked)
         if (active) sink_flush(sk, a, f);
         hist_flush(L.hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
         return;
     }
-    const int n = active ? sk.n : 0;
+    // The segment's place in the list: one returning atomic, issued before the histogram work so that
+    // its round trip overlaps the counting sort's scan (thread 0 waits for it only at its LDS store).
+    uint32_t seg_base_early = 0;
+    const uint32_t seg_total = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    if (tid == 0 && seg_total) seg_base_early = atomicAdd(&a.list_count[f], seg_total);
     auto bin_of = [&](float r) { return ((float_key(r) - a.key_base) << a.key_lz) >> 20; };
     if (!sk.ehist)  // (FAST counted its candidates at emit time)
         for (int i = lane; i < n; i += kWave) atomicAdd(&L.hist[bin_of(sk.resp[i])], 1u);
@@ -161,7 +167,7 @@ __device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, 
         run += v[k];
     }
     if (tid == 0) {
-        wg_base = total ? atomicAdd(&a.list_count[f], total) : 0u;
+        wg_base = seg_base_early;
         const int g = logical_block() % a.blocks_per_frame;
         a.segdesc[static_cast<int64_t>(f) * a.blocks_per_frame + g] = make_uint2(wg_base, total);
     }
