@@ -111,7 +111,7 @@ struct LpGeom {
 };
 
 template <bool HIST>
-struct LpLds {
+struct alignas(HIST ? 16 : 4) LpLds {  // (with HIST: hist is cleared and read as uint4, fd_corner_common.h)
     uint32_t slot[4][kLpSlots][128];  // [wave][slot][0..63 response bits | 64..127 raster index]
     uint32_t hist[HIST ? kHistBins : 1];
 };

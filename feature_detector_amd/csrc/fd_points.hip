@@ -114,12 +114,13 @@ __device__ __forceinline__ uint32_t mask_bits4(const PointsArgs &a, int f, int r
 
 // Workgroup-shared staging + level-0 histogram (detect mode).
 template <int S>
-struct DetectLdsT {
+struct alignas(16) DetectLdsT {  // (16-byte aligned: hist is cleared and read as uint4, fd_corner_common.h)
     float resp[4][S];
     uint32_t idx[4][S];
     uint32_t hist[kHistBins];
 };
 using DetectLds = DetectLdsT<kStage>;
+static_assert(sizeof(DetectLds) % 16 == 0 && offsetof(DetectLds, hist) % 16 == 0, "uint4 histogram access");
 
 // Sorted-segment flush (PointsArgs::segdesc; small launches whose tiles never overflow the staging):
 // the workgroup's candidates, all still staged in LDS, go to the frame's list as one contiguous
