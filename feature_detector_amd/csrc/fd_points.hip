@@ -201,8 +201,17 @@ __device__ __forceinline__ void corner_tile(const PointsArgs &a, int f, int ty, 
 // c0 = tx*kTileW + 4(l-1) .. c0+3 and walks the rows keeping 3-row sliding windows in registers:
 // pixels (+ DPP halo dwords), horizontal tensor sums, responses.
 // ---------------------------------------------------------------------------------------------------
+#ifdef FD_K1_CLOCKS  // diagnostic build only (tools/k1_wg_clock.py): per-workgroup s_memrealtime phase clocks
+}  // namespace
+__device__ unsigned long long g_fdk_k1_clocks[4096];
+namespace {
+#define FD_K1_CLOCK(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#else
+#define FD_K1_CLOCK(v)
+#endif
 template <int KIND, bool RASTER, bool MASKED, bool ALIGNED, bool G1>
 __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
+    FD_K1_CLOCK(t_entry);
     __shared__ DetectLds lds_all[1];
     int f, ty, tx;
     const bool active = decode_tile(a, f, ty, tx);
@@ -215,11 +224,24 @@ __global__ __launch_bounds__(256) void k_corner(PointsArgs a) {
         if (a.hist0) hist_clear(lds_all[0].hist);
         else __syncthreads();
     }
+    FD_K1_CLOCK(t_clr);
     if (active) corner_tile<KIND, RASTER, MASKED, ALIGNED, G1>(a, f, ty, tx, sk);
+    FD_K1_CLOCK(t_tile);
     if constexpr (!RASTER) {
         if (a.segdesc) {
             __shared__ uint32_t seg_wtot[4], seg_base;
             seg_flush(sk, a, f, active, lds_all[0], seg_wtot, seg_base);
+#ifdef FD_K1_CLOCKS
+            __syncthreads();
+            FD_K1_CLOCK(t_end);
+            if (threadIdx.x == 0 && blockIdx.x < 1024) {
+                unsigned long long *c = g_fdk_k1_clocks + 4 * blockIdx.x;
+                c[0] = t_entry;
+                c[1] = t_clr;
+                c[2] = t_tile;
+                c[3] = t_end;
+            }
+#endif
         } else {
             if (active) sink_flush(sk, a, f);
             if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
@@ -810,3 +832,10 @@ hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s) {
 }
 
 }  // namespace fdk
+
+#ifdef FD_K1_CLOCKS
+extern "C" int fd_debug_k1_clocks(unsigned long long *out, int n) {
+    return static_cast<int>(hipMemcpyFromSymbol(out, HIP_SYMBOL(fdk::g_fdk_k1_clocks), sizeof(unsigned long long) * n, 0,
+                                                hipMemcpyDeviceToHost));
+}
+#endif

@@ -418,9 +418,20 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     // order, waiting for the histogram leaves the list loads in flight.
     // The list loads go straight to LDS (global_load_lds: no VGPRs held across the histogram scan),
     // into the occupancy grid's space, which is initialised only after this first round is consumed.
+    // (4 bins per thread: thread t loads bins 4t..4t+3 as one 16-byte load and forms the level-0
+    // suffix sums from registers, below; other workgroup sizes load strided bins and go through LDS)
+    constexpr bool kHist4 = kHistPerThread == 4;
     uint32_t hv[kHistPerThread];
+    if constexpr (kHist4) {
+        const uint4 h4 = reinterpret_cast<const uint4 *>(a.hist0 + static_cast<int64_t>(f) * kHistBins)[tid];
+        hv[0] = h4.x;
+        hv[1] = h4.y;
+        hv[2] = h4.z;
+        hv[3] = h4.w;
+    } else {
 #pragma unroll
-    for (int j = 0; j < kHistPerThread; ++j) hv[j] = a.hist0[static_cast<int64_t>(f) * kHistBins + tid + j * NT];
+        for (int j = 0; j < kHistPerThread; ++j) hv[j] = a.hist0[static_cast<int64_t>(f) * kHistBins + tid + j * NT];
+    }
     float *const pre_lds = reinterpret_cast<float *>(grid_lds);
     static_assert(kRegGather * NT <= kGridLdsCells, "first gather round fits the grid's LDS");
     // sorted-segment mode: this frame's segment descriptors instead of the list prefetch
@@ -562,10 +573,28 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     };
     auto suf = [&](int lvl) -> uint32_t * { return lvl == 0 ? suf0 : sufl[lvl - 1]; };
 
-    for (int j = 0; j < kHistPerThread; ++j) suf0[tid + j * NT] = hv[j];
-    __syncthreads();
-    FD_STAMP(1);
-    suffix(suf0, kHistBins);
+    if constexpr (kHist4) {
+        // suffix(suf0, kHistBins) from the registers: no LDS round trip per bin, one 16-byte store
+        FD_STAMP(1);
+        const uint32_t sacc = hv[0] + hv[1] + hv[2] + hv[3];
+        const uint32_t incl = wave_suffix_add(sacc);
+        if (lane == 0) wtot[wave] = incl;
+        __syncthreads();
+        const uint32_t after = wave_total_add((lane > wave && lane < nthr / kWave) ? wtot[lane] : 0u);
+        uint4 o;
+        o.w = incl - sacc + after + hv[3];
+        o.z = o.w + hv[2];
+        o.y = o.z + hv[1];
+        o.x = o.y + hv[0];
+        reinterpret_cast<uint4 *>(suf0)[tid] = o;
+        if (tid == 0) suf0[kHistBins] = 0;
+        __syncthreads();
+    } else {
+        for (int j = 0; j < kHistPerThread; ++j) suf0[tid + j * NT] = hv[j];
+        __syncthreads();
+        FD_STAMP(1);
+        suffix(suf0, kHistBins);
+    }
     FD_STAMP(2);
 
     // Register-blocked gather of the keys whose 32-bit key lies in [k32lo, k32hi] (exact for chunks
