@@ -296,16 +296,38 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
 }
 
 // Conflict masks of a chunk in scan order: bit j of cmask[p] = candidate (p & ~63) + j, earlier in p's
-// batch of 64, lies within Chebyshev distance d. One work item per (candidate, quarter of its batch):
-// 16 entries each, no divergent trip counts; each item writes its 16 bits of the 64-bit mask.
+// batch of 64, lies within Chebyshev distance d. One work item per (candidate, quarter of its batch)
+// that holds earlier candidates: 16 entries each, no divergent trip counts; each item writes its 16
+// bits of the 64-bit mask. Only those items are enumerated (157 per batch of 64 instead of 4 x 64, the
+// rest were idle lanes): quarter 0 for every position me (me = 0 tests nothing) -- that item also
+// zeroes the quarters past its own -- and quarter q >= 1 for me > 16q, q-major within the batch.
+constexpr int kCmItems = 64 + 47 + 31 + 15;
 __device__ __forceinline__ void conflict_masks(const uint32_t *pxy, int c, int d, int rows, int cols, uint64_t *cmask,
                                                int tid, int nthr) {
     uint16_t *cm16 = reinterpret_cast<uint16_t *>(cmask);
     const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
     const uint32_t w2 = 2u * static_cast<uint32_t>(d);
-    for (int item = tid; item < 4 * c; item += nthr) {
-        const int p = item >> 2, q = item & 3;
-        const int bb = p & ~63, me = p - bb;
+    const int n_items = ((c + kWave - 1) / kWave) * kCmItems;
+    for (int item = tid; item < n_items; item += nthr) {
+        const int bi = item / kCmItems, t = item - bi * kCmItems;
+        int q, me;
+        if (t < 64) {
+            q = 0;
+            me = t;
+        } else if (t < 64 + 47) {
+            q = 1;
+            me = t - 64 + 17;
+        } else if (t < 64 + 47 + 31) {
+            q = 2;
+            me = t - (64 + 47) + 33;
+        } else {
+            q = 3;
+            me = t - (64 + 47 + 31) + 49;
+        }
+        const int bb = bi * kWave, p = bb + me;
+        if (p >= c) continue;
+        if (q == 0)  // quarters without an item of their own (16q >= me): no earlier candidates there
+            for (int qz = max(1, (me + 15) >> 4); qz < 4; ++qz) cm16[4 * p + qz] = 0;
         const uint32_t e = pxy[p];
         uint32_t bits = 0;
         if (e != kEmpty && 16 * q < me) {
