@@ -87,9 +87,13 @@ __device__ __forceinline__ uint64_t make_key(float resp, uint32_t idx, const Sel
 
 constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
 #ifndef FD_SEQ_CONFLICTS
-#define FD_SEQ_CONFLICTS 12
+#define FD_SEQ_CONFLICTS 0
 #endif
-constexpr int kSeqConflicts = FD_SEQ_CONFLICTS;  // greedy batch: ordered scalar pass up to this many conflicted lanes
+// greedy batch: ordered scalar pass up to this many conflicted lanes, else the fixed point. Sweep at the
+// headline (profiles/r03_select_rejected.txt): 0 (always the fixed point) 19.3-19.5 us, 2: 19.6-20.0,
+// 4: 19.5-19.7, 12: 20.1-20.2 -- the fixed point's passes (the longest conflict chain, ~2-3) cost less
+// than one ordered step per conflicted lane.
+constexpr int kSeqConflicts = FD_SEQ_CONFLICTS;
 // Keys ordered per greedy sub-chunk: corner frames usually stop within the first few hundred; FAST's
 // long scans drop most keys before ordering (grid prefilter), so there the whole superchunk is one
 // sub-chunk (measured at 1280x720x64: 512 -> 190 us, 768 -> 166, 2048 -> 160; the 1080p list-mode
@@ -207,10 +211,10 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         gst(26);  // grid test
         C &= m;
         // Resolution in scan order: a lane with no earlier ok neighbour in the batch is accepted; the
-        // others (few: distance-d pairs inside 64 consecutive candidates) are decided one by one in
-        // ascending order on the scalar unit -- accepted iff none of their earlier neighbours was.
-        // Many conflicted lanes (FAST's clustered top keys): a fixed point instead, where each pass
-        // decides every lane whose earlier neighbours are all decided (passes = the longest chain).
+        // conflicted ones are decided by a fixed point, where each pass decides every lane whose earlier
+        // neighbours are all decided (passes = the longest chain) -- accepted iff none of them was. (With
+        // FD_SEQ_CONFLICTS > 0, up to that many conflicted lanes are instead decided one by one in
+        // ascending order on the scalar unit: slower at every threshold measured, see kSeqConflicts.)
         const uint64_t conf = ballot(C != 0ull) & m;
         uint64_t acc_m = m & ~conf;
         if (popc64(conf) <= kSeqConflicts) {
