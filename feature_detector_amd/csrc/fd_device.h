@@ -80,6 +80,15 @@ __device__ __forceinline__ uint32_t wave_suffix_add(uint32_t x) {
     return tot - p + x;
 }
 
+// A value the compiler cannot see through: an LDS address derived from it inside a loop is recomputed
+// there (one VALU op) instead of being hoisted across the enclosing loops -- k_select runs at its
+// 128-VGPR limit, and such hoisted addresses were spilled to scratch and reloaded (a memory round trip)
+// at every sub-chunk.
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 __device__ __forceinline__ uint64_t lanes_below() {

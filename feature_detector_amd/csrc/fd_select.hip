@@ -276,7 +276,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         // and cannot matter, see select_frame.)
         const int last = done ? stop : cnt - 1;
         bool t = false;
-        for (int w = lane; w * kWave <= last; w += kWave) {
+        for (int w = opaque(lane); w * kWave <= last; w += kWave) {
             uint64_t word = tmask[w];
             if (w * kWave + kWave - 1 > last) word &= (2ull << (last & (kWave - 1))) - 1ull;
             t = t || word != 0ull;
@@ -1324,7 +1324,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     }
                     if (!a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
                         const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;
-                        for (int i = tid; i < c64; i += nthr) {
+                        for (int i = opaque(tid); i < c64; i += nthr) {
                             const bool t = i > 0 && i < c && L.pk32[i] == L.pk32[i - 1];
                             const uint64_t m = ballot(t);
                             if (lane == 0) L.tmask[i >> 6] = m;
