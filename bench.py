@@ -12,7 +12,7 @@ batch (weak scaling) with no collective on the data path; only the timing barrie
 the process group. value = pixels processed by all ranks / max-over-ranks time.
 
 Also reported: the roofline of the per-pixel kernel (HIP-event timed, algorithmic bytes = 1 B/px of
-frame input; traffic = measured FETCH_SIZE from profiles/r02_traffic.json), the north-star shape
+frame input; traffic = measured FETCH_SIZE from profiles/r03_traffic.json), the north-star shape
 (Shi-Tomasi 1920x1080 batch 256), and the CPU baseline (the oracle restatement on a bounded sample of
 the same workload: single thread, and a pool of up to 16 threads).
 """
