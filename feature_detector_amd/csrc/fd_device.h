@@ -69,6 +69,27 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
     x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xC, 0xF, false));  // row_bcast:31
     return x;
 }
+// Max / min over the wave (unsigned), in every lane: the same DPP row_shr / row_bcast ladder as
+// wave_incl_add with the identity as the value of lanes that have no source, then lane 63's result
+// (instead of six ds_bpermute round trips of a __shfl_xor butterfly).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xF, 0xF, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xF, 0xF, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xF, 0xF, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xF, 0xF, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xA, 0xF, false)));
+    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xC, 0xF, false)));
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    x = min(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(x), 0x111, 0xF, 0xF, false)));
+    x = min(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(x), 0x112, 0xF, 0xF, false)));
+    x = min(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(x), 0x114, 0xF, 0xF, false)));
+    x = min(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(x), 0x118, 0xF, 0xF, false)));
+    x = min(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(x), 0x142, 0xA, 0xF, false)));
+    x = min(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(-1, static_cast<int>(x), 0x143, 0xC, 0xF, false)));
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+}
 // Sum over the wave, in every lane.
 __device__ __forceinline__ uint32_t wave_total_add(uint32_t x) {
     return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wave_incl_add(x)), 63));

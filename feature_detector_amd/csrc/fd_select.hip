@@ -1100,6 +1100,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                                                                       (udiv16q(x, s1, rcp_s1) + 1));
                                     const uint32_t e = (y << 16) | x;
                                     const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+                                    if (grid_in_lds && grid_pk15(rows, cols, d)) {  // as greedy_chunk's grid test
+                                        uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+                                        for (int q = 0; q < 9; ++q) {
+                                            const u16x2 dt = __builtin_bit_cast(u16x2, grid_lds[cell + (q / 3 - 1) * gw2 + (q % 3 - 1)]) - base;
+                                            mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
+                                        }
+                                        if (mn <= w2) keep = false;
+                                    } else
 #pragma unroll
                                     for (int q = 0; q < 9; ++q) {
                                         const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
@@ -1125,10 +1134,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                                 if (keep) kbuf[mbcnt64(m, off)] = sk;
                             }
                         }
-                        for (int o = kWave / 2; o > 0; o >>= 1) {
-                            kmax = max(kmax, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmax), o)));
-                            kmin = min(kmin, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmin), o)));
-                        }
+                        kmax = wave_max_u32(kmax);
+                        kmin = wave_min_u32(kmin);
                         if (lane == 0) {
                             atomicMax(&L.seg_more[0], kmax);
                             atomicMin(&L.seg_more[1], kmin);
@@ -1214,10 +1221,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                             kmx = max(kmx, static_cast<uint32_t>(kk[j] >> 32));
                         }
                     }
-                    for (int o = kWave / 2; o > 0; o >>= 1) {
-                        kmn = min(kmn, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmn), o)));
-                        kmx = max(kmx, static_cast<uint32_t>(__shfl_xor(static_cast<int>(kmx), o)));
-                    }
+                    kmn = wave_min_u32(kmn);
+                    kmx = wave_max_u32(kmx);
                     __syncthreads();  // (lb_rng, lcnt initialised)
                     if (lane == 0 && kmn <= kmx) {
                         atomicMin(&L.lb_rng[0], kmn);
