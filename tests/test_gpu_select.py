@@ -78,3 +78,13 @@ def test_sorted_segment_lists_toggle(fd, oracle, seg, monkeypatch):
         frames = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 700 + i, *shape) for i in range(bsz)])
         for name, dist, need in (("harris", 20, 200), ("shi_tomasi", 3, 800), ("fast", 20, 200), ("harris", 0, 50)):
             _check(fd, oracle, name, frames, need, dist)
+
+
+@pytest.mark.parametrize("rows,cols,dist", [(24, 32760, 3), (24, 40000, 20), (20, 65400, 100), (33000, 24, 20)])
+@pytest.mark.parametrize("name", ["harris", "fast"])
+def test_wide_frames_grid_sentinels(fd, oracle, name, rows, cols, dist):
+    # The greedy's occupancy grid marks empty cells 0x7FFF7FFF (a position that fails the packed distance
+    # test by itself) only while rows, cols + 3d < 2^15; wider frames keep 0xFFFFFFFF with explicit
+    # checks, in the packed-halves test (+ 3d < 2^16) or the plain one (the 65400-column case).
+    img = oracle.make_frame("noise", 910 + cols % 97, rows, cols)
+    _check(fd, oracle, name, img[None], 400, dist)
