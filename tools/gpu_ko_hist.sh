@@ -1,3 +1,5 @@
+# Timing-only knockout A/B (profiles/r03_k1_hist_ko.txt): abvar/base.so = HEAD, abvar/kohist.so = HEAD with
+# hist_flush (fd_corner_common.h) adding only when (logical_block() & 7) == 0; both under rocprofv3 kernel stats.
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out/abl
 for L in abvar/base.so abvar/kohist.so abvar/base.so abvar/kohist.so; do
   n=$(basename $L .so)_$RANDOM
