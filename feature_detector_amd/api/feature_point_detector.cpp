@@ -63,13 +63,45 @@ bool FeaturePointDetector::Fail(const std::string &what) {
     return false;
 }
 
-// DetectGoodFeatures (feature_point_detector.cpp:7-25) + SelectGoodFeatures (:54-74), on the GPU.
+// DetectGoodFeatures (feature_point_detector.cpp:7-25): the mask state of :12-16 (materialised on
+// access), a cleared candidate list (:19), the virtual ComputeCandidates (:20), then SelectGoodFeatures
+// (:23, :54-74) on the GPU -- fused with the candidate stage when ComputeCandidates deferred to it.
 bool FeaturePointDetector::DetectGoodFeatures(const GrayImage &image, const uint32_t needed_feature_num,
                                               std::vector<Vec2> &features) {
     if (image.data() == nullptr) return false;  // RETURN_FALSE_IF(image.data() == nullptr) (:9)
-    if (KindId() < 0) return DetectWithOwnCandidates(image, needed_feature_num, features);
     fd_ctx *ctx = Context();
     if (!ctx) return Fail("no device context");
+    last_prior_ = features;
+    last_new_.clear();
+    last_rows_ = image.rows();
+    last_cols_ = image.cols();
+    last_options_ = options_;
+    last_reached_need_ = false;
+    staged_frame_ = nullptr;
+    mask_valid_ = false;
+    candidates_.clear();
+    candidates_valid_ = true;
+    candidates_sorted_ = true;
+    fused_kind_ = -1;
+    in_detect_ = true;
+    const bool ok = ComputeCandidates(image);
+    in_detect_ = false;
+    if (!ok) return false;  // RETURN_FALSE_IF_FALSE(ComputeCandidates(image)) (:20)
+    if (fused_kind_ >= 0) return DetectFused(image, fused_kind_, needed_feature_num, features);
+    candidates_sorted_ = false;
+    return SelectOwnCandidates(needed_feature_num, features);
+}
+
+bool FeaturePointDetector::DeferCandidatesToGpu(int kind) {
+    if (!in_detect_) return Fail("DeferCandidatesToGpu outside DetectGoodFeatures");
+    fused_kind_ = kind;
+    return true;
+}
+
+// The built-in detectors: mask, candidates and selection as one fd_points_detect on the staged frame.
+bool FeaturePointDetector::DetectFused(const GrayImage &image, int kind, const uint32_t needed_feature_num,
+                                       std::vector<Vec2> &features) {
+    fd_ctx *ctx = ctx_;
     const int32_t rows = image.rows(), cols = image.cols();
     const uint8_t *dframe = nullptr;
     if (fd_ctx_stage(ctx, image.data(), static_cast<int64_t>(rows) * cols, &dframe) != FD_OK)
@@ -85,51 +117,26 @@ bool FeaturePointDetector::DetectGoodFeatures(const GrayImage &image, const uint
     const int32_t stride = static_cast<int32_t>(std::max<uint32_t>(needed_feature_num, 1u)) + 1;
     std::vector<float> out(2 * static_cast<size_t>(stride));
     int32_t count = 0;
-    const int rc = fd_points_detect(ctx, KindId(), dframe, 1, 1, rows, cols, &opts,
+    const int rc = fd_points_detect(ctx, kind, dframe, 1, 1, rows, cols, &opts,
                                     nprior ? prior.data() : nullptr, nprior ? &nprior : nullptr, needed_feature_num,
                                     out.data(), stride, &count, 0);
     if (rc != FD_OK) return Fail("fd_points_detect");
 
-    last_prior_ = features;
-    last_new_.clear();
     for (int32_t i = 0; i < count; ++i) {
         features.emplace_back(Vec2(out[2 * i], out[2 * i + 1]));
         last_new_.emplace_back(Vec2(out[2 * i], out[2 * i + 1]));
     }
     staged_frame_ = dframe;
-    last_rows_ = rows;
-    last_cols_ = cols;
-    last_options_ = options_;
     last_reached_need_ = count > 0 && features.size() >= needed_feature_num;
     candidates_valid_ = false;
     mask_valid_ = false;
     return true;
 }
 
-// DetectGoodFeatures (:7-25) for a subclass with its own ComputeCandidates: the mask state of :12-16
-// (materialised on access), the subclass's candidates (:19-20), then SelectGoodFeatures (:23, :54-74)
-// on the GPU over them (fd_points_select, in the order they were pushed).
-bool FeaturePointDetector::DetectWithOwnCandidates(const GrayImage &image, const uint32_t needed_feature_num,
-                                                   std::vector<Vec2> &features) {
-    fd_ctx *ctx = Context();
-    if (!ctx) return Fail("no device context");
-    const int32_t rows = image.rows(), cols = image.cols();
-    last_prior_ = features;
-    last_new_.clear();
-    last_rows_ = rows;
-    last_cols_ = cols;
-    last_options_ = options_;
-    last_reached_need_ = false;
-    staged_frame_ = nullptr;
-    mask_valid_ = false;
-    candidates_.clear();
-    candidates_valid_ = true;
-    candidates_sorted_ = true;
-    if (!ComputeCandidates(image)) return false;  // RETURN_FALSE_IF_FALSE (:20)
-    candidates_valid_ = true;
-    candidates_sorted_ = false;
+// SelectGoodFeatures (:54-74) over the candidates a subclass pushed (fd_points_select, in the order
+// they were pushed).
+bool FeaturePointDetector::SelectOwnCandidates(const uint32_t needed_feature_num, std::vector<Vec2> &features) {
     if (candidates_.empty()) return true;  // RETURN_TRUE_IF(candidates_.empty()) (:55)
-
     const size_t n = candidates_.size();
     std::vector<float> resp(n);
     std::vector<int32_t> xs(n), ys(n);
@@ -149,9 +156,9 @@ bool FeaturePointDetector::DetectWithOwnCandidates(const GrayImage &image, const
     std::vector<float> out(2 * static_cast<size_t>(stride));
     const int64_t count_in = static_cast<int64_t>(n);
     int32_t count = 0;
-    const int rc = fd_points_select(ctx, 1, rows, cols, &opts, resp.data(), xs.data(), ys.data(), &count_in, count_in,
-                                    0, nprior ? prior.data() : nullptr, nprior ? &nprior : nullptr, needed_feature_num,
-                                    out.data(), stride, &count, 0);
+    const int rc = fd_points_select(ctx_, 1, last_rows_, last_cols_, &opts, resp.data(), xs.data(), ys.data(),
+                                    &count_in, count_in, 0, nprior ? prior.data() : nullptr,
+                                    nprior ? &nprior : nullptr, needed_feature_num, out.data(), stride, &count, 0);
     if (rc != FD_OK) return Fail("fd_points_select");
     for (int32_t i = 0; i < count; ++i) {
         features.emplace_back(Vec2(out[2 * i], out[2 * i + 1]));
@@ -162,14 +169,12 @@ bool FeaturePointDetector::DetectWithOwnCandidates(const GrayImage &image, const
     return true;
 }
 
-// ComputeCandidates seam (feature_point_detector.h:44) of the built-in kinds: raster-ordered
-// candidates of the staged frame. A subclass without a kind and without its own ComputeCandidates
-// has no candidates: false, as the reference's pure virtual would not have compiled.
-bool FeaturePointDetector::ComputeCandidates(const GrayImage & /*image*/) {
+// candidates() after a fused call: the raster-ordered candidates of the staged frame (the sequence the
+// reference's ComputeCandidates pushes), recomputed on the GPU.
+bool FeaturePointDetector::FetchCandidates() {
     candidates_.clear();
-    if (KindId() < 0) return Fail("ComputeCandidates is not overridden and KindId() names no built-in detector");
-    if (!staged_frame_ || !ctx_) return false;
-    const int64_t cap = static_cast<int64_t>(last_rows_) * last_cols_ / (KindId() == FD_FAST ? 1 : 2) + 16;
+    if (fused_kind_ < 0 || !staged_frame_ || !ctx_) return false;
+    const int64_t cap = static_cast<int64_t>(last_rows_) * last_cols_ / (fused_kind_ == FD_FAST ? 1 : 2) + 16;
     std::vector<float> resp(static_cast<size_t>(cap));
     std::vector<int32_t> xs(static_cast<size_t>(cap)), ys(static_cast<size_t>(cap));
     std::vector<float> prior(2 * last_prior_.size());
@@ -180,7 +185,7 @@ bool FeaturePointDetector::ComputeCandidates(const GrayImage & /*image*/) {
     const int32_t nprior = static_cast<int32_t>(last_prior_.size());
     const fd_point_opts opts{last_options_.kMinFeatureDistance, last_options_.kMinValidResponse};
     int64_t n = 0;
-    const int rc = fd_points_candidates(ctx_, KindId(), staged_frame_, 1, 1, last_rows_, last_cols_, &opts,
+    const int rc = fd_points_candidates(ctx_, fused_kind_, staged_frame_, 1, 1, last_rows_, last_cols_, &opts,
                                         nprior ? prior.data() : nullptr, nprior ? &nprior : nullptr, resp.data(),
                                         xs.data(), ys.data(), cap, &n, nullptr, 0);
     if (rc != FD_OK) return Fail("fd_points_candidates");
@@ -198,8 +203,7 @@ void FeaturePointDetector::Materialise() const {
     };
     if (!candidates_valid_) {
         candidates_valid_ = true;
-        GrayImage none;
-        if (self->ComputeCandidates(none)) sort_ref();
+        if (self->FetchCandidates()) sort_ref();
     } else if (!candidates_sorted_) {
         candidates_sorted_ = true;
         sort_ref();
@@ -258,8 +262,12 @@ void FeaturePointDetector::SparsifyFeatures(const std::vector<Vec2> &features, c
     mask_valid_ = true;  // mask_ now holds the grid mask, as in the reference
 }
 
-int FeaturePointHarrisDetector::KindId() const { return FD_HARRIS; }
-int FeaturePointShiTomasDetector::KindId() const { return FD_SHI_TOMASI; }
-int FeaturePointFastDetector::KindId() const { return FD_FAST; }
+// The built-in detectors' ComputeCandidates (feature_point_harris_detector.cpp:5-15, shi_tomas :5-15,
+// fast :83-98): the whole detection runs fused on the GPU.
+bool FeaturePointHarrisDetector::ComputeCandidates(const GrayImage & /*image*/) { return DeferCandidatesToGpu(FD_HARRIS); }
+bool FeaturePointShiTomasDetector::ComputeCandidates(const GrayImage & /*image*/) {
+    return DeferCandidatesToGpu(FD_SHI_TOMASI);
+}
+bool FeaturePointFastDetector::ComputeCandidates(const GrayImage & /*image*/) { return DeferCandidatesToGpu(FD_FAST); }
 
 }  // namespace feature_detector

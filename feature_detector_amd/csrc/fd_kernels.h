@@ -130,6 +130,18 @@ struct OrderedArgs {
     const int32_t *frame;   // [n_frames] frame index (into SelectArgs' per-frame arrays)
 };
 
+// k_select_reference (FD_TIES_REFERENCE on the GPU): per-frame scratch of cap entries each (cap >= the
+// list capacity and >= rows * cols / 32: the raster-order bitmap and its word prefix live in lpos / rpos).
+struct RefSortArgs {
+    uint2 *x;        // [batch][cap] (response bits, raster index) in push order, partitioned in place
+    uint32_t *lpos;  // [batch][cap] left-stopper positions by rank (per level)
+    uint32_t *rpos;  // [batch][cap] right-stopper positions by rank
+    uint32_t *ord;   // [batch][cap] the reference's visiting order (raster indices) of the finalised prefix
+    int64_t cap;
+    int push_order;  // the list is already in push order (fd_points_select); else unique raster indices
+    uint32_t *dbg;   // [batch][8] first broken invariant per frame (FD_REF_DEBUG), or null
+};
+
 // fd_points_select: caller candidates (response, x, y at [f * stride], counts[f]) -> list format.
 struct CandInArgs {
     const float *resp;
@@ -255,6 +267,8 @@ hipError_t launch_corner_lp_any(int kind, const PointsArgs &a, hipStream_t s);  
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s);
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
 hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);
+// libstdc++ std::sort order emulated on the GPU for the frames k_select flagged (FD_FRAME_TIES)
+hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r, int batch, hipStream_t s);
 hipError_t launch_cand_lists(const CandInArgs &a, int64_t max_count, hipStream_t s);
 hipError_t launch_nn_pick(const NnPickArgs &a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);

@@ -57,7 +57,8 @@ struct fd_ctx {
     DevBuf status;
     int status_batch = 0;
     int tie_order = FD_TIES_RASTER;
-    DevBuf ord, ord_meta;  // FD_TIES_REFERENCE: host-computed visiting orders of flagged frames
+    DevBuf ord, ord_meta;  // FD_TIES_REFERENCE host path: host-computed visiting orders of flagged frames
+    DevBuf r_x, r_lpos, r_rpos, r_ord;  // FD_TIES_REFERENCE on the GPU (k_select_reference scratch)
     DevBuf run_lut;        // FAST score per 16-bit ring mask (FastOffsets::run_lut), filled once
     // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
     DevBuf l_lnorm, l_langle, l_fbase;
@@ -440,6 +441,23 @@ std::string hex(uint32_t v) {
     return std::string(t);
 }
 
+// Scratch of k_select_reference for `batch` frames of lists of `cap` entries.
+int ref_buffers(fd_ctx *c, int batch, int rows, int cols, int64_t cap, fdk::RefSortArgs &r) {
+    const int64_t words = (static_cast<int64_t>(rows) * cols + 31) / 32;
+    const int64_t rcap = std::max<int64_t>({cap, words, 1});
+    const size_t n = static_cast<size_t>(rcap) * static_cast<size_t>(batch);
+    FD_HIP_TRY(c, ensure(c, c->r_x, sizeof(uint2) * n));
+    FD_HIP_TRY(c, ensure(c, c->r_lpos, sizeof(uint32_t) * n));
+    FD_HIP_TRY(c, ensure(c, c->r_rpos, sizeof(uint32_t) * n));
+    FD_HIP_TRY(c, ensure(c, c->r_ord, sizeof(uint32_t) * n));
+    r.x = as<uint2>(c->r_x);
+    r.lpos = as<uint32_t>(c->r_lpos);
+    r.rpos = as<uint32_t>(c->r_rpos);
+    r.ord = as<uint32_t>(c->r_ord);
+    r.cap = rcap;
+    return FD_OK;
+}
+
 // FD_TIES_REFERENCE (fd_ctx_set_tie_order): frames whose greedy scan met equal responses
 // (FD_FRAME_TIES from k_select) are selected again in the reference's own order. The reference sorts
 // its raster-ordered candidates with an unstable std::sort (feature_point_detector.cpp:58-60), whose
@@ -448,7 +466,9 @@ std::string hex(uint32_t v) {
 // (the order ComputeCandidates pushes them, feature_point_harris_detector.cpp:120-137,
 // feature_point_fast_detector.cpp:83-98), sorted here with std::sort and the reference comparator,
 // and the resulting visiting order goes back to the GPU for the greedy pass (k_select_ordered).
-int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb, bool push_order) {
+// `which` selects the frames: FD_FRAME_TIES (FD_TIES_HOST=1: the host path for every flagged frame) or
+// FD_FRAME_UNRESOLVED (the frames k_select_reference left to the host).
+int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb, bool push_order, uint32_t which) {
     // The status read below synchronises the stream, which a stream being captured into a graph cannot
     // do (and the host sort could not be replayed): refuse before touching the capture.
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -464,7 +484,7 @@ int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb, 
         if (st[b] & FD_FRAME_GUARD)  // (read here anyway: reported for device outputs too)
             return fail(c, FD_ERR_HIP, "internal: selection consistency guard tripped (status 0x" + hex(st[b]) +
                                            ", frame " + std::to_string(b) + ")");
-        if (st[b] & FD_FRAME_TIES) frames.push_back(b);
+        if (st[b] & which) frames.push_back(b);
     }
     if (frames.empty()) return FD_OK;
     struct Cand {
@@ -644,8 +664,36 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         }
     }
     if (c->tie_order == FD_TIES_REFERENCE && !q.tie_idx_desc) {
-        const int rc = resolve_ties(c, s, batch, sb, q.push_order);
-        if (rc) return rc;
+        static const bool host_ties = std::getenv("FD_TIES_HOST") && std::atoi(std::getenv("FD_TIES_HOST")) != 0;
+        if (host_ties) {  // the round-3 host path (A/B and checker): every flagged frame sorted on the host
+            const int rc = resolve_ties(c, s, batch, sb, q.push_order, FD_FRAME_TIES);
+            if (rc) return rc;
+        } else {
+            fdk::RefSortArgs r{};
+            const int rc = ref_buffers(c, batch, rows, cols, q.cap, r);
+            if (rc) return rc;
+            r.push_order = q.push_order ? 1 : 0;
+            static const bool ref_debug = std::getenv("FD_REF_DEBUG") != nullptr;  // diagnostic: broken invariants
+            if (ref_debug) {
+                FD_HIP_TRY(c, ensure(c, c->dbg, sizeof(uint32_t) * 8 * batch));
+                FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint32_t) * 8 * batch, c->stream));
+                r.dbg = as<uint32_t>(c->dbg);
+            }
+            FD_HIP_TRY(c, fdk::launch_select_reference(s, r, batch, c->stream));
+            if (ref_debug) {
+                std::vector<uint32_t> h(static_cast<size_t>(8) * batch);
+                FD_HIP_TRY(c, hipMemcpyAsync(h.data(), c->dbg.p, sizeof(uint32_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
+                FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+                for (int b = 0; b < batch; ++b)
+                    if (h[8 * b])
+                        std::fprintf(stderr, "k_select_reference frame %d: check %u idx %u bound %u m_act %u T %u\n", b, h[8 * b],
+                                     h[8 * b + 1], h[8 * b + 2], h[8 * b + 3], h[8 * b + 4]);
+            }
+            if (!outputs_on_device) {  // the call synchronises anyway: frames left to the host
+                const int rc2 = resolve_ties(c, s, batch, sb, q.push_order, FD_FRAME_UNRESOLVED);
+                if (rc2) return rc2;
+            }
+        }
     }
     if (!outputs_on_device) {
         std::vector<uint32_t> st(static_cast<size_t>(batch));
@@ -735,7 +783,8 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
                       &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
-                      &c->l_lnorm,  &c->l_langle, &c->l_fbase, &c->wide_keys};
+                      &c->l_lnorm,  &c->l_langle, &c->l_fbase, &c->wide_keys, &c->r_x, &c->r_lpos,
+                      &c->r_rpos,   &c->r_ord};
     for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle, &c->h_png}) release(*b);
     release(c->d_png);
     for (DevBuf *b : bufs) release(*b);
@@ -844,6 +893,11 @@ int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t m
         }
     }
     FD_HIP_TRY(c, ensure(c, c->status, sizeof(uint32_t) * 2 * static_cast<size_t>(batch)));
+    if (c->tie_order == FD_TIES_REFERENCE) {  // k_select_reference's scratch
+        fdk::RefSortArgs r{};
+        rc = ref_buffers(c, batch, rows, cols, cap, r);
+        if (rc) return rc;
+    }
     for (const int px : {0, corner_px(kind, batch, rows, cols, 0.0f)}) {  // (either kernel's geometry)
         const PointGeom g = point_geom(kind, batch, rows, cols, px);
         if (!g.empty && use_seg_lists(g.blocks_per_frame, rows, cols)) {
@@ -1044,7 +1098,9 @@ static int points_response(fd_ctx *c, int kind, const uint8_t *frames, int batch
     if (!opts || !frames || !out_resp || !out_idx || !out_counts || cand_cap < 1)
         return fail(c, FD_ERR_INVALID, "bad arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
-    const int px = corner_px(kind, batch, rows, cols, opts->min_valid_response);
+    // k_corner_lp addresses the caller's list through a buffer resource of cand_cap * 4 bytes and
+    // 32-bit byte offsets: larger capacities take k_corner (64-bit positions against the int64 cap).
+    const int px = cand_cap < (int64_t(1) << 30) ? corner_px(kind, batch, rows, cols, opts->min_valid_response) : 0;
     const PointGeom g = point_geom(kind, batch, rows, cols, px);
     if (reset_counts) FD_HIP_TRY(c, hipMemsetAsync(out_counts, 0, sizeof(uint32_t) * batch, c->stream));
     if (g.empty) return FD_OK;

@@ -1,0 +1,567 @@
+// K4d k_select_reference: the reference tie order (FD_TIES_REFERENCE) on the GPU, graph-capturable.
+//
+// SelectGoodFeatures sorts its raster-ordered candidates with an unstable std::sort
+// (feature_point_detector.cpp:58-60); among equal responses the visiting order is whatever libstdc++'s
+// introsort leaves. k_select visits equal responses by raster index and flags every frame whose scanned
+// prefix meets a tie (FD_FRAME_TIES); this kernel re-selects exactly those frames in libstdc++'s order.
+//
+// libstdc++ (GCC 11, bits/stl_algo.h) std::sort = __introsort_loop(first, last, 2 * __lg(n)) then
+// __final_insertion_sort. The loop partitions a range of more than 16 elements around the median of
+// (first + 1, mid, last - 1) moved to `first` (__move_median_to_first), by __unguarded_partition over
+// [first + 1, last): a left scan stops at elements e with !(e > pivot) ("left stoppers", LS: resp <=
+// pivot), a right scan at !(pivot > e) ("right stoppers", RS: resp >= pivot), and the k-th left stopper
+// from the left swaps with the k-th right stopper from the right while l_k < r_k. With K such swaps the
+// cut is min(l_{K+1}, r_K) (the left scan's last stop: the next original left stopper, or at the latest
+// r_K, which now holds a left stopper). Both halves recurse with depth - 1; the loop leaves ranges of <=
+// 16 elements, which the final insertion sort orders stably and never crosses (every element right of a
+// cut is <= every element left of it). So the final order of any prefix follows from partitions of the
+// ranges that overlap it alone: ranks of the stoppers come from prefix counts (ballots), the pairing is
+// a scatter of stopper positions by rank, and K per range is where l_k < r_k stops holding (monotone).
+//
+// One 1024-thread workgroup per flagged frame:
+//   1. the frame's candidates in push order: raster order for the built-in detectors (a bitmap of the
+//      candidate pixels and its word prefix ranks the unordered list), the list order as given for
+//      caller lists (fd_points_select);
+//   2. windows of kSelectChunk positions from the front: every range overlapping the window is
+//      partitioned, level by level, all of a level's ranges at once (flat index space over their
+//      partition spans, one block of it per wave), until only leaves (<= 16) cover the window; leaves
+//      are insertion-sorted by one thread each into the visiting order;
+//   3. the greedy scan of k_select_ordered over the new positions (one wave, occupancy grid); stop at
+//      `need`, else the next window (ranges right of the window wait in the range list).
+// A range that would reach the depth limit (std::__partial_sort, heapsort) is not emulated: the frame
+// gets FD_FRAME_UNRESOLVED and keeps k_select's features (the host resolves it when it synchronises).
+#include "fd_greedy.h"
+
+namespace fdk {
+
+namespace {
+
+constexpr int kRefThreads = 1024;
+constexpr int kRefWaves = kRefThreads / kWave;
+constexpr int kRefMaxRanges = 256;  // unresolved ranges (> 16) in the list; bound: DESIGN.md
+constexpr int kRefLeaf = 16;        // libstdc++ _S_threshold
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;
+
+struct alignas(16) RefLds {
+    // greedy (k_select_ordered's layout)
+    uint32_t pxy[kSelectChunk];
+    uint32_t pcell[kSelectChunk];
+    uint64_t cmask[kSelectChunk];
+    uint32_t grid_lds[kGridLdsCells];
+    // sorted list of the unresolved ranges [lo, hi) (> 16 elements), double-buffered, with depth left
+    uint32_t r_lo[2][kRefMaxRanges];
+    uint32_t r_hi[2][kRefMaxRanges];
+    uint32_t r_dep[2][kRefMaxRanges];
+    // the level's active ranges (the list's prefix overlapping the window) j < m_act
+    uint32_t o[kRefMaxRanges + 1];  // flat offset of range j's partition span [lo + 1, hi)
+    float piv[kRefMaxRanges];
+    uint32_t headL[kRefMaxRanges], headR[kRefMaxRanges], headW[kRefMaxRanges];
+    uint32_t bL[kRefMaxRanges], nL[kRefMaxRanges], eR[kRefMaxRanges], nR[kRefMaxRanges];
+    uint32_t K[kRefMaxRanges], cut[kRefMaxRanges];
+    uint32_t waveL[kRefWaves], waveR[kRefWaves];
+    // leaves produced by the level
+    uint32_t leaf_lo[2 * kRefMaxRanges], leaf_hi[2 * kRefMaxRanges];
+    uint32_t wsum[kRefWaves];
+    int cur, m_all, m_act, n_leaf, fail;
+    uint32_t T, fin;
+    int s_done, s_acc;
+    uint32_t tie_prev;
+    int tie_has_prev;
+};
+
+__device__ __forceinline__ float as_f(uint32_t u) { return __uint_as_float(u); }
+
+// Range guard of every data-dependent index (the emulation's invariants keep them in range; a broken
+// invariant clamps the access, marks the frame failed and, with RefSortArgs::dbg, records the first
+// violation: code, index, bound, level).
+#define FD_REF_IDX(idx, bound, code) ref_idx((idx), (bound), (code), L, r, f)
+__device__ __forceinline__ uint32_t ref_idx(uint32_t idx, uint32_t bound, uint32_t code, struct RefLds &L,
+                                            const RefSortArgs &r, int f);
+
+// libstdc++ __move_median_to_first(result = lo, a = lo + 1, b = mid, c = hi - 1) with comp = resp
+// greater: the position whose element becomes the pivot (swapped into lo).
+__device__ __forceinline__ uint32_t median_pos(float ra, float rb, float rc, uint32_t a, uint32_t b, uint32_t c) {
+    if (ra > rb) {
+        if (rb > rc) return b;
+        if (ra > rc) return c;
+        return a;
+    }
+    if (ra > rc) return a;
+    if (rb > rc) return c;
+    return b;
+}
+
+__device__ __forceinline__ uint32_t ref_idx(uint32_t idx, uint32_t bound, uint32_t code, RefLds &L,
+                                            const RefSortArgs &r, int f) {
+    if (idx < bound) return idx;
+    L.fail = 4;
+    if (r.dbg && atomicCAS(&r.dbg[static_cast<int64_t>(f) * 8], 0u, code) == 0u) {
+        r.dbg[static_cast<int64_t>(f) * 8 + 1] = idx;
+        r.dbg[static_cast<int64_t>(f) * 8 + 2] = bound;
+        r.dbg[static_cast<int64_t>(f) * 8 + 3] = static_cast<uint32_t>(L.m_act);
+        r.dbg[static_cast<int64_t>(f) * 8 + 4] = L.T;
+    }
+    return bound ? bound - 1u : 0u;
+}
+
+// Exclusive prefix of v over the workgroup; total in *tot. Two barriers.
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t *wsum, uint32_t &tot) {
+    const int lane = lane_id(), w = threadIdx.x / kWave;
+    const uint32_t incl = wave_incl_add(v);
+    if (lane == kWave - 1) wsum[w] = incl;
+    __syncthreads();
+    const uint32_t ws = lane < kRefWaves ? wsum[lane] : 0u;
+    const uint32_t wincl = wave_incl_add(ws);
+    const uint32_t wbase = static_cast<uint32_t>(__shfl(static_cast<int>(wincl - ws), w));
+    tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wincl), kRefWaves - 1));
+    __syncthreads();
+    return wbase + incl - v;
+}
+
+// Index of the active range holding flat element e (o[j] <= e < o[j+1]), from a wave-uniform start j0
+// at most 5 ranges back (every span has >= 16 elements, a round of 64 lanes meets <= 5 of them).
+__device__ __forceinline__ int range_of(const uint32_t *o, int m, int j0, uint32_t e) {
+    int j = j0;
+    while (j + 1 < m && o[j + 1] <= e) ++j;
+    return j;
+}
+
+// First active range whose span holds flat element e (binary search, wave-uniform e).
+__device__ __forceinline__ int range_search(const uint32_t *o, int m, uint32_t e) {
+    int lo = 0, hi = m - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (o[mid] <= e) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Wave 0: the active prefix of the current list for window [fin, win_end) and the flat offsets of
+// the active ranges' partition spans.
+__device__ __forceinline__ void set_active(RefLds &L, uint32_t win_end) {
+    const int lane = lane_id();
+    const int c = L.cur, m = L.m_all;
+    uint32_t carry = 0;
+    int act = 0;
+    for (int b = 0; b < m; b += kWave) {
+        const int j = b + lane;
+        const bool in = j < m && L.r_lo[c][j] < win_end;
+        const uint64_t bal = ballot(in);
+        const uint32_t span = in ? L.r_hi[c][j] - L.r_lo[c][j] - 1u : 0u;
+        const uint32_t incl = wave_incl_add(span);
+        if (in) L.o[j] = carry + incl - span;
+        carry += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), kWave - 1));
+        act += popc64(bal);
+        if (bal != ~0ull) break;  // sorted list: the first range past the window ends the prefix
+    }
+    if (lane == 0) {
+        L.m_act = act;
+        L.o[act] = carry;
+        L.T = carry;
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortArgs r) {
+    static_assert(NT == kRefThreads, "k_select_reference runs 1024 threads");
+    __shared__ RefLds L;
+    const int f = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
+    const uint32_t st0 = a.status[f];
+    if (!(st0 & FD_FRAME_TIES) || (st0 & FD_FRAME_GUARD)) return;
+    const uint32_t n = static_cast<uint32_t>(min(static_cast<int64_t>(a.cand_n[f]), a.list_cap));
+    const int rows = a.rows, cols = a.cols, d = a.dist;
+    const uint32_t npx = static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols);
+    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    uint2 *X = r.x + static_cast<int64_t>(f) * r.cap;
+    uint32_t *lpos = r.lpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t *rpos = r.rpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t *ord = r.ord + static_cast<int64_t>(f) * r.cap;
+
+    // ---- 1. the push order -------------------------------------------------------------------------
+    if (r.push_order) {
+        for (uint32_t i = tid; i < n; i += NT) X[i] = make_uint2(__float_as_uint(lresp[i]), lidx[i]);
+    } else {
+        // raster order of unique pixel indices: bitmap (in lpos), word prefix (in rpos), rank = prefix +
+        // set bits below. The bitmap words are read with device-scope loads (the atomics bypass L1).
+        const uint32_t words = (npx + 31u) >> 5;
+        uint32_t *bits = lpos, *wpre = rpos;
+        for (uint32_t w = tid; w < words; w += NT) bits[w] = 0u;
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += NT) {
+            const uint32_t q = lidx[i];
+            if (q < npx) atomicOr(&bits[q >> 5], 1u << (q & 31u));
+        }
+        __syncthreads();
+        const uint32_t per = (words + NT - 1) / NT;
+        const uint32_t w0 = min(words, tid * per), w1 = min(words, w0 + per);
+        uint32_t cnt = 0;
+        for (uint32_t w = w0; w < w1; ++w)
+            cnt += __popc(__hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        uint32_t tot;
+        uint32_t base = block_excl(cnt, L.wsum, tot);
+        for (uint32_t w = w0; w < w1; ++w) {
+            wpre[w] = base;
+            base += __popc(__hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += NT) {
+            const uint32_t q = lidx[i];
+            if (q >= npx) continue;  // (guarded upstream: k_select trips FD_FRAME_GUARD)
+            const uint32_t bw = __hip_atomic_load(&bits[q >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t rk = wpre[q >> 5] + __popc(bw & ((1u << (q & 31u)) - 1u));
+            X[FD_REF_IDX(rk, n, 1)] = make_uint2(__float_as_uint(lresp[i]), q);
+        }
+    }
+
+    // ---- greedy state (k_select_ordered) --------------------------------------------------------------
+    const bool use_grid = d >= 1 || (d == 0 && a.grid_at_d0);
+    const int gw2 = a.grid_w + 2;
+    const int cells = gw2 * (a.grid_h + 2);
+    const bool grid_in_lds = cells <= kGridLdsCells;
+    uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
+    uint32_t *const grid = grid_in_lds ? L.grid_lds : grid_g;
+    const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
+    const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
+    const uint32_t s1 = static_cast<uint32_t>(d + 1);
+    if (use_grid)
+        for (int i = tid; i < cells; i += NT) grid[i] = grid_empty(rows, cols, d);
+    if (tid == 0) {
+        L.s_done = 0;
+        L.s_acc = 0;
+        L.tie_prev = 0;
+        L.tie_has_prev = 0;
+        L.fail = 0;
+        L.cur = 0;
+        L.n_leaf = 0;
+        L.fin = 0;
+        // __introsort_loop(0, n, 2 * __lg(n)); n <= 16: the final insertion sort alone (one leaf)
+        if (n > static_cast<uint32_t>(kRefLeaf)) {
+            L.r_lo[0][0] = 0;
+            L.r_hi[0][0] = n;
+            L.r_dep[0][0] = 2u * (31u - __clz(n));
+            L.m_all = 1;
+        } else {
+            L.m_all = 0;
+            if (n > 0) {
+                L.leaf_lo[0] = 0;
+                L.leaf_hi[0] = n;
+                L.n_leaf = 1;
+            }
+        }
+    }
+    __syncthreads();
+    if (wv == 0) set_active(L, kSelectChunk);
+    __syncthreads();
+
+    for (int guard = 0; guard < 1 << 16; ++guard) {  // windows x levels (bounded: each level halves)
+        const int m = L.m_act;
+        if (m > 0) {
+            // ---- one partition level over the active ranges ----------------------------------------------
+            const int c = L.cur;
+            if (tid < m) {
+                const uint32_t lo = L.r_lo[c][tid], hi = L.r_hi[c][tid];
+                if (L.r_dep[c][tid] == 0u) L.fail = 1;  // std::__partial_sort: not emulated
+                const uint32_t mid = lo + (hi - lo) / 2u;
+                const uint2 xa = X[FD_REF_IDX(lo + 1, n, 2)], xb = X[FD_REF_IDX(mid, n, 2)], xc = X[FD_REF_IDX(hi - 1, n, 2)];
+                const uint32_t ch = median_pos(as_f(xa.x), as_f(xb.x), as_f(xc.x), lo + 1, mid, hi - 1);
+                const uint2 xp = ch == lo + 1 ? xa : (ch == mid ? xb : xc);
+                const uint2 x0 = X[FD_REF_IDX(lo, n, 3)];
+                X[FD_REF_IDX(lo, n, 3)] = xp;
+                X[FD_REF_IDX(ch, n, 3)] = x0;
+                L.piv[tid] = as_f(xp.x);
+                L.K[tid] = 0;
+            }
+            __syncthreads();
+            if (L.fail) break;
+            const uint32_t T = L.T;
+            const uint32_t blk = ((T + kRefWaves * kWave - 1) / (kRefWaves * kWave)) * kWave;
+            const uint32_t e0 = min(T, wv * blk), e1 = min(T, e0 + blk);
+            // pass 1: stopper counts per wave, local prefixes at the range heads
+            {
+                uint32_t cl = 0, cr = 0;
+                int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
+                for (uint32_t b = e0; b < e1; b += kWave) {
+                    const uint32_t e = b + lane;
+                    const bool valid = e < e1;
+                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
+                    const uint32_t p = L.r_lo[c][j] + 1u + (e - L.o[j]);
+                    const float rv = valid ? as_f(X[FD_REF_IDX(p, n, 5)].x) : 0.0f;
+                    const float pv = L.piv[j];
+                    const bool ls = valid && rv <= pv, rs = valid && rv >= pv;
+                    const uint64_t bl = ballot(ls), br = ballot(rs);
+                    if (valid && e == L.o[j]) {
+                        L.headL[j] = cl + mbcnt64(bl, 0);
+                        L.headR[j] = cr + mbcnt64(br, 0);
+                        L.headW[j] = wv;
+                    }
+                    cl += popc64(bl);
+                    cr += popc64(br);
+                }
+                if (lane == 0) {
+                    L.waveL[wv] = cl;
+                    L.waveR[wv] = cr;
+                }
+            }
+            __syncthreads();
+            // per range: global stopper bases and counts
+            uint32_t wbL, wbR;  // exclusive wave prefixes, lane i = wave i
+            {
+                const uint32_t vl = lane < kRefWaves ? L.waveL[lane] : 0u, vr = lane < kRefWaves ? L.waveR[lane] : 0u;
+                wbL = wave_incl_add(vl) - vl;
+                wbR = wave_incl_add(vr) - vr;
+            }
+            const uint32_t totL = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wbL), kRefWaves - 1)) +
+                                  L.waveL[kRefWaves - 1];
+            const uint32_t totR = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wbR), kRefWaves - 1)) +
+                                  L.waveR[kRefWaves - 1];
+            {
+                // every wave computes its lanes' ranges (shuffles are per wave); ranges j = tid < m
+                const int j = tid < m ? tid : 0;
+                const int jn = j + 1;
+                const uint32_t hw = L.headW[j], hwn = jn < m ? L.headW[jn] : 0u;
+                const uint32_t bLj = static_cast<uint32_t>(__shfl(static_cast<int>(wbL), static_cast<int>(hw))) + L.headL[j];
+                const uint32_t bRj = static_cast<uint32_t>(__shfl(static_cast<int>(wbR), static_cast<int>(hw))) + L.headR[j];
+                // (shuffles with every lane active: ds_bpermute does not read inactive source lanes)
+                const uint32_t sLn = static_cast<uint32_t>(__shfl(static_cast<int>(wbL), static_cast<int>(hwn)));
+                const uint32_t sRn = static_cast<uint32_t>(__shfl(static_cast<int>(wbR), static_cast<int>(hwn)));
+                const uint32_t bLn = jn < m ? sLn + L.headL[jn] : totL;
+                const uint32_t bRn = jn < m ? sRn + L.headR[jn] : totR;
+                if (tid < m) {
+                    L.bL[tid] = bLj;
+                    L.nL[tid] = bLn - bLj;
+                    L.eR[tid] = bRn;
+                    L.nR[tid] = bRn - bRj;
+                }
+            }
+            __syncthreads();
+            // pass 2: scatter stopper positions by rank (left stoppers from the left, right from the right)
+            {
+                const uint32_t mywbL = static_cast<uint32_t>(__shfl(static_cast<int>(wbL), wv));
+                const uint32_t mywbR = static_cast<uint32_t>(__shfl(static_cast<int>(wbR), wv));
+                uint32_t cl = mywbL, cr = mywbR;
+                int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
+                for (uint32_t b = e0; b < e1; b += kWave) {
+                    const uint32_t e = b + lane;
+                    const bool valid = e < e1;
+                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
+                    const uint32_t oj = L.o[j];
+                    const uint32_t p = L.r_lo[c][j] + 1u + (e - oj);
+                    const float rv = valid ? as_f(X[FD_REF_IDX(p, n, 6)].x) : 0.0f;
+                    const float pv = L.piv[j];
+                    const bool ls = valid && rv <= pv, rs = valid && rv >= pv;
+                    const uint64_t bl = ballot(ls), br = ballot(rs);
+                    if (ls) {
+                        const uint32_t rankL = static_cast<uint32_t>(mbcnt64(bl, 0)) + cl - L.bL[j];  // 0-based
+                        lpos[FD_REF_IDX(oj + rankL, L.T, 7)] = p;
+                    }
+                    if (rs) {
+                        const uint32_t rankR = L.eR[j] - (static_cast<uint32_t>(mbcnt64(br, 0)) + cr) - 1u;  // 0-based from the right
+                        rpos[FD_REF_IDX(oj + rankR, L.T, 8)] = p;
+                    }
+                    cl += popc64(bl);
+                    cr += popc64(br);
+                }
+            }
+            __syncthreads();
+            // pass 3: K = number of pairs with l_k < r_k (monotone in k: the last true k writes it)
+            {
+                int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
+                for (uint32_t b = e0; b < e1; b += kWave) {
+                    const uint32_t e = b + lane;
+                    const bool valid = e < e1;
+                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
+                    const uint32_t k = e - L.o[j];  // 0-based pair index
+                    const uint32_t mn = min(L.nL[j], L.nR[j]);
+                    const bool t = valid && k < mn && lpos[FD_REF_IDX(e, L.T, 9)] < rpos[FD_REF_IDX(e, L.T, 9)];
+                    const bool tn = t && k + 1 < mn && lpos[FD_REF_IDX(e + 1, L.T, 10)] < rpos[FD_REF_IDX(e + 1, L.T, 10)];
+                    if (t && !tn) L.K[j] = k + 1;
+                }
+            }
+            __syncthreads();
+            // pass 4: the swaps; the cuts
+            {
+                int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
+                for (uint32_t b = e0; b < e1; b += kWave) {
+                    const uint32_t e = b + lane;
+                    const bool valid = e < e1;
+                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
+                    const uint32_t k = e - L.o[j];
+                    if (valid && k < L.K[j]) {
+                        const uint32_t pl = FD_REF_IDX(lpos[FD_REF_IDX(e, L.T, 11)], n, 12), pr = FD_REF_IDX(rpos[FD_REF_IDX(e, L.T, 11)], n, 13);
+                        const uint2 vl = X[pl], vr = X[pr];
+                        X[pl] = vr;
+                        X[pr] = vl;
+                    }
+                }
+                if (tid < m) {
+                    const uint32_t K = L.K[tid], oj = L.o[tid];
+                    uint32_t cut = kNoPos;
+                    if (K < L.nL[tid]) cut = lpos[FD_REF_IDX(oj + K, L.T, 14)];
+                    if (K >= 1u) cut = min(cut, rpos[FD_REF_IDX(oj + K - 1u, L.T, 15)]);
+                    L.cut[tid] = cut;
+                }
+            }
+            __syncthreads();
+            // children: ranges > 16 into the next list (in order), the rest are leaves
+            if (wv == 0) {
+                const int nc = c ^ 1;
+                uint32_t w_at = 0, l_at = 0;
+                for (int b = 0; b < m; b += kWave) {
+                    const int j = b + lane;
+                    const bool in = j < m;
+                    uint32_t lo = 0, hi = 0, ct = 0, dp = 0;
+                    if (in) {
+                        lo = L.r_lo[c][j];
+                        hi = L.r_hi[c][j];
+                        ct = L.cut[j];
+                        dp = L.r_dep[c][j] - 1u;
+                        if (ct <= lo || ct >= hi) {  // (cannot happen: the scans stop inside the range)
+                            L.fail = 2;
+                            ct = lo + 1;
+                        }
+                    }
+                    const bool bigL = in && ct - lo > static_cast<uint32_t>(kRefLeaf);
+                    const bool bigR = in && hi - ct > static_cast<uint32_t>(kRefLeaf);
+                    const uint32_t nb = (bigL ? 1u : 0u) + (bigR ? 1u : 0u);
+                    const uint32_t nlf = in ? 2u - nb : 0u;
+                    const uint32_t ib = wave_incl_add(nb), il = wave_incl_add(nlf);
+                    uint32_t pb = w_at + ib - nb, pl = l_at + il - nlf;
+                    if (bigL && pb < kRefMaxRanges) {
+                        L.r_lo[nc][pb] = lo;
+                        L.r_hi[nc][pb] = ct;
+                        L.r_dep[nc][pb] = dp;
+                    }
+                    if (bigL) ++pb;
+                    if (bigR && pb < kRefMaxRanges) {
+                        L.r_lo[nc][pb] = ct;
+                        L.r_hi[nc][pb] = hi;
+                        L.r_dep[nc][pb] = dp;
+                    }
+                    if (in && !bigL) {
+                        L.leaf_lo[pl] = lo;
+                        L.leaf_hi[pl] = ct;
+                        ++pl;
+                    }
+                    if (in && !bigR) {
+                        L.leaf_lo[pl] = ct;
+                        L.leaf_hi[pl] = hi;
+                    }
+                    w_at += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ib), kWave - 1));
+                    l_at += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(il), kWave - 1));
+                }
+                // the ranges right of the window follow unchanged
+                const int rest = L.m_all - m;
+                for (int i = lane; i < rest; i += kWave) {
+                    const uint32_t q = w_at + static_cast<uint32_t>(i);
+                    if (q < kRefMaxRanges) {
+                        L.r_lo[nc][q] = L.r_lo[c][m + i];
+                        L.r_hi[nc][q] = L.r_hi[c][m + i];
+                        L.r_dep[nc][q] = L.r_dep[c][m + i];
+                    }
+                }
+                if (lane == 0) {
+                    const uint32_t tot = w_at + static_cast<uint32_t>(rest);
+                    if (tot > kRefMaxRanges) L.fail = 3;
+                    L.m_all = static_cast<int>(min(tot, static_cast<uint32_t>(kRefMaxRanges)));
+                    L.cur = nc;
+                    L.n_leaf = static_cast<int>(l_at);
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+                set_active(L, L.fin + kSelectChunk);
+            }
+            __syncthreads();
+            if (L.fail) break;
+        }
+        // ---- leaves: the final insertion sort (stable, response descending) into the visiting order ---
+        if (tid < L.n_leaf) {
+            const uint32_t lo = L.leaf_lo[tid], hi = L.leaf_hi[tid];
+            const int len = min(static_cast<int>(hi - lo), kRefLeaf);
+            uint2 v[kRefLeaf];
+#pragma unroll
+            for (int i = 0; i < kRefLeaf; ++i) v[i] = i < len ? X[FD_REF_IDX(lo + i, n, 16)] : make_uint2(0u, 0u);
+#pragma unroll
+            for (int i = 0; i < kRefLeaf; ++i) {
+                const float ri = as_f(v[i].x);
+                uint32_t rk = 0;
+#pragma unroll
+                for (int q = 0; q < kRefLeaf; ++q) {
+                    const float rq = as_f(v[q].x);
+                    rk += (q < len && (rq > ri || (rq == ri && q < i))) ? 1u : 0u;
+                }
+                if (i < len) ord[FD_REF_IDX(lo + rk, n, 17)] = v[i].y;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) L.n_leaf = 0;
+        if (L.m_act > 0) {
+            __syncthreads();
+            continue;
+        }
+        // ---- window final: greedy over [fin, fin_new) -------------------------------------------------
+        const uint32_t fin = L.fin;
+        const uint32_t fin_new = L.m_all > 0 ? L.r_lo[L.cur][0] : n;
+        for (uint32_t base = fin; base < fin_new; base += kSelectChunk) {
+            if (L.s_done) break;
+            const int cn = static_cast<int>(min(static_cast<uint32_t>(kSelectChunk), fin_new - base));
+            for (int i = tid; i < cn; i += NT) {
+                uint32_t idx = ord[FD_REF_IDX(base + i, n, 18)];
+                bool ok = true;
+                if (idx >= npx) {  // consistency guard
+                    ok = false;
+                    idx = 0;
+                    atomicOr(&a.status[f], 0x80000000u);
+                }
+                const uint32_t y = idx / static_cast<uint32_t>(cols), x = idx - y * static_cast<uint32_t>(cols);
+                if (fmask) ok = ok && ((fmask[static_cast<int64_t>(y) * a.mask_wpr + (x >> 5)] >> (x & 31)) & 1u);
+                L.pxy[i] = ok ? ((y << 16) | x) : kEmpty;
+                if (use_grid) L.pcell[i] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
+            }
+            __syncthreads();
+            if (use_grid) conflict_masks(L.pxy, cn, d, rows, cols, L.cmask, tid, NT);
+            __syncthreads();
+            if (tid < kWave) {
+                if (!use_grid)
+                    greedy_chunk<0>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
+                                    0u, 0u, L.tie_prev, L.tie_has_prev);
+                else if (grid_in_lds)
+                    greedy_chunk<1>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
+                                    0u, 0u, L.tie_prev, L.tie_has_prev);
+                else
+                    greedy_chunk<2>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
+                                    0u, 0u, L.tie_prev, L.tie_has_prev);
+            }
+            __syncthreads();
+        }
+        if (L.s_done || fin_new >= n) break;
+        if (wv == 0) {
+            if (lane == 0) L.fin = fin_new;
+            __builtin_amdgcn_s_waitcnt(0);
+            set_active(L, fin_new + kSelectChunk);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (L.fail) {
+            atomicOr(&a.status[f], FD_FRAME_UNRESOLVED);
+        } else {
+            a.out_counts[f] = L.s_acc;
+            atomicOr(&a.status[f], FD_FRAME_RESOLVED);
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r, int batch, hipStream_t s) {
+    if (batch <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_select_reference<kRefThreads>, dim3(static_cast<unsigned>(batch)), dim3(kRefThreads), 0, s, a, r);
+    return hipGetLastError();
+}
+
+}  // namespace fdk

@@ -19,7 +19,7 @@ from ._lib import FD_FAST, FD_HARRIS, FD_SHI_TOMASI, fd_point_opts
 KINDS = {"harris": FD_HARRIS, "shi_tomasi": FD_SHI_TOMASI, "fast": FD_FAST}
 # order of equal responses in the selection (include/fd_hip.h fd_ctx_set_tie_order)
 TIES = {"raster": 0, "reference": 1}
-FRAME_TIES, FRAME_RESOLVED, FRAME_VALUE_RANGE, FRAME_GUARD = 0x1, 0x2, 0x40000000, 0xBE000000
+FRAME_TIES, FRAME_RESOLVED, FRAME_UNRESOLVED, FRAME_VALUE_RANGE, FRAME_GUARD = 0x1, 0x2, 0x4, 0x40000000, 0xBE000000
 
 _ctx_lock = threading.Lock()
 _contexts: dict[int, "Context"] = {}
@@ -183,8 +183,9 @@ class DetectResult:
         return st.astype(np.uint32)
 
     def check(self) -> "DetectResult":
-        """Raise if a frame tripped an internal guard (device results carry no flags in their counts)."""
-        bad = np.nonzero(self.frame_flags() & np.uint32(FRAME_GUARD | FRAME_VALUE_RANGE))[0]
+        """Raise if a frame tripped an internal guard, or was left unresolved in the reference tie order
+        (FRAME_UNRESOLVED: device results carry no flags in their counts)."""
+        bad = np.nonzero(self.frame_flags() & np.uint32(FRAME_GUARD | FRAME_VALUE_RANGE | FRAME_UNRESOLVED))[0]
         if len(bad):
             raise _lib.FdError(_lib.FD_ERR_HIP, f"selection flags 0x{int(self.frame_flags()[bad[0]]):x} on frame {bad[0]}")
         return self
@@ -196,11 +197,11 @@ def detect_points(kind, frames, need: int, min_feature_distance: int = 15, min_v
 
     Returns the NEW features per frame (x, y), in selection order, and the per-frame status words.
     ties="reference": frames whose greedy scan meets equal responses are re-selected in the
-    reference's std::sort order, so every frame equals the reference's DetectGoodFeatures; the call
-    synchronises the stream once (a status read), so it cannot run under graph capture (the library
-    refuses it there). ties="raster": equal responses by raster index, fully asynchronous and
-    graph-capturable; identical to "reference" wherever no tie reaches the scan, and FD_FRAME_TIES in
-    the status words marks the frames where one did. Default (None): "reference" for host frames
+    reference's std::sort order (libstdc++'s introsort emulated on the GPU, k_select_reference), so
+    every frame equals the reference's DetectGoodFeatures; asynchronous and graph-capturable once the
+    workspace exists (one call of the shape first). ties="raster": equal responses by raster index;
+    identical to "reference" wherever no tie reaches the scan, and FD_FRAME_TIES in the status words
+    marks the frames where one did. Default (None): "reference" for host frames
     (the reference API's semantics), "raster" for torch device frames (asynchronous; check
     `frame_flags() & FRAME_TIES` or pass ties="reference" to get the reference order there too).
     With torch device frames the outputs are device tensors (on the current stream); `out` may pass

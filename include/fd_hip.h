@@ -71,10 +71,14 @@ int fd_ctx_reserve(fd_ctx *ctx, int kind, int batch, int rows, int cols, int64_t
  *   FD_TIES_RASTER     (default) response descending, equal responses by raster index ascending: a
  *                      total order, fully asynchronous and graph-capturable.
  *   FD_TIES_REFERENCE  the reference's own permutation: every frame whose greedy scan meets two equal
- *                      responses (FD_FRAME_TIES) is re-selected in the order libstdc++'s std::sort
- *                      leaves the raster-ordered candidates in (the sort runs on the host, the greedy
- *                      selection again on the GPU). Frames without such a tie are identical in both
- *                      modes. Each selection call then synchronises its stream once to read the flags.
+ *                      responses (FD_FRAME_TIES) is re-selected, on the GPU, in the order libstdc++'s
+ *                      (GCC 11) std::sort leaves the raster-ordered candidates in (its introsort is
+ *                      emulated over the visited prefix; FD_FRAME_RESOLVED). Frames without such a tie
+ *                      are identical in both modes. Asynchronous and graph-capturable (reserve first,
+ *                      fd_ctx_reserve after fd_ctx_set_tie_order). If the sort would reach its depth limit
+ *                      (heapsort) inside the visited prefix, the frame gets FD_FRAME_UNRESOLVED instead:
+ *                      host-output calls then resolve it on the host; device-output calls leave its
+ *                      features undefined and the flag in fd_ctx_frame_status.
  * SuperPoint's fd_nn_select has a defined order (std::multimap) and ignores this setting.
  */
 enum fd_tie_order { FD_TIES_RASTER = 0, FD_TIES_REFERENCE = 1 };
@@ -88,6 +92,7 @@ int fd_ctx_set_tie_order(fd_ctx *ctx, int order);
  */
 #define FD_FRAME_TIES 0x00000001u       /* equal responses met in the greedy scan (order defined by the mode) */
 #define FD_FRAME_RESOLVED 0x00000002u   /* re-selected in the reference's std::sort order (FD_TIES_REFERENCE) */
+#define FD_FRAME_UNRESOLVED 0x00000004u /* FD_TIES_REFERENCE: not emulated on the GPU (see fd_tie_order) */
 #define FD_FRAME_VALUE_RANGE 0x40000000u /* fd_nn_select: a heatmap value above fd_nn_opts::max_response */
 #define FD_FRAME_GUARD 0xBE000000u      /* internal consistency guard tripped (host-output calls fail FD_ERR_HIP) */
 int fd_ctx_frame_status(fd_ctx *ctx, uint32_t *dst, int batch, int async);

@@ -3,11 +3,13 @@
 // MI355X kernels of libfdhip.so through the C ABI in include/fd_hip.h.
 //
 // DetectGoodFeatures keeps the reference's template method (feature_point_detector.cpp:7-25): mask,
-// ComputeCandidates, SelectGoodFeatures. For the built-in detectors (KindId() >= 0) the three run
-// fused on the GPU (fd_points_detect). A subclass that supplies its own candidates overrides
-// ComputeCandidates (pushing (response, pixel) pairs into candidates(), as the reference's subclasses
-// do) and leaves KindId() at kOwnCandidates; its candidates are then selected on the GPU by
-// fd_points_select. candidates() and mask() are materialised on first access after a call:
+// the pure virtual ComputeCandidates, SelectGoodFeatures. It always calls ComputeCandidates, as the
+// reference does (:20). The built-in detectors' ComputeCandidates only marks the call for the fused GPU
+// path (DeferCandidatesToGpu), after which mask, candidates and selection run as one fd_points_detect.
+// Any other ComputeCandidates -- a direct subclass of FeaturePointDetector, or a subclass of a
+// built-in detector that overrides it -- pushes (response, pixel) pairs into candidates(), as the
+// reference's subclasses do, and those are selected on the GPU by fd_points_select.
+// candidates() and mask() are materialised on first access after a call:
 // candidates() holds the candidates sorted with the reference's std::sort comparator
 // (feature_point_detector.cpp:58-60), exactly what the reference leaves there (the built-in detectors
 // recompute them on the GPU for that). mask() may be read inside ComputeCandidates (prior boxes,
@@ -65,20 +67,20 @@ public:
     const std::string &last_error() const { return error_; }
 
 protected:
-    // libfdhip detector kind (FD_HARRIS / FD_SHI_TOMASI / FD_FAST): the fused GPU path. The default,
-    // kOwnCandidates, makes DetectGoodFeatures call ComputeCandidates (a subclass of a built-in
-    // detector that overrides ComputeCandidates overrides this too).
-    static constexpr int kOwnCandidates = -1;
-    virtual int KindId() const { return kOwnCandidates; }
+    // For the built-in detectors' ComputeCandidates: instead of pushing candidates, hand the whole
+    // call to the fused GPU path for libfdhip detector kind `kind` (FD_HARRIS / FD_SHI_TOMASI /
+    // FD_FAST). Valid only inside DetectGoodFeatures; returns true.
+    bool DeferCandidatesToGpu(int kind);
     fd_ctx *Context();
     bool Fail(const std::string &what);
 
 private:
     // The ComputeCandidates seam (feature_point_detector.h:44, called at feature_point_detector.cpp:20):
-    // push the image's candidates into candidates() (already cleared). The default serves the
-    // built-in kinds: the raster-ordered candidates of the frame staged by the last call.
-    virtual bool ComputeCandidates(const GrayImage &image);
-    bool DetectWithOwnCandidates(const GrayImage &image, uint32_t needed_feature_num, std::vector<Vec2> &features);
+    // push the image's candidates into candidates() (already cleared), or DeferCandidatesToGpu.
+    virtual bool ComputeCandidates(const GrayImage &image) = 0;
+    bool DetectFused(const GrayImage &image, int kind, uint32_t needed_feature_num, std::vector<Vec2> &features);
+    bool SelectOwnCandidates(uint32_t needed_feature_num, std::vector<Vec2> &features);
+    bool FetchCandidates();
     void Materialise() const;
 
 private:
@@ -89,6 +91,8 @@ private:
     mutable bool candidates_valid_ = true;
     mutable bool candidates_sorted_ = true;  // own candidates: sorted (:58-60) on first access
     mutable bool mask_valid_ = true;
+    bool in_detect_ = false;     // inside DetectGoodFeatures' ComputeCandidates call
+    int fused_kind_ = -1;        // kind of the last call's fused GPU path, -1 = own candidates
     const uint8_t *staged_frame_ = nullptr;  // device copy of the last image (owned by the context)
     int32_t last_rows_ = 0, last_cols_ = 0;
     Options last_options_;
@@ -113,8 +117,8 @@ public:
     virtual ~FeaturePointHarrisDetector() = default;
     virtual std::string DetectorTypeName() const override { return "Harris"; }
 
-protected:
-    virtual int KindId() const override;
+private:
+    virtual bool ComputeCandidates(const GrayImage &image) override;
 
 private:
     SubOptions sub_options_;
@@ -132,8 +136,8 @@ public:
     virtual ~FeaturePointShiTomasDetector() = default;
     virtual std::string DetectorTypeName() const override { return "Shi-Tomas"; }
 
-protected:
-    virtual int KindId() const override;
+private:
+    virtual bool ComputeCandidates(const GrayImage &image) override;
 
 private:
     SubOptions sub_options_;
@@ -152,8 +156,8 @@ public:
     virtual ~FeaturePointFastDetector() = default;
     virtual std::string DetectorTypeName() const override { return "Fast"; }
 
-protected:
-    virtual int KindId() const override;
+private:
+    virtual bool ComputeCandidates(const GrayImage &image) override;
 
 private:
     SubOptions sub_options_;

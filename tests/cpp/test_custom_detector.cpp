@@ -2,20 +2,28 @@
 // feature_point_detector.h:44): the drop-in base class calls it from DetectGoodFeatures and selects
 // its candidates on the GPU (fd_points_select). The candidates here are integer gradient magnitudes
 // (many equal responses, so the reference's std::sort order of the pushed sequence decides).
-//   usage: fd_demo_custom <raw u8 gray file> <rows> <cols> <order> <dist> <need> [prior]
+//   usage: fd_demo_custom <raw u8 gray file> <rows> <cols> <order> <dist> <need> [prior] [base]
 //     order: raster | reverse | twice (every candidate pushed twice, the copy right after it)
 //     prior: 1 = the demo's 9x9 lattice of prior features (test_feature_point_detector.cpp:52-55)
+//     base:  plain (default: derives from FeaturePointDetector) | harris (derives from
+//            FeaturePointHarrisDetector and overrides only ComputeCandidates, the NVI extension point of
+//            feature_point_harris_detector.h:24: its override must be the one that runs)
 // Prints one JSON object: ok, the new features, the candidate count and the first 64 of candidates().
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "feature_detector/feature_point_detector.h"
 
 using namespace feature_detector;
 
-class FeaturePointGradientDetector : public FeaturePointDetector {
+// as in the reference, the base class is abstract (pure virtual ComputeCandidates, feature_point_detector.h:44)
+static_assert(std::is_abstract<FeaturePointDetector>::value, "FeaturePointDetector must stay abstract");
+
+template <typename Base>
+class FeaturePointGradientDetector : public Base {
 public:
     explicit FeaturePointGradientDetector(std::string order) : order_(std::move(order)) {}
     std::string DetectorTypeName() const override { return "Gradient"; }
@@ -27,7 +35,7 @@ private:
         const int32_t rows = image.rows(), cols = image.cols();
         const uint8_t *p = image.data();
         // the prior mask is readable here, as in the reference (mask_ is set before :20)
-        const MatInt &m = mask();
+        const MatInt &m = this->mask();
         if (m.rows() != rows || m.cols() != cols) return false;
         std::vector<std::pair<float, Pixel>> found;
         for (int32_t r = 1; r < rows - 1; ++r) {
@@ -35,10 +43,10 @@ private:
                 const int gx = std::abs(p[r * cols + c + 1] - p[r * cols + c - 1]);
                 const int gy = std::abs(p[(r + 1) * cols + c] - p[(r - 1) * cols + c]);
                 const float v = static_cast<float>(gx + gy);
-                if (v > options().kMinValidResponse) found.emplace_back(v, Pixel(c, r));
+                if (v > this->options().kMinValidResponse) found.emplace_back(v, Pixel(c, r));
             }
         }
-        auto &out = candidates();
+        auto &out = this->candidates();
         if (order_ == "reverse") {
             for (auto it = found.rbegin(); it != found.rend(); ++it) out.emplace_back(*it);
         } else {
@@ -53,25 +61,9 @@ private:
     std::string order_;
 };
 
-int main(int argc, char **argv) {
-    if (argc < 7) {
-        std::fprintf(stderr, "usage: %s <raw u8 file> <rows> <cols> <order> <dist> <need> [prior]\n", argv[0]);
-        return 2;
-    }
-    const int rows = std::atoi(argv[2]), cols = std::atoi(argv[3]);
-    const int dist = std::atoi(argv[5]), need = std::atoi(argv[6]);
-    const bool prior = argc > 7 && std::atoi(argv[7]) != 0;
-    std::vector<uint8_t> buf(static_cast<size_t>(rows) * cols);
-    FILE *f = std::fopen(argv[1], "rb");
-    if (!f || std::fread(buf.data(), 1, buf.size(), f) != buf.size()) {
-        std::fprintf(stderr, "cannot read %s\n", argv[1]);
-        return 2;
-    }
-    std::fclose(f);
-    GrayImage image;
-    image.SetImage(buf.data(), rows, cols, false);
-
-    FeaturePointGradientDetector detector(argv[4]);
+template <typename Base>
+int Run(const GrayImage &image, const char *order, int dist, int need, bool prior) {
+    FeaturePointGradientDetector<Base> detector(order);
     detector.options().kMinFeatureDistance = dist;
     detector.options().kMinValidResponse = 40.0f;
     std::vector<Vec2> features;
@@ -93,4 +85,27 @@ int main(int argc, char **argv) {
     for (size_t i = 0; i < m.size(); ++i) zeros += m.data()[i] == 0;
     std::printf("], \"mask_zeros\": %ld}\n", zeros);
     return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 7) {
+        std::fprintf(stderr, "usage: %s <raw u8 file> <rows> <cols> <order> <dist> <need> [prior] [plain|harris]\n", argv[0]);
+        return 2;
+    }
+    const int rows = std::atoi(argv[2]), cols = std::atoi(argv[3]);
+    const int dist = std::atoi(argv[5]), need = std::atoi(argv[6]);
+    const bool prior = argc > 7 && std::atoi(argv[7]) != 0;
+    std::vector<uint8_t> buf(static_cast<size_t>(rows) * cols);
+    FILE *f = std::fopen(argv[1], "rb");
+    if (!f || std::fread(buf.data(), 1, buf.size(), f) != buf.size()) {
+        std::fprintf(stderr, "cannot read %s\n", argv[1]);
+        return 2;
+    }
+    std::fclose(f);
+    GrayImage image;
+    image.SetImage(buf.data(), rows, cols, false);
+
+    const bool harris = argc > 8 && std::string(argv[8]) == "harris";
+    return harris ? Run<FeaturePointHarrisDetector>(image, argv[4], dist, need, prior)
+                  : Run<FeaturePointDetector>(image, argv[4], dist, need, prior);
 }

@@ -134,15 +134,19 @@ def test_descriptor_demo_matches_oracle(tmp_path, image_png, oracle, sampler):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("order,dist,prior", [("raster", 20, 0), ("reverse", 20, 1), ("twice", 0, 0), ("reverse", 1, 0)])
-def test_custom_subclass_candidates(tmp_path, image_png, oracle, order, dist, prior):
-    """A FeaturePointDetector subclass with its own ComputeCandidates (tests/cpp/test_custom_detector.cpp):
-    DetectGoodFeatures calls it once and selects its candidates on the GPU in the reference's order;
-    candidates() and mask() afterwards hold what the reference leaves there."""
+@pytest.mark.parametrize("order,dist,prior,base", [("raster", 20, 0, "plain"), ("reverse", 20, 1, "plain"),
+                                                    ("twice", 0, 0, "plain"), ("reverse", 1, 0, "plain"),
+                                                    ("raster", 20, 0, "harris"), ("reverse", 20, 1, "harris")])
+def test_custom_subclass_candidates(tmp_path, image_png, oracle, order, dist, prior, base):
+    """A subclass with its own ComputeCandidates (tests/cpp/test_custom_detector.cpp), deriving from
+    FeaturePointDetector or from FeaturePointHarrisDetector (overriding only ComputeCandidates, the NVI
+    extension point of feature_point_harris_detector.h:24): DetectGoodFeatures calls the override once
+    and selects its candidates on the GPU in the reference's order; candidates() and mask() afterwards
+    hold what the reference leaves there."""
     from test_gpu_select_custom import PRIOR, gradient_candidates
 
     _build()
-    r = _run("fd_demo_custom", image_png, tmp_path, order, dist, 300, prior)[0]
+    r = _run("fd_demo_custom", image_png, tmp_path, order, dist, 300, prior, base)[0]
     assert r["ok"] is True and r["calls"] == 1
     rr, xx, yy = gradient_candidates(image_png, order=order)
     pr = PRIOR if prior else None

@@ -259,6 +259,31 @@ def test_point_response_and_append(fd, oracle, name):
         fd.point_response(name, dev, THR[name], append=True)
 
 
+def test_point_response_huge_capacity(fd, oracle):
+    """cand_cap >= 2^30 on a launch large enough for the lane-wide kernel (1024x2048, 2^21 px): the
+    library must not address the caller's list through a 32-bit buffer range (2^30 * 4 B wraps to 0);
+    the list still equals the oracle's candidate set. 8 GiB of HBM for the two list arrays."""
+    torch = pytest.importorskip("torch")
+    img = oracle.make_frame("noise", 77, 1024, 2048)
+    dev = torch.from_numpy(np.ascontiguousarray(img[None])).cuda()
+    cap = 1 << 30
+    out = (torch.empty((1, cap), dtype=torch.float32, device="cuda"),
+           torch.empty((1, cap), dtype=torch.int32, device="cuda"),
+           torch.empty((1,), dtype=torch.int32, device="cuda"))
+    resp, idx, cnt = fd.point_response("shi_tomasi", dev, THR["shi_tomasi"], out=out)
+    torch.cuda.synchronize()
+    n = int(cnt.cpu()[0])
+    er, ex, ey = oracle_candidates(oracle, "shi_tomasi", img, THR["shi_tomasi"])
+    assert n == len(er)
+    gi = idx[0, :n].cpu().numpy().astype(np.int64)
+    gr = resp[0, :n].cpu().numpy()
+    o = np.argsort(gi, kind="stable")
+    assert np.array_equal(gi[o], ey.astype(np.int64) * 2048 + ex)
+    assert np.array_equal(gr[o].view(np.uint32), er.view(np.uint32))
+    del out, resp, idx
+    torch.cuda.empty_cache()
+
+
 def test_sqrt_rsq_exhaustive():
     # The Shi-Tomasi kernel's sqrt (fd_device.h sqrt_rn_rsq2: v_rsq_f32 + one Newton step) equals the
     # correctly rounded sqrt on every float of its domain ({0} U [2^-60, FLT_MAX], ~1.6e9 values).

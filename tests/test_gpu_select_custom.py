@@ -62,6 +62,45 @@ def test_custom_lists_with_ties(fd, oracle, image_png, order, dist):
             res = fd.select_points([(r, x, y)], rows, cols, need, dist, prior=pr, ties=ties)
             exp = oracle.select(r, x, y, rows, cols, dist, need, prior, sort_mode=sm)
             assert np.array_equal(res.features(0), exp), (ties, prior is None)
+            if ties == "reference":  # device lists: the GPU emulation alone (no host fallback behind it)
+                dres = fd.select_points(_dev_lists([(r, x, y)]), rows, cols, need, dist, prior=pr, ties=ties)
+                assert np.array_equal(dres.check().features(0), exp), ("device", prior is None)
+
+
+def _dev_lists(lists):
+    import torch
+
+    cap = max(max(len(l[0]) for l in lists), 1)
+    t = [torch.zeros((len(lists), cap), dtype=dt) for dt in (torch.float32, torch.int32, torch.int32)]
+    for i, l in enumerate(lists):
+        for k in range(3):
+            t[k][i, :len(l[k])] = torch.from_numpy(np.ascontiguousarray(l[k]))
+    counts = torch.tensor([len(l[0]) for l in lists], dtype=torch.int64)
+    return tuple(x.cuda() for x in (*t, counts))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_reference_order_emulation_stress(fd, oracle, seed):
+    """libstdc++'s introsort emulated on the GPU (k_select_reference) on lists with heavy ties: sizes
+    around the 16-element threshold and up to 60k, responses from small integer sets (most comparisons
+    meet equal keys) or continuous, needs that stop in the first window or run through several (dist 0:
+    every visited candidate is kept), with and without the occupancy grid. Device lists, so the GPU
+    result stands alone; against the oracle's std::sort (sort_mode 0)."""
+    rng = np.random.default_rng(seed)
+    rows, cols = 480, 640
+    sizes = [0, 1, 2, 15, 16, 17, 18, 33, 300, 2047, 2049, 5000, 60000]
+    lists, needs = [], []
+    for n in sizes:
+        k = int(rng.integers(1, 40))
+        r = (rng.integers(0, k, n).astype(np.float32) if seed % 2 == 0 else rng.standard_normal(n).astype(np.float32))
+        idx = rng.permutation(rows * cols)[:n]
+        lists.append((r, (idx % cols).astype(np.int32), (idx // cols).astype(np.int32)))
+    for dist, need in ((0, 5000), (0, 37), (3, 700), (20, 200)):
+        res = fd.select_points(_dev_lists(lists), rows, cols, need, dist, ties="reference")
+        res.check()
+        for b, (r, x, y) in enumerate(lists):
+            exp = oracle.select(r, x, y, rows, cols, dist, need, None, sort_mode=0)
+            assert np.array_equal(res.features(b), exp), (sizes[b], dist, need)
 
 
 def test_batch_device_lists(fd, oracle):

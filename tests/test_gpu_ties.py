@@ -30,7 +30,15 @@ def _both(fd, oracle, name, frames, need, dist, prior=None):
     ref = fd.detect_points(name, frames, need, dist, THR[name], prior=prior)
     ras = fd.detect_points(name, frames, need, dist, THR[name], prior=prior, ties="raster")
     flags = ref.frame_flags()
+    # device frames and outputs: no host fallback behind the GPU emulation (FRAME_UNRESOLVED would raise)
+    import torch
+
+    dev = fd.detect_points(name, torch.from_numpy(np.ascontiguousarray(frames)).cuda(), need, dist, THR[name],
+                           prior=prior, ties="reference")
+    torch.cuda.synchronize()
+    dev.check()
     for b in range(frames.shape[0]):
+        np.testing.assert_array_equal(dev.features(b), ref.features(b), err_msg=f"{name} frame {b} device path")
         p = None if prior is None else prior[b]
         e0 = oracle.detect(KIND[name], frames[b], dist, THR[name], need, p, sort_mode=0)[0]
         e1 = oracle.detect(KIND[name], frames[b], dist, THR[name], need, p, sort_mode=1)[0]
@@ -93,25 +101,34 @@ def test_device_frames_reference_order(fd, oracle):
         np.testing.assert_array_equal(ras.features(b), oracle.detect(1, host[b], 20, 40.0, 200, sort_mode=1)[0])
 
 
-def test_reference_order_refused_under_graph_capture(fd, oracle):
-    """ties="reference" synchronises the stream (status read + host sort): under hipGraph capture the
-    library refuses it with FD_ERR_INVALID before touching the capture; raster order captures fine."""
+def test_reference_order_under_graph_capture(fd, oracle):
+    """ties="reference" runs on the GPU (k_select_reference, no host round trip): it captures into a
+    hipGraph once its workspace exists, and every replay gives the oracle's std::sort order."""
     torch = pytest.importorskip("torch")
-    dev = torch.from_numpy(oracle.make_frame("noise", 5, 480, 640)[None].copy()).cuda()
-    xy = torch.empty((1, 201, 2), dtype=torch.float32, device="cuda")
-    cnt = torch.empty((1,), dtype=torch.int32, device="cuda")
-    fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt))  # warm (workspace sized outside capture)
+    host = np.stack([make_tie_frame(oracle, seed=s) for s in (11, 12)])
+    dev = torch.from_numpy(host).cuda()
+    xy = torch.empty((2, 201, 2), dtype=torch.float32, device="cuda")
+    cnt = torch.empty((2,), dtype=torch.int32, device="cuda")
+    fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt), ties="reference")  # sizes the workspace
     torch.cuda.synchronize()
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
-    with pytest.raises(fd.FdError):
-        with torch.cuda.graph(g, stream=s):
-            fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt), ties="reference")
-    torch.cuda.synchronize()
-    g2 = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g2, stream=s):
-        fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt))
-    g2.replay()
-    torch.cuda.synchronize()
-    exp = oracle.detect(0, dev[0].cpu().numpy(), 20, 30.0, 200, sort_mode=1)[0]
-    np.testing.assert_array_equal(xy[0, :int(cnt[0])].cpu().numpy(), exp)
+    with torch.cuda.graph(g, stream=s):
+        fd.detect_points("harris", dev, 200, 20, 30.0, out=(xy, cnt), ties="reference")
+    for rep in range(3):
+        xy.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        for b in range(2):
+            exp = oracle.detect(0, host[b], 20, 30.0, 200, sort_mode=0)[0]
+            np.testing.assert_array_equal(xy[b, :int(cnt[b])].cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("name", ["harris", "shi_tomasi"])
+def test_tie_frames_1080p_batch(fd, oracle, name):
+    """The north-star frame size in the reference order: a batch of 1080p tie frames (list-mode
+    selection, ~100k+ candidates per frame partitioned on the GPU) next to plain noise frames."""
+    frames = np.stack([make_tie_frame(oracle, 1080, 1920, seed=40 + i, copies=(9, 14)) if i % 2 == 0 else
+                       oracle.make_frame("noise", 40 + i, 1080, 1920) for i in range(4)])
+    _both(fd, oracle, name, frames, 200, 20)
