@@ -426,14 +426,22 @@ def _line_threads():
     return int(os.environ.get("FD_LINE_THREADS", n))
 
 
-def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5, line_reps=3):
+def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5, line_reps=3, global_batch=None,
+            barrier=None, max_fn=None):
     """BASELINE configs[3]: LSD level-line map (norm, angle, valid + column-major valid list) on
-    structured 64-px checker frames, all on the device (the host region growing is not timed)."""
+    structured 64-px checker frames, all on the device (the host region growing is not timed).
+
+    Strong scaling: this rank's contiguous block (`batch` frames) of the global 256-frame batch. With
+    ranks, the map is also timed wall-clock between barriers (max over ranks) -> the whole job's rate."""
+    global_batch = global_batch or batch
     frames = make_frames(torch, "checker", batch, rows, cols, seed, dev, period=64)
     out = fd.lsd_map(frames)
     torch.cuda.synchronize()
     valid = int(out[4].sum().item())
     ms = graph_time_ms(torch, lambda: fd.lsd_map(frames, out=out), reps)
+    job_ms = None
+    if max_fn is not None:
+        job_ms = ranked_time_ms(torch, lambda: fd.lsd_map(frames, out=out), reps, barrier, max_fn)
     px = batch * rows * cols
     mpx = batch * (rows - 1) * (cols - 1)
     alg = px + 9 * mpx + 4 * valid  # read u8 frame; write norm f32 + angle f32 + valid u8; 4 B per listed pixel
@@ -452,9 +460,11 @@ def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5, line_
              "lines_per_s": round(n_lines / line_s, 1), "lines_per_batch": n_lines,
              "mpix_s": round(px / line_s / 1e6, 1), "host_threads": _line_threads(),
              "note": "fd_lsd_lines: GPU level-line map (compact lists) + D2H + host region growing on worker threads"}
-    return {
-        "workload": f"LSD level-line map, {cols}x{rows} gray 64-px checker + noise, batch {batch}/GPU "
-                    "(BASELINE configs[3]); whole line detector under 'lines'",
+    res = {
+        "workload": f"LSD level-line map, {cols}x{rows} gray 64-px checker + noise, global batch {global_batch} "
+                    f"frame-sharded over the ranks ({batch} on this rank; BASELINE configs[3]); whole line detector "
+                    "under 'lines'",
+        "scaling": "strong", "global_batch": global_batch, "frames_this_rank": batch,
         "ms_per_batch": round(ms, 4), "mpix_s": round(px / (ms * 1e-3) / 1e6, 1), "valid_pixels": valid,
         "kernels": "k_lsd_map + k_lsd_scan + k_lsd_scatter",
         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -462,6 +472,37 @@ def run_lsd(torch, fd, dev, seed, batch=256, rows=1080, cols=1920, reps=5, line_
                      "bytes_per_launch": alg},
         "lines": lines,
     }
+    if job_ms is not None:
+        res["job"] = {"ms_per_global_batch": round(job_ms, 4),
+                      "mpix_s": round(global_batch * rows * cols / (job_ms * 1e-3) / 1e6, 1),
+                      "note": "all ranks' blocks, wall clock between barriers, max over ranks"}
+    return res
+
+
+def ranked_time_ms(torch, fn, reps, barrier, max_fn):
+    """Wall time per call of fn() over all ranks: `reps` calls replayed from one hipGraph per rank,
+    bracketed by barrier + device synchronisation on both sides, max over ranks (ms)."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+
+    def fence():
+        torch.cuda.synchronize()
+        if barrier is not None:
+            barrier()
+        torch.cuda.synchronize()
+
+    fence()
+    t0 = time.perf_counter()
+    g.replay()
+    fence()
+    el = time.perf_counter() - t0
+    del g
+    return max_fn(el) / reps * 1e3
 
 
 def copy_bandwidth(torch, dev, nbytes=1 << 30, reps=5):
@@ -534,38 +575,64 @@ def conv_flops(net, rows, cols):
     return total
 
 
-def run_superpoint(torch, fd, dev, seed, batch=64, rows=480, cols=640, steps=10):
-    """BASELINE configs[4]: SuperPoint fp16 on 640x480, 512 frames over 8 GPUs = 64 per GPU: network
+def run_superpoint(torch, fd, dev, seed, batch=64, rows=480, cols=640, steps=10, global_batch=None, chunk=64,
+                   barrier=None, max_fn=None):
+    """BASELINE configs[4]: SuperPoint fp16 on 640x480, a global batch of 512 frames frame-sharded over
+    the ranks (strong scaling: `batch` = this rank's block, run as network batches of `chunk`): network
     (PyTorch-ROCm, MIOpen convs), then GPU selection + descriptors (fd_nn_select / fd_nn_descriptors)."""
     from feature_detector_amd import superpoint as spm
 
+    global_batch = global_batch or batch
     det = spm.SuperPointDetector(spm.Options(kComputeDescriptors=True, kMaxImageRows=rows, kMaxImageCols=cols),
                                  device=dev.index or 0)
     det.Initialize()
     frames = make_frames(torch, "noise", batch, rows, cols, seed, dev)
+    chunks = [frames[i:i + chunk] for i in range(0, batch, chunk)]
+
+    def step():
+        for c in chunks:
+            res = det.DetectGoodFeaturesWithDescriptor(c)
+        return res
+
     for _ in range(2):
-        det.DetectGoodFeaturesWithDescriptor(frames)
-    torch.cuda.synchronize()
+        step()
+
+    def fence():
+        torch.cuda.synchronize()
+        if barrier is not None:
+            barrier()
+        torch.cuda.synchronize()
+
+    fence()
     t0 = time.perf_counter()
     for _ in range(steps):
-        xy, cnt, d = det.DetectGoodFeaturesWithDescriptor(frames)
-    torch.cuda.synchronize()
+        xy, cnt, d = step()
+    fence()
     el = (time.perf_counter() - t0) / steps
+    job_s = max_fn(el) if max_fn is not None else el
+    first = chunks[0]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(steps):
-        heat, desc = det.InferenceSession(frames)
+        heat, desc = det.InferenceSession(first)
     e1.record()
     torch.cuda.synchronize()
     net_ms = e0.elapsed_time(e1) / steps
+    xy, cnt, d = det.DetectGoodFeaturesWithDescriptor(first)
     post_ms = graph_time_ms(torch, lambda: (spm.nn_select(heat, det.options(), out=(xy, cnt)),
                                             spm.nn_descriptors(desc, xy, cnt, out=d)), 10)
-    flops = conv_flops(det.net, rows, cols) * batch
+    nb = len(first)
+    flops = conv_flops(det.net, rows, cols) * nb
     return {
         "workload": f"SuperPoint (random weights, fp16 convs) + heatmap selection (thr 0.1, dist 15, max 240) + "
-                    f"256-d descriptors, {cols}x{rows} noise, batch {batch}/GPU (BASELINE configs[4]: 512 over 8 GPUs)",
+                    f"256-d descriptors, {cols}x{rows} noise, global batch {global_batch} frame-sharded over the "
+                    f"ranks ({batch} on this rank, network batches of {chunk}; BASELINE configs[4])",
+        "scaling": "strong", "global_batch": global_batch, "frames_this_rank": batch,
         "ms_per_step": round(el * 1e3, 3), "frames_per_s": round(batch / el, 1),
-        "mpix_s": round(batch * rows * cols / el / 1e6, 1), "network_ms": round(net_ms, 3),
+        "mpix_s": round(batch * rows * cols / el / 1e6, 1),
+        "job": {"ms_per_global_batch": round(job_s * 1e3, 3), "frames_per_s": round(global_batch / job_s, 1),
+                "note": "all ranks' blocks, wall clock between barriers, max over ranks"},
+        "network_ms": round(net_ms, 3), "network_batch": nb,
         "postprocess_ms": round(post_ms, 4), "features_per_frame": round(float(cnt.float().mean().item()), 1),
         "network_roofline": {"bound": "mfma", "achieved": round(flops / (net_ms * 1e-3) / 1e12, 1),
                              "peak": MFMA_PEAK_TFLOPS_FP16, "unit": "TFLOP/s",
@@ -654,17 +721,40 @@ def launch_ranks(n):
     return bad[0] if bad else 0
 
 
+# Global batches of the strong-scaled legs (BASELINE configs[3]: 256 frames over the GPUs; configs[4]:
+# 512 frames over the GPUs): each rank takes its contiguous block (shard.shard_range).
+STRONG_GLOBAL = {"config4_lsd_map": 256, "config5_superpoint": 512}
+
+
+def strong_blocks(world, rank):
+    from feature_detector_amd.shard import shard_range
+
+    return {leg: shard_range(n, rank, world) for leg, n in STRONG_GLOBAL.items()}
+
+
+def rank_layout(dist, world, rank, local, device, device_count):
+    """Every rank's placement, gathered to all ranks over the process group (control plane only)."""
+    me = {"rank": rank, "local_rank": local, "device": device, "device_count": device_count, "pid": os.getpid(),
+          "strong_blocks": strong_blocks(world, rank)}
+    if world == 1:
+        return [me], {"backend": None, "world_size": 1}
+    objs = [None] * world
+    dist.all_gather_object(objs, me)
+    return objs, {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+
+
 def launch_check(args, world, rank, local):
     """FD_BENCH_LAUNCH_CHECK=1: the rank layout without any GPU work (the CPU tests use it with gloo):
-    every rank reports its device index; rank 0 prints one JSON line."""
+    every rank reports its device index and its blocks of the strong-scaled legs; rank 0 prints one
+    JSON line in the bench's own `ranks` / `process_group` format."""
     import torch.distributed as dist
 
     ndev = int(os.environ.get("FD_BENCH_LAUNCH_CHECK_DEVICES", "0")) or world
     dist.init_process_group("gloo")
-    objs = [None] * world
-    dist.all_gather_object(objs, {"rank": rank, "local_rank": local, "device": local % ndev, "pid": os.getpid()})
+    objs, pg = rank_layout(dist, world, rank, local, local % ndev, ndev)
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "requested_gpus": args.gpus, "ranks": objs}), flush=True)
+        print(json.dumps({"n_gpus": world, "requested_gpus": args.gpus, "ranks": objs, "process_group": pg,
+                          "strong_global_batch": STRONG_GLOBAL}), flush=True)
     dist.destroy_process_group()
 
 
@@ -802,14 +892,25 @@ def main():
             out["config3_fast_brief"] = run_config3(torch, fd, dev, seed=777 + rank)
 
     # ---- BASELINE configs[4]: SuperPoint, 640x480, 64 frames per GPU --------------------------------
+    # (strong scaling: the global batch split over the ranks; every rank's block, device and the process
+    # group's own world size go into the line)
+    blocks = strong_blocks(world, rank)
+    max_fn = (lambda v: max_over_ranks(v, dist if world > 1 else None, dev if backend == "nccl" else None))
     if not args.no_superpoint:
+        s0, e0 = blocks["config5_superpoint"]
         with phase(torch, "config5_superpoint"):
-            out["config5_superpoint"] = run_superpoint(torch, fd, dev, seed=5151 + rank)
+            out["config5_superpoint"] = run_superpoint(torch, fd, dev, seed=5151 + 7 * s0, batch=e0 - s0,
+                                                       global_batch=STRONG_GLOBAL["config5_superpoint"],
+                                                       barrier=barrier, max_fn=max_fn)
 
-    # ---- BASELINE configs[3]: LSD map, 1920x1080 batch 256 per GPU ----------------------------------
+    # ---- BASELINE configs[3]: LSD map, 1920x1080, 256 frames over the ranks ------------------------
     if not args.no_lsd:
+        s0, e0 = blocks["config4_lsd_map"]
         with phase(torch, "config4_lsd_map"):
-            out["config4_lsd_map"] = run_lsd(torch, fd, dev, seed=4242 + rank)
+            out["config4_lsd_map"] = run_lsd(torch, fd, dev, seed=4242 + 7 * s0, batch=e0 - s0,
+                                             global_batch=STRONG_GLOBAL["config4_lsd_map"], barrier=barrier,
+                                             max_fn=max_fn)
+    out["ranks"], out["process_group"] = rank_layout(dist, world, rank, local, dev_index, ndev)
     with phase(torch, "device_copy"):
         out["device_copy_gbs"] = copy_bandwidth(torch, dev)
     if world == 1:

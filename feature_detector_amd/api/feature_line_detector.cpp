@@ -56,6 +56,13 @@ bool FeatureLineDetector::DetectGoodFeatures(const GrayImage &image, const uint3
 
     const fd_lsd_opts opts{options_.kMinValidGradientNorm, options_.kMinToleranceAngleResidualInRad,
                            options_.kMinValidLineLengthInPixel, options_.kMaxToleranceInlierRation};
+    // Drop the previous call's lazy state first: staging reuses (or reallocates) the context's frame
+    // buffer, so a failure below must not leave pixels()/sorted_pixels() pointing at it.
+    staged_ = nullptr;
+    members_valid_ = true;
+    pixels_ = PixelMatrix();
+    sorted_pixels_.clear();
+    rectangles_.clear();
     const uint8_t *dframe = nullptr;
     if (fd_ctx_stage(ctx_, image.data(), static_cast<int64_t>(image.rows()) * image.cols(), &dframe) != FD_OK) {
         error_ = std::string("fd_ctx_stage: ") + fd_last_error(ctx_);
@@ -104,6 +111,7 @@ bool FeatureLineDetector::DetectGoodFeatures(const GrayImage &image, const uint3
 void FeatureLineDetector::Materialise() const {
     if (members_valid_) return;
     members_valid_ = true;
+    if (!staged_) return;
     if (!ComputeLineLevelAngleMap()) return;
     // is_used as the reference's regions leave it (every listed pixel; unlisted ones are invalid)
     int64_t n = 0;

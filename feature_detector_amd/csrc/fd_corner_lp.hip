@@ -82,6 +82,9 @@ __device__ __forceinline__ f2 corner_response_fp(f2 sxx, f2 syy, f2 sxy, float t
 #ifndef FD_LP_FP
 #define FD_LP_FP 1
 #endif
+#ifndef FD_LP_PKQ
+#define FD_LP_PKQ 0
+#endif
 
 // ---------------------------------------------------------------------------------------------------
 // K1 (list mode, lane-private emission): the per-pixel kernel of fd_points_detect / fd_points_response.
@@ -101,6 +104,20 @@ __device__ __forceinline__ f2 corner_response_fp(f2 sxx, f2 syy, f2 sxy, float t
 // Only for thr >= 0 (the single-gate form); negative thresholds use k_corner.
 // ---------------------------------------------------------------------------------------------------
 constexpr int kLpSlots = FD_LP_SLOTS;  // lane-private slots per lane (LDS: 8 B x 64 lanes each)
+// With the selection histogram (16 KiB) the workgroup's LDS is slots + histogram: FD_LP_SLOTS_H slots
+// keep it (with the sorted-segment words) under 40 KiB: 4 workgroups per CU instead of 3 at 48 KiB.
+#ifndef FD_LP_SLOTS_H
+#define FD_LP_SLOTS_H 11
+#endif
+template <bool HIST>
+constexpr int lp_slots() { return HIST ? FD_LP_SLOTS_H : kLpSlots; }
+
+// Occupancy the register allocation must allow: LDS admits 5 workgroups (20 waves) per CU without the
+// histogram, 4 with it (FD_LP_SLOTS_H = 11); the allocator then keeps <= 96 / <= 128 VGPRs (8 columns
+// per lane and the unaligned no-histogram variants would spill at those limits: no target).
+#ifndef FD_LP_WAVES
+#define FD_LP_WAVES(PX, HIST, ALIGNED) __attribute__((amdgpu_waves_per_eu((PX) == 8 ? 1 : (HIST) || !(ALIGNED) ? 4 : 5)))
+#endif
 
 template <int PX>
 struct LpGeom {
@@ -111,9 +128,17 @@ struct LpGeom {
 };
 
 template <bool HIST>
-struct alignas(HIST ? 16 : 4) LpLds {  // (with HIST: hist is cleared and read as uint4, fd_corner_common.h)
-    uint32_t slot[4][kLpSlots][128];  // [wave][slot][0..63 response bits | 64..127 raster index]
-    uint32_t hist[HIST ? kHistBins : 1];
+struct alignas(16) LpLds {  // (hist is cleared and read as uint4, fd_corner_common.h)
+    uint32_t slot[4][lp_slots<true>()][128];  // [wave][slot][0..63 response bits | 64..127 raster index]
+    uint32_t hist[kHistBins];
+    uint32_t seg_ovf;  // sorted-segment mode: a wave flushed before the end (the segment is unsorted)
+};
+// Without the histogram the slots alone: exactly 32 KiB at 16 slots, so 5 workgroups (20 waves) fit a
+// CU's 160 KiB (one extra word made it 4).
+template <>
+struct alignas(16) LpLds<false> {
+    uint32_t slot[4][lp_slots<false>()][128];
+    static constexpr uint32_t *hist = nullptr;  // (never used: keeps L.hist well-formed)
 };
 
 // One row's pixels of the lane's PX columns (out-of-range bytes read 0 through the buffer resource).
@@ -207,7 +232,7 @@ __device__ __forceinline__ void lp_seg_flush(uint32_t &n, const uint32_t *sl, co
     }
     if (!active) n = 0;
     auto bin_of = [&](float r) { return ((float_key(r) - a.key_base) << a.key_lz) >> 20; };
-    for (int j = 0; j < kLpSlots; ++j) {
+    for (int j = 0; j < lp_slots<true>(); ++j) {
         if (ballot(n > static_cast<uint32_t>(j)) == 0) break;
         if (n > static_cast<uint32_t>(j)) atomicAdd(&L.hist[bin_of(lp_resp<KIND>(sl, j))], 1u);
     }
@@ -241,7 +266,7 @@ __device__ __forceinline__ void lp_seg_flush(uint32_t &n, const uint32_t *sl, co
     const int64_t base = wg_base;
     const int g = logical_block() % a.blocks_per_frame;
     uint64_t *head = a.seghead + (static_cast<int64_t>(f) * a.blocks_per_frame + g) * kSegHead;
-    for (int j = 0; j < kLpSlots; ++j) {
+    for (int j = 0; j < lp_slots<true>(); ++j) {
         if (ballot(n > static_cast<uint32_t>(j)) == 0) break;
         if (n > static_cast<uint32_t>(j)) {
             const float r = lp_resp<KIND>(sl, j);
@@ -277,11 +302,10 @@ __device__ __forceinline__ void lp_emit(uint32_t &A, float x, float nb, uint32_t
 }
 
 template <int KIND, int PX, bool MASKED, bool ALIGNED, bool HIST, bool SEG>
-__global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
+FD_LP_WAVES(PX, HIST, ALIGNED) __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
     using G = LpGeom<PX>;
     constexpr int NW = G::NW;
     __shared__ LpLds<HIST> L;
-    __shared__ uint32_t seg_ovf;
     int f, ty, tx;
     const bool active = decode_tile(a, f, ty, tx);
     const int lane = lane_id(), wv = threadIdx.x >> 6;
@@ -289,7 +313,7 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
     typedef __attribute__((address_space(3))) uint32_t lds_u32;
     const uint32_t sl_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_u32 *)sl));  // LDS byte address
     if constexpr (SEG) {
-        if (threadIdx.x == 0) seg_ovf = 0;
+        if (threadIdx.x == 0) L.seg_ovf = 0;
     }
     if constexpr (HIST) hist_clear(L.hist);
     else if constexpr (SEG) __syncthreads();
@@ -377,6 +401,20 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
                 // float integers; the halo pixels and the halo columns' products from the neighbour lanes
                 const float fL = from_left_f(fpx[sc][PX - 1]), fR = from_right_f(fpx[sc][0]);
                 float qxx[PX + 2], qyy[PX + 2], qxy[PX + 2];
+#if FD_LP_PKQ
+                // column pairs: iy and the three products as packed ops (2 results per issue slot;
+                // separate full-rate ops pair up only when two waves offer them in the same cycle)
+#pragma unroll
+                for (int m = 0; m < PX; m += 2) {
+                    const f2 ix = f2{(m + 1 < PX ? fpx[sc][m + 1] : fR) - (m > 0 ? fpx[sc][m - 1] : fL),
+                                     (m + 2 < PX ? fpx[sc][m + 2] : fR) - fpx[sc][m]};
+                    const f2 iy = f2{fpx[s][m], fpx[s][m + 1]} - f2{fpx[su][m], fpx[su][m + 1]};
+                    const f2 pxx2 = ix * ix, pyy2 = iy * iy, pxy2 = ix * iy;
+                    qxx[m + 1] = pxx2.x, qxx[m + 2] = pxx2.y;
+                    qyy[m + 1] = pyy2.x, qyy[m + 2] = pyy2.y;
+                    qxy[m + 1] = pxy2.x, qxy[m + 2] = pxy2.y;
+                }
+#else
 #pragma unroll
                 for (int m = 0; m < PX; ++m) {
                     const float ix = (m + 1 < PX ? fpx[sc][m + 1] : fR) - (m > 0 ? fpx[sc][m - 1] : fL);
@@ -385,6 +423,7 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
                     qyy[m + 1] = iy * iy;
                     qxy[m + 1] = ix * iy;
                 }
+#endif
                 qxx[0] = from_left_f(qxx[PX]);
                 qyy[0] = from_left_f(qyy[PX]);
                 qxy[0] = from_left_f(qxy[PX]);
@@ -480,11 +519,11 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
                 const int nr = ri - 3;
                 if (nr >= y0 && nr < y1) {  // wave-uniform
                     // at most PX/2 hits per lane and row (adjacent columns cannot both be strict maxima)
-                    if (ballot(A >= sl_addr + 512u * (kLpSlots - PX / 2)) != 0ull) {
+                    if (ballot(A >= sl_addr + 512u * (lp_slots<HIST>() - PX / 2)) != 0ull) {
                         if constexpr (SEG) {  // this workgroup's segment is no longer one sorted run
                             if (lane == 0) {
                                 atomicOr(&a.seg_bad[f], 1u);
-                                seg_ovf = 1u;
+                                L.seg_ovf = 1u;
                             }
                         }
                         uint32_t n = (A - sl_addr) >> 9;
@@ -534,7 +573,7 @@ __global__ __launch_bounds__(256) void k_corner_lp(PointsArgs a) {
     uint32_t n = (A - sl_addr) >> 9;  // this lane's used slots
     if constexpr (SEG) {
         __shared__ uint32_t seg_wtot[4], seg_base;
-        lp_seg_flush<KIND>(n, sl, a, f, active, L, &seg_ovf, seg_wtot, seg_base);
+        lp_seg_flush<KIND>(n, sl, a, f, active, L, &L.seg_ovf, seg_wtot, seg_base);
     } else {
         if (active) lp_flush<KIND>(n, sl, a, f, lhist);
         if constexpr (HIST) hist_flush(L.hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);

@@ -199,6 +199,7 @@ struct LsdArgs {
     float min_norm;
     float *norm, *angle;
     uint8_t *valid;
+    int pitch;          // dense maps: entries per map row (>= cols-1; a multiple of 4 keeps the row stores aligned)
     uint32_t *rowbits;  // [batch][chunks][words][cols-1]: valid rows of each (column, chunk), bit r - r0
                         // (column fastest: a wave's stores and loads are contiguous)
     int words;          // ceil(chunk_h / 32)

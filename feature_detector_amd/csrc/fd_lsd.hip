@@ -169,7 +169,7 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     const int lane = lane_id(), wv = threadIdx.x >> 6;
     uint32_t *const qsd = Q.sd[wv];
     uint32_t *const qidx = Q.idx[wv];
-    const int rows = a.rows, cols = a.cols, mc = cols - 1;
+    const int rows = a.rows, cols = a.cols, mc = cols - 1, mp = a.pitch;  // mp: map row pitch (entries)
     const int c0 = strip * 256 + 4 * lane;
     const int r0 = 1 + chunk * a.chunk_h;
     const int r1 = min(r0 + a.chunk_h, rows - 2);  // rows [r0, r1) within [1, rows-3]
@@ -181,9 +181,9 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     }
     const bool full = c0 + 3 <= cols - 2;  // all four map columns exist: one store per map
     const auto rs = make_rsrc(a.frames + static_cast<int64_t>(f) * rows * cols, static_cast<uint32_t>(rows * cols));
-    const int64_t mbase = static_cast<int64_t>(f) * (rows - 1) * mc;
+    const int64_t mbase = static_cast<int64_t>(f) * (rows - 1) * mp;
     float *const amap = a.angle ? a.angle + mbase : nullptr;
-    const uint32_t mbytes = static_cast<uint32_t>(rows - 1) * static_cast<uint32_t>(mc);
+    const uint32_t mbytes = static_cast<uint32_t>(rows - 1) * static_cast<uint32_t>(mp);
     const auto rn = make_rsrc(a.norm ? a.norm + mbase : nullptr, a.norm ? 4 * mbytes : 0u);
     const auto ra = make_rsrc(amap, amap ? 4 * mbytes : 0u);
     const auto rv = make_rsrc(a.valid ? a.valid + mbase : nullptr, a.valid ? mbytes : 0u);
@@ -195,11 +195,11 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
         if constexpr (INTERIOR) {
             __builtin_amdgcn_raw_buffer_store_b128(
                 u4{__float_as_uint(av[0]), __float_as_uint(av[1]), __float_as_uint(av[2]), __float_as_uint(av[3])}, ra,
-                4 * (r * mc + c0), 0, 0);
+                4 * (r * mp + c0), 0, 0);
             return;
         }
         if (!a.angle) return;
-        const int64_t i = mbase + static_cast<int64_t>(r) * mc + c0;
+        const int64_t i = mbase + static_cast<int64_t>(r) * mp + c0;
         if (full) {
             *reinterpret_cast<F4 *>(a.angle + i) = F4{av[0], av[1], av[2], av[3]};
         } else {
@@ -212,14 +212,14 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     auto put = [&](int r, const float (&nv)[4], uint32_t vb) {
         if constexpr (INTERIOR) {
             // (null maps: a zero-range resource drops the stores)
-            const int o = r * mc + c0;  // < 2^31: checked on the host
+            const int o = r * mp + c0;  // < 2^31: checked on the host
             __builtin_amdgcn_raw_buffer_store_b128(
                 u4{__float_as_uint(nv[0]), __float_as_uint(nv[1]), __float_as_uint(nv[2]), __float_as_uint(nv[3])}, rn,
                 4 * o, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(vb, rv, o, 0, 0);
             return;
         }
-        const int64_t i = mbase + static_cast<int64_t>(r) * mc + c0;
+        const int64_t i = mbase + static_cast<int64_t>(r) * mp + c0;
         if (full) {
             if (a.norm) *reinterpret_cast<F4 *>(a.norm + i) = F4{nv[0], nv[1], nv[2], nv[3]};
             typedef uint32_t u32a1 __attribute__((aligned(1)));

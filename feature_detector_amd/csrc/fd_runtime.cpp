@@ -552,6 +552,25 @@ int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb, 
     return FD_OK;
 }
 
+bool host_ties_env() {  // FD_TIES_HOST=1: the round-3 host path for every flagged frame (A/B and checker)
+    static const bool v = std::getenv("FD_TIES_HOST") && std::atoi(std::getenv("FD_TIES_HOST")) != 0;
+    return v;
+}
+
+// Calls that will synchronise the context stream (host outputs, or the host tie path) cannot run while
+// that stream is being captured into a graph: refuse at entry, before any work is enqueued, so that a
+// failed call leaves nothing half-recorded in the capture.
+int refuse_sync_under_capture(fd_ctx *c, int outputs_on_device) {
+    const bool syncs = !outputs_on_device || (c->tie_order == FD_TIES_REFERENCE && host_ties_env());
+    if (!syncs || !c->stream) return FD_OK;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    FD_HIP_TRY(c, hipStreamIsCapturing(c->stream, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+        return fail(c, FD_ERR_INVALID, "this call synchronises the stream (host outputs or FD_TIES_HOST): not allowed "
+                                       "during stream capture; pass device outputs");
+    return FD_OK;
+}
+
 // K4 (k_gather + k_select) on the candidate lists, features into out_xy / out_counts (device, or copied
 // back to the host and checked when !outputs_on_device).
 int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const SelectBufs &sb, float *out_xy,
@@ -664,8 +683,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         }
     }
     if (c->tie_order == FD_TIES_REFERENCE && !q.tie_idx_desc) {
-        static const bool host_ties = std::getenv("FD_TIES_HOST") && std::atoi(std::getenv("FD_TIES_HOST")) != 0;
-        if (host_ties) {  // the round-3 host path (A/B and checker): every flagged frame sorted on the host
+        if (host_ties_env()) {  // the round-3 host path (A/B and checker): every flagged frame sorted on the host
             const int rc = resolve_ties(c, s, batch, sb, q.push_order, FD_FRAME_TIES);
             if (rc) return rc;
         } else {
@@ -726,6 +744,7 @@ void lsd_geometry(fdk::LsdArgs &a, int batch, int rows, int cols, const uint8_t 
     a.strips = (cols - 1 + 63) / 64;  // map columns [0, cols-2]
     a.strips4 = (cols - 1 + 255) / 256;
     a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
+    a.pitch = cols - 1;  // dense maps: unpitched unless the caller gives a pitch (fd_lsd_map_pitched)
     int64_t target = 16384;  // waves of the map kernel
     if (const char *e = std::getenv("FD_LSD_WAVES")) target = std::max<int64_t>(64, std::atoll(e));  // A/B
     int64_t ch = (static_cast<int64_t>(batch) * a.strips4 * work_rows) / target;
@@ -915,6 +934,7 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     if (rc) return rc;
     if (!opts || !out_xy || !out_counts || out_stride < 1) return fail(c, FD_ERR_INVALID, "bad output arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
+    if ((rc = refuse_sync_under_capture(c, outputs_on_device))) return rc;
     const uint8_t *dframes = nullptr;
     rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
     if (rc) return rc;
@@ -1009,6 +1029,7 @@ int fd_points_select(fd_ctx *c, int batch, int rows, int cols, const fd_point_op
     if (!cand_counts || cand_cap < 0 || cand_cap > 0xFFFFFFFFll)
         return fail(c, FD_ERR_INVALID, "cand_counts is NULL or cand_cap out of range");
     FD_HIP_TRY(c, hipSetDevice(c->device));
+    if ((rc = refuse_sync_under_capture(c, outputs_on_device))) return rc;
     int64_t max_n = cand_cap;
     if (!cands_on_device) {
         max_n = 0;
@@ -1260,19 +1281,35 @@ int fd_points_candidates(fd_ctx *c, int kind, const uint8_t *frames, int frames_
 int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols, float min_norm,
                float *norm, float *angle, uint8_t *valid, int32_t *valid_idx, int64_t idx_cap, int64_t *valid_counts,
                int outputs_on_device) {
+    return fd_lsd_map_pitched(c, frames, frames_on_device, batch, rows, cols, min_norm, norm, angle, valid,
+                              static_cast<int64_t>(cols) - 1, valid_idx, idx_cap, valid_counts, outputs_on_device);
+}
+
+// Row pitch of the library's own (device) dense maps: 16 entries, so every f32 map row starts on a
+// 64-byte and every u8 row on a 16-byte boundary and the map kernel's dword / dwordx4 row stores are
+// aligned (a 1919-entry row is misaligned on 3 of 4 rows: the vector-memory address unit then splits
+// the stores).
+int64_t lsd_aligned_pitch(int cols) { return (static_cast<int64_t>(cols) - 1 + 15) / 16 * 16; }
+
+int fd_lsd_map_pitched(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
+                       float min_norm, float *norm, float *angle, uint8_t *valid, int64_t map_pitch, int32_t *valid_idx,
+                       int64_t idx_cap, int64_t *valid_counts, int outputs_on_device) {
     int rc = check_shape(c, FD_HARRIS, batch, rows, cols, false);
     if (rc) return rc;
     if (rows < 2 || cols < 2) return fail(c, FD_ERR_INVALID, "LSD needs rows >= 2 and cols >= 2");  // :14
-    if (static_cast<int64_t>(rows - 1) * (cols - 1) >= (int64_t(1) << 29))  // 32-bit byte offsets into a frame's maps
-        return fail(c, FD_ERR_INVALID, "LSD frame too large ((rows-1)*(cols-1) must be < 2^29)");
+    const int mc = cols - 1;
+    if (map_pitch < mc || map_pitch > (int64_t(1) << 29)) return fail(c, FD_ERR_INVALID, "map_pitch must be >= cols-1");
+    // device maps: the caller's pitch; host maps: the library's staging maps use the aligned pitch
+    const int64_t dpitch = outputs_on_device ? map_pitch : lsd_aligned_pitch(cols);
+    if (static_cast<int64_t>(rows - 1) * dpitch >= (int64_t(1) << 29))  // 32-bit byte offsets into a frame's maps
+        return fail(c, FD_ERR_INVALID, "LSD frame too large ((rows-1)*pitch must be < 2^29)");
     if (!valid_counts || idx_cap < 0 || (idx_cap > 0 && !valid_idx))
         return fail(c, FD_ERR_INVALID, "bad output arguments");
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const uint8_t *dframes = nullptr;
     rc = stage_frames(c, frames, frames_on_device, batch, rows, cols, dframes);
     if (rc) return rc;
-    const int mc = cols - 1;
-    const size_t nmap = static_cast<size_t>(batch) * (rows - 1) * mc;
+    const size_t nmap = static_cast<size_t>(batch) * (rows - 1) * static_cast<size_t>(dpitch);
     float *dn = nullptr, *da = nullptr;
     uint8_t *dv = nullptr;
     if (outputs_on_device) {
@@ -1309,9 +1346,10 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         if (da) FD_HIP_TRY(c, hipMemsetAsync(da, 0, sizeof(float) * nmap, c->stream));
         FD_HIP_TRY(c, hipMemsetAsync(dv, 0, nmap, c->stream));
         FD_HIP_TRY(c, hipMemsetAsync(dc, 0, sizeof(int64_t) * batch, c->stream));
-    } else {  // k_lsd_map writes every map entry (zeros outside the scanned rows/columns)
+    } else {  // k_lsd_map writes every map entry (zeros outside the scanned rows/columns; pitch padding untouched)
         fdk::LsdArgs a{};
         lsd_geometry(a, batch, rows, cols, dframes);
+        a.pitch = static_cast<int>(dpitch);
         a.min_norm = min_norm;
         a.norm = dn;
         a.angle = da;
@@ -1332,9 +1370,16 @@ int fd_lsd_map(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch
         FD_HIP_TRY(c, hipMemcpyAsync(valid_counts, dc, sizeof(int64_t) * batch, hipMemcpyDeviceToHost, c->stream));
         if (idx_cap > 0)
             FD_HIP_TRY(c, hipMemcpyAsync(valid_idx, di, sizeof(int32_t) * idx_cap * batch, hipMemcpyDeviceToHost, c->stream));
-        if (norm) FD_HIP_TRY(c, hipMemcpyAsync(norm, dn, sizeof(float) * nmap, hipMemcpyDeviceToHost, c->stream));
-        if (angle) FD_HIP_TRY(c, hipMemcpyAsync(angle, da, sizeof(float) * nmap, hipMemcpyDeviceToHost, c->stream));
-        if (valid) FD_HIP_TRY(c, hipMemcpyAsync(valid, dv, nmap, hipMemcpyDeviceToHost, c->stream));
+        // pitched device maps -> the host's maps (row pitch map_pitch entries)
+        const size_t hrows = static_cast<size_t>(batch) * (rows - 1);
+        if (norm)
+            FD_HIP_TRY(c, hipMemcpy2DAsync(norm, sizeof(float) * map_pitch, dn, sizeof(float) * dpitch, sizeof(float) * mc,
+                                           hrows, hipMemcpyDeviceToHost, c->stream));
+        if (angle)
+            FD_HIP_TRY(c, hipMemcpy2DAsync(angle, sizeof(float) * map_pitch, da, sizeof(float) * dpitch, sizeof(float) * mc,
+                                           hrows, hipMemcpyDeviceToHost, c->stream));
+        if (valid)
+            FD_HIP_TRY(c, hipMemcpy2DAsync(valid, map_pitch, dv, dpitch, mc, hrows, hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         for (int b = 0; b < batch; ++b)
             if (valid_counts[b] > idx_cap) return fail(c, FD_ERR_CAPACITY, "idx_cap smaller than the valid pixels");
@@ -1599,6 +1644,7 @@ int fd_nn_select(fd_ctx *c, const float *heatmap, int heatmap_on_device, int bat
     if (opts->invalid_boundary < 0) return fail(c, FD_ERR_INVALID, "invalid_boundary must be >= 0");
     if (opts->max_features < 0) return fail(c, FD_ERR_INVALID, "max_features must be >= 0");
     FD_HIP_TRY(c, hipSetDevice(c->device));
+    if ((rc = refuse_sync_under_capture(c, outputs_on_device))) return rc;
     const int64_t npx = static_cast<int64_t>(rows) * cols;
     const float *dheat = heatmap;
     if (!heatmap_on_device) {
@@ -1670,6 +1716,7 @@ int fd_nn_select_list(fd_ctx *c, const int64_t *keypoints, const float *scores, 
     if (!counts || cap < 0 || cap > 0x7FFFFFFFll) return fail(c, FD_ERR_INVALID, "counts is NULL or cap out of range");
     if (cand_desc && (desc_dim < 1 || !out_desc)) return fail(c, FD_ERR_INVALID, "descriptors need desc_dim >= 1 and out_desc");
     FD_HIP_TRY(c, hipSetDevice(c->device));
+    if ((rc = refuse_sync_under_capture(c, outputs_on_device))) return rc;
     if (!inputs_on_device)
         for (int b = 0; b < batch; ++b)
             if (counts[b] < 0 || counts[b] > cap)
@@ -1789,9 +1836,11 @@ int fd_nn_select_list(fd_ctx *c, const int64_t *keypoints, const float *scores, 
     return FD_OK;
 }
 
-int fd_nn_bias_relu(fd_ctx *c, const void *x, const void *bias, void *y, int n, int h, int w, int ch, int pool) {
+int fd_nn_bias_relu(fd_ctx *c, const void *x, const void *bias, int64_t bias_len, void *y, int n, int h, int w, int ch,
+                    int pool) {
     if (!c) return FD_ERR_INVALID;
     if (!x || !bias || !y) return fail(c, FD_ERR_INVALID, "bad arguments");
+    if (bias_len != ch) return fail(c, FD_ERR_INVALID, "bias length must equal the channel count");
     if (n < 0 || h < 0 || w < 0 || ch <= 0 || ch % 8) return fail(c, FD_ERR_INVALID, "need n, h, w >= 0, c a multiple of 8");
     if (pool && ((h | w) & 1)) return fail(c, FD_ERR_INVALID, "pooling needs even h and w");
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(y)) & 15)

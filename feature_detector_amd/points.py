@@ -397,12 +397,14 @@ def point_candidates(kind, frames, min_feature_distance: int = 15, min_valid_res
 
 
 def lsd_map(frames, min_norm: float = 20.0, cap: int | None = None, ctx: Context | None = None, out=None):
-    """ComputeLineLevelAngleMap (fd_lsd_map).
+    """ComputeLineLevelAngleMap (fd_lsd_map / fd_lsd_map_pitched).
 
     Host (numpy) frames: returns per frame (norm, angle, valid, valid_idx_colmajor); maps are
     (rows-1, cols-1). Torch device frames: returns device tensors (norm [B, R-1, C-1] f32, angle f32,
     valid u8, valid_idx int32 [B, cap], counts int64 [B]), asynchronous on torch's current stream;
-    `out` may pass them preallocated (graph capture); any of norm/angle/valid may be None to skip.
+    the maps are views of storage whose rows are padded to 16 entries (aligned row stores); `out` may
+    pass them preallocated (graph capture), contiguous or as such row-padded views sharing one row
+    pitch; any of norm/angle/valid may be None to skip.
     """
     ptr, on_dev, b, r, c, keep = _frames(frames)
     ctx = _resolve_ctx(ctx, frames)
@@ -413,20 +415,32 @@ def lsd_map(frames, min_norm: float = 20.0, cap: int | None = None, ctx: Context
 
         if out is None:
             dev = frames.device
-            out = (torch.empty((b, mr, mc), dtype=torch.float32, device=dev),
-                   torch.empty((b, mr, mc), dtype=torch.float32, device=dev),
-                   torch.empty((b, mr, mc), dtype=torch.uint8, device=dev),
+            pitch = (mc + 15) // 16 * 16
+            out = (torch.empty((b, mr, pitch), dtype=torch.float32, device=dev)[..., :mc],
+                   torch.empty((b, mr, pitch), dtype=torch.float32, device=dev)[..., :mc],
+                   torch.empty((b, mr, pitch), dtype=torch.uint8, device=dev)[..., :mc],
                    torch.empty((b, max(cap, 1)), dtype=torch.int32, device=dev),
                    torch.empty((b,), dtype=torch.int64, device=dev))
         norm, ang, val, idx, cnt = out
+        pitch = None
+        for t in (norm, ang, val):
+            if t is None:
+                continue
+            if tuple(t.shape) != (b, mr, mc) or t.stride(2) != 1 or t.stride(0) != mr * t.stride(1):
+                raise ValueError(f"lsd_map: maps must be [{b}, {mr}, {mc}] with unit column stride and rows "
+                                 "packed at one pitch")
+            if pitch not in (None, t.stride(1)):
+                raise ValueError("lsd_map: norm / angle / valid must share one row pitch")
+            pitch = t.stride(1)
+        pitch = mc if pitch is None else pitch
         cap = idx.shape[1]
         _bind_stream(ctx, True)
 
         def p(t):
             return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
-        rc = _lib.load().fd_lsd_map(ctx.ptr, ctypes.c_void_p(ptr), 1, b, r, c, float(min_norm), p(norm), p(ang),
-                                    p(val), p(idx), int(cap), p(cnt), 1)
+        rc = _lib.load().fd_lsd_map_pitched(ctx.ptr, ctypes.c_void_p(ptr), 1, b, r, c, float(min_norm), p(norm),
+                                            p(ang), p(val), int(pitch), p(idx), int(cap), p(cnt), 1)
         _lib.check(ctx.ptr, rc)
         del keep
         return out

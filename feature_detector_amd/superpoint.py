@@ -177,22 +177,31 @@ def nn_select_list(keypoints, scores, rows: int, cols: int, counts=None, options
 def bias_relu(x, bias, pool: bool = False, out=None, ctx: Context | None = None):
     """fd_nn_bias_relu: relu(x + bias) (and the 2x2 max pool when pool) of a channels-last fp16
     activation [N, C, H, W] on the device, in one pass (torch's current stream). x is the output of a
-    bias-free convolution; the result equals PyTorch's conv-with-bias -> ReLU (-> MaxPool2d(2, 2)) in
-    half precision bit for bit. out: preallocated result (may be x itself when not pooling)."""
+    bias-free convolution; the result equals PyTorch's separate half-precision add / ReLU (/ MaxPool2d(2,
+    2)) ops on it, bit for bit (not a conv-with-bias, whose bias is added before the rounding to half;
+    and a NaN sum gives 0 here). out: preallocated result (may be x itself when not pooling)."""
     import torch
 
     if not (_is_torch_device_tensor(x) and x.dtype == torch.float16 and x.dim() == 4
             and x.is_contiguous(memory_format=torch.channels_last)):
         raise ValueError("bias_relu: x must be a channels-last float16 [N, C, H, W] device tensor")
     n, c, h, w = x.shape
+    if pool and (h % 2 or w % 2):
+        raise ValueError("bias_relu: pooling needs even H and W")
+    shape = (n, c, h // 2, w // 2) if pool else (n, c, h, w)
     if out is None:
-        shape = (n, c, h // 2, w // 2) if pool else (n, c, h, w)
         out = torch.empty(shape, dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
-    b = bias.detach().to(torch.float16).contiguous()
+    elif not (_is_torch_device_tensor(out) and out.device == x.device and out.dtype == torch.float16
+              and tuple(out.shape) == shape and out.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError(f"bias_relu: out must be a channels-last float16 {list(shape)} tensor on {x.device}")
+    if bias.numel() != c:
+        raise ValueError(f"bias_relu: bias has {bias.numel()} values for {c} channels")
+    b = bias.detach().to(device=x.device, dtype=torch.float16).contiguous()
     ctx = _resolve_ctx(ctx, x)
     _bind_stream(ctx, True)
     rc = _lib.load().fd_nn_bias_relu(ctx.ptr, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(b.data_ptr()),
-                                      ctypes.c_void_p(out.data_ptr()), int(n), int(h), int(w), int(c), 1 if pool else 0)
+                                      int(b.numel()), ctypes.c_void_p(out.data_ptr()), int(n), int(h), int(w), int(c),
+                                      1 if pool else 0)
     _lib.check(ctx.ptr, rc)
     return out
 

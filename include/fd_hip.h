@@ -196,6 +196,18 @@ int fd_lsd_map(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int bat
                float *norm, float *angle, uint8_t *valid, int32_t *valid_idx, int64_t idx_cap, int64_t *valid_counts,
                int outputs_on_device);
 
+/*
+ * fd_lsd_map_pitched -- fd_lsd_map with dense maps of row pitch map_pitch entries (>= cols-1): row r of
+ * frame b's maps starts at entry (b * (rows-1) + r) * map_pitch of norm / angle / valid (entries past
+ * cols-2 in a row are left untouched). The map indices in valid_idx stay row * (cols-1) + col. With a
+ * pitch that is a multiple of 16 entries every map row starts 64-byte (f32) / 16-byte (u8) aligned and
+ * the map kernel's row stores are aligned (the faster layout for device outputs; host outputs are
+ * always computed that way and copied to the caller's pitch). fd_lsd_map = map_pitch cols-1.
+ */
+int fd_lsd_map_pitched(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
+                       float min_norm, float *norm, float *angle, uint8_t *valid, int64_t map_pitch, int32_t *valid_idx,
+                       int64_t idx_cap, int64_t *valid_counts, int outputs_on_device);
+
 /* ---- LSD line segments (level-line map on the GPU, region growing on host threads) --------------- */
 /* FeatureLineDetector::Options (feature_line_detector.h:40-45). */
 typedef struct fd_lsd_opts {
@@ -344,11 +356,13 @@ int fd_nn_descriptors(fd_ctx *ctx, const float *map, int map_on_device, int map_
  * fd_nn_bias_relu -- the NN detectors' bias + ReLU after a bias-free convolution, and with pool = 1 the
  * 2x2 / stride-2 max pool that follows (nn.MaxPool2d(2, 2)), in one pass over an NHWC (channels-last)
  * fp16 activation x [n][h][w][c] on the device: y = relu(x + bias[c]) ([n][h][w][c]; may alias x), or
- * its pooled [n][h/2][w/2][c]. Arithmetic as PyTorch's half ops (the add in float, rounded to half).
- * bias: c fp16 values on the device; c a multiple of 8; pool needs even h and w; 16-byte aligned
- * pointers. Runs on the context's stream.
+ * its pooled [n][h/2][w/2][c]. Arithmetic as PyTorch's separate half-precision add / ReLU / max-pool ops
+ * (the add in float, rounded to half); a NaN sum becomes 0 (torch.relu would keep it).
+ * bias: bias_len fp16 values on the device, bias_len == c (FD_ERR_INVALID otherwise); c a multiple of 8;
+ * pool needs even h and w; 16-byte aligned pointers. Runs on the context's stream.
  */
-int fd_nn_bias_relu(fd_ctx *ctx, const void *x, const void *bias, void *y, int n, int h, int w, int c, int pool);
+int fd_nn_bias_relu(fd_ctx *ctx, const void *x, const void *bias, int64_t bias_len, void *y, int n, int h, int w,
+                    int c, int pool);
 
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);

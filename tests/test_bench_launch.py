@@ -27,6 +27,28 @@ def test_self_launch_two_ranks():
     assert sorted(x["rank"] for x in out["ranks"]) == [0, 1]
     assert sorted(x["device"] for x in out["ranks"]) == [0, 1]  # distinct devices
     assert len({x["pid"] for x in out["ranks"]}) == 2
+    assert out["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert all(x["device_count"] == 2 for x in out["ranks"])
+    # strong-scaled legs: the ranks' blocks partition each global batch (configs[3] 256, configs[4] 512)
+    for leg, total in out["strong_global_batch"].items():
+        spans = sorted(tuple(x["strong_blocks"][leg]) for x in out["ranks"])
+        assert spans[0][0] == 0 and spans[-1][1] == total and spans[0][1] == spans[1][0], (leg, spans)
+    assert out["strong_global_batch"] == {"config4_lsd_map": 256, "config5_superpoint": 512}
+
+
+def test_self_launch_four_ranks_strong_blocks():
+    """Four gloo ranks rehearse an N=4 scaling run: distinct devices, and each strong-scaled leg's
+    global batch split into four contiguous equal blocks."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], capture_output=True,
+                       text=True, timeout=240, env=_env(FD_BENCH_LAUNCH_CHECK_DEVICES="4"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert out["process_group"]["world_size"] == 4
+    assert sorted(x["device"] for x in out["ranks"]) == [0, 1, 2, 3]
+    for leg, total in out["strong_global_batch"].items():
+        spans = sorted(tuple(x["strong_blocks"][leg]) for x in out["ranks"])
+        assert [e - s for s, e in spans] == [total // 4] * 4
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
 
 
 def test_world_size_must_match_gpus():

@@ -102,6 +102,41 @@ def test_device_path_matches_host(fd, oracle):
         assert np.array_equal(idx[b, :len(hidx)].cpu().numpy(), hidx)
 
 
+@pytest.mark.parametrize("shape", [(120, 200), (67, 5), (33, 257), (40, 1920)])
+def test_pitched_maps(fd, oracle, shape):
+    """fd_lsd_map_pitched: the default device maps (rows padded to 16 entries: aligned row stores) and a
+    caller pitch (odd on purpose) equal the host path; the padding entries are never written."""
+    torch = pytest.importorskip("torch")
+    rows, cols = shape
+    frames = np.stack([oracle.make_frame("checker", 80 + i, rows, cols, 16) for i in range(2)]
+                      + [oracle.make_frame("noise", 90, rows, cols)])
+    host = fd.lsd_map(frames)
+    dev = torch.from_numpy(frames).cuda()
+    mr, mc = rows - 1, cols - 1
+    outs = [fd.lsd_map(dev)]
+    pitch = mc + 5
+    bufs = (torch.full((3, mr, pitch), 7.0, device="cuda"), torch.full((3, mr, pitch), 7.0, device="cuda"),
+            torch.full((3, mr, pitch), 7, dtype=torch.uint8, device="cuda"))
+    outs.append(fd.lsd_map(dev, out=tuple(t[..., :mc] for t in bufs) + (
+        torch.empty((3, mr * mc), dtype=torch.int32, device="cuda"), torch.empty((3,), dtype=torch.int64, device="cuda"))))
+    torch.cuda.synchronize()
+    assert outs[0][0].stride(1) % 16 == 0 and outs[0][0].stride(1) >= mc
+    for n, a, v, idx, cnt in outs:
+        for b in range(3):
+            hn, ha, hv, hidx = host[b]
+            assert np.array_equal(n[b].cpu().numpy().view(np.uint32), hn.view(np.uint32)), b
+            assert np.array_equal(a[b].cpu().numpy().view(np.uint32), ha.view(np.uint32)), b
+            assert np.array_equal(v[b].cpu().numpy(), hv), b
+            assert int(cnt[b]) == len(hidx)
+            assert np.array_equal(idx[b, :len(hidx)].cpu().numpy(), hidx), b
+    for t, fill in zip(bufs, (7.0, 7.0, 7)):
+        assert bool((t[..., mc:] == fill).all())  # padding untouched
+    with pytest.raises(Exception):  # a pitch below cols-1 is refused
+        bad = torch.empty((3, mr, mc), device="cuda").as_strided((3, mr, mc), (mr * (mc - 1), mc - 1, 1))
+        fd.lsd_map(dev, out=(bad, None, None, torch.empty((3, mr * mc), dtype=torch.int32, device="cuda"),
+                             torch.empty((3,), dtype=torch.int64, device="cuda")))
+
+
 def test_config4_batch_spot_check(fd, oracle):
     """BASELINE configs[3] shape (1920x1080 x256, the bench's 64-px checker + noise): the dense maps and
     the valid list of frames 0, 127 and 255 against the oracle, and every frame's count consistent."""
@@ -114,13 +149,10 @@ def test_config4_batch_spot_check(fd, oracle):
     base = torch.where(((r + c) % 2) == 1, 180, 60)
     noise = torch.randint(-10, 11, (n, rows, cols), generator=g, device="cuda", dtype=torch.int32)
     frames = (base + noise).clamp(0, 255).to(torch.uint8)
-    mr, mc = rows - 1, cols - 1
-    out = (torch.empty((n, mr, mc), device="cuda"), torch.empty((n, mr, mc), device="cuda"),
-           torch.empty((n, mr, mc), dtype=torch.uint8, device="cuda"),
-           torch.empty((n, mr * mc), dtype=torch.int32, device="cuda"), torch.empty((n,), dtype=torch.int64, device="cuda"))
-    nm, am, vm, idx, cnt = fd.lsd_map(frames, out=out)
+    nm, am, vm, idx, cnt = fd.lsd_map(frames)  # the bench's layout: row-padded (aligned) maps
     torch.cuda.synchronize()
-    assert torch.equal(cnt, vm.view(n, -1).sum(dim=1, dtype=torch.int64))
+    assert nm.stride(1) == 1920  # 1919 entries padded to 16
+    assert torch.equal(cnt, vm.sum(dim=(1, 2), dtype=torch.int64))
     host = frames.cpu().numpy()
     for b in (0, 127, 255):
         en, ea, ev, eidx = oracle.lsd_map(host[b])

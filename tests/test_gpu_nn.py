@@ -280,6 +280,18 @@ def test_bias_relu_matches_torch(sp):
         assert torch.equal(inplace, ref), c
     with pytest.raises(ValueError):
         sp.bias_relu(torch.zeros(1, 8, 4, 4, device="cuda"), torch.zeros(8, device="cuda"))  # fp32, not fp16
+    x8 = torch.zeros(1, 16, 4, 4, device="cuda", dtype=torch.float16).contiguous(memory_format=torch.channels_last)
+    with pytest.raises(ValueError):
+        sp.bias_relu(x8, torch.zeros(8, device="cuda", dtype=torch.float16))  # short bias
+    with pytest.raises(ValueError):
+        sp.bias_relu(x8, torch.zeros(16, device="cuda", dtype=torch.float16), pool=True, out=x8)  # out not pooled
+    import ctypes
+    from feature_detector_amd import _lib
+    ctx = sp._resolve_ctx(None, x8)
+    b16 = torch.zeros(16, device="cuda", dtype=torch.float16)
+    rc = _lib.load().fd_nn_bias_relu(ctx.ptr, ctypes.c_void_p(x8.data_ptr()), ctypes.c_void_p(b16.data_ptr()), 8,
+                                      ctypes.c_void_p(x8.data_ptr()), 1, 4, 4, 16, 0)
+    assert rc != 0  # the C ABI refuses a bias length that is not the channel count
     net = sp.build_net(0).cuda().eval().half().to(memory_format=torch.channels_last)
     frames = torch.randint(0, 256, (2, 1, 96, 128), generator=g, device="cuda", dtype=torch.int32)
     x = (frames.half() / 255.0).contiguous(memory_format=torch.channels_last)

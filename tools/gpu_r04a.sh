@@ -1,0 +1,14 @@
+# Round 4 session A: GPU tests + smoke on the in-tree library, then A/B of library builds under rocprofv3
+# (north-star response kernel, north-star detect) and the LSD dense map with padded vs unpadded rows.
+set -e
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
+bash tools/gpu_tests_smoke.sh
+bash tools/gpu_ab_libs.sh "northstar --kind shi_tomasi" abvar/base.so abvar/occ.so abvar/pkq.so abvar/base.so abvar/occ.so abvar/pkq.so > gpurun_out/ab_ns.txt 2>&1
+cat gpurun_out/ab_ns.txt
+bash tools/gpu_ab_libs.sh "nsdetect --kind shi_tomasi" abvar/base.so abvar/occ.so abvar/pkq.so > gpurun_out/ab_nsd.txt 2>&1
+cat gpurun_out/ab_nsd.txt
+bash tools/gpu_ab_libs.sh "lsd --kind dense_unpitched" feature_detector_amd/lib/libfdhip.so > gpurun_out/ab_lsd.txt 2>&1
+bash tools/gpu_ab_libs.sh "lsd --kind dense" feature_detector_amd/lib/libfdhip.so >> gpurun_out/ab_lsd.txt 2>&1
+bash tools/gpu_ab_libs.sh "lsd --kind dense_unpitched" feature_detector_amd/lib/libfdhip.so >> gpurun_out/ab_lsd.txt 2>&1
+bash tools/gpu_ab_libs.sh "lsd --kind dense" feature_detector_amd/lib/libfdhip.so >> gpurun_out/ab_lsd.txt 2>&1
+cat gpurun_out/ab_lsd.txt

@@ -7,7 +7,8 @@ fixed number of times, on seeded uniform-noise frames generated on the GPU.
   --shape fast720    fd_points_detect, FAST, 1280x720 batch 64 (BASELINE configs[2]), 10 calls
   --shape fastbrief  the same + BRIEF-256 on the detected keypoints (fd_brief_compute), 10 calls
   --shape lsd        fd_lsd_map (dense) and fd_lsd_lines (compact map + host stage), 1920x1080 batch 256,
-                     64-px checker + noise (BASELINE configs[3]), 3 calls each (--kind dense / compact: one)
+                     64-px checker + noise (BASELINE configs[3]), 3 calls each (--kind dense / compact: one;
+                     dense_unpitched: dense maps with unpadded rows)
 """
 import argparse
 import os
@@ -21,7 +22,7 @@ import feature_detector_amd as fd  # noqa: E402
 THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 p = argparse.ArgumentParser()
 p.add_argument("--shape", default="bench", choices=["bench", "northstar", "nsdetect", "fast720", "fast720r", "fastbrief", "lsd"])
-p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast", "dense", "compact"])
+p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast", "dense", "compact", "dense_unpitched"])
 p.add_argument("--calls", type=int, default=0)
 p.add_argument("--thr", type=float, default=None, help="response threshold override (e.g. 1e30: no candidates)")
 a = p.parse_args()
@@ -53,7 +54,16 @@ elif a.shape == "lsd":
     c = torch.arange(cols, device="cuda").view(1, 1, cols) // 64
     base = torch.where(((r + c) % 2) == 1, 180, 60)
     frames = (base + torch.randint(-10, 11, (n, rows, cols), generator=g, device="cuda", dtype=torch.int32)).clamp(0, 255).to(torch.uint8)
+    flat = None
+    if a.kind == "dense_unpitched":  # the dense maps without row padding (misaligned row stores)
+        mr, mc = rows - 1, cols - 1
+        flat = (torch.empty((n, mr, mc), device="cuda"), torch.empty((n, mr, mc), device="cuda"),
+                torch.empty((n, mr, mc), dtype=torch.uint8, device="cuda"),
+                torch.empty((n, mr * mc), dtype=torch.int32, device="cuda"), torch.empty((n,), dtype=torch.int64, device="cuda"))
     for _ in range(a.calls or 3):  # --kind dense / compact: one of the two only
+        if a.kind == "dense_unpitched":
+            fd.lsd_map(frames, out=flat)
+            continue
         if a.kind != "compact":
             fd.lsd_map(frames)
         if a.kind != "dense":
