@@ -267,18 +267,33 @@ def tie_frames(fd, dev, detector, frames_pool, need, dist):
     return tied, total
 
 
-def tie_report(torch, fd, dev, detector, frames_pool, need, dist, steps=10):
-    """The leg's tie count; when nonzero the same workload is also timed with ties="reference"
-    (un-captured: the re-selection reads the status words on the host)."""
+def tie_report(torch, fd, dev, detector, frames_pool, need, dist, steps=10, raster_ms=None):
+    """The leg's tie count; when nonzero the same workload is also timed with ties="reference" (the
+    reference's std::sort order on the GPU: k_select_reference emulates libstdc++'s introsort over the
+    visited prefix), replayed from a hipGraph like the raster steps, and the frames it had to leave to
+    the host (FD_FRAME_UNRESOLVED: the introsort's heapsort fallback) are counted."""
     tied, total = tie_frames(fd, dev, detector, frames_pool, need, dist)
     rep = {"tie_frames": tied, "frames_checked": total,
            "timed_order": "raster (equal to the reference order on every frame without FD_FRAME_TIES)"}
     if tied:
         b, rows, cols = frames_pool[0].shape
         secs, done, _, _ = run_config(torch, fd, dev, detector, rows, cols, b, len(frames_pool), need, dist, None,
-                                      steps, 2, False, 0, ties="reference", frames_pool=frames_pool)
-        rep["reference_order_ms_per_step"] = round(secs / done * 1e3, 5)
+                                      steps, 2, True, 0, ties="reference", frames_pool=frames_pool)
+        ms = secs / done * 1e3
+        rep["reference_order_ms_per_step"] = round(ms, 5)
         rep["reference_order_mpix_s"] = round(done * b * rows * cols / secs / 1e6, 1)
+        rep["reference_order_graph"] = True
+        if raster_ms:
+            rep["reference_vs_raster_step"] = round(ms / raster_ms, 3)
+        ctx = fd.default_context(dev.index or 0)
+        unresolved = resolved = 0
+        for f in frames_pool:
+            fd.detect_points(detector, f, need, dist, THR[detector], ctx=ctx, ties="reference")
+            st = ctx.frame_status(f.shape[0])
+            unresolved += int(((st & fd.points.FRAME_UNRESOLVED) != 0).sum())
+            resolved += int(((st & fd.points.FRAME_RESOLVED) != 0).sum())
+        rep["reference_resolved_on_gpu"] = resolved
+        rep["reference_unresolved_frames"] = unresolved
     return rep
 
 
@@ -360,7 +375,7 @@ def run_config3(torch, fd, dev, seed, batch=64, rows=720, cols=1280, need=200, d
     brief_ms = e0.elapsed_time(e1) / reps
     kp = int(cnt.sum().item())
     px = batch * rows * cols
-    ties = tie_report(torch, fd, dev, "fast", pool, need, dist, steps=4)
+    ties = tie_report(torch, fd, dev, "fast", pool, need, dist, steps=4, raster_ms=secs / done * 1e3)
     if "reference_order_ms_per_step" in ties:
         ties["reference_order_note"] = "detect + select only (no BRIEF)"
     return {
@@ -818,7 +833,7 @@ def main():
     traffic, traffic_src = (measured_traffic("bench_k_corner") if (args.detector == "harris" and args.rows == 480
                                                                      and args.cols == 640 and args.batch == 1)
                             else (None, None))
-    ties_headline = tie_report(torch, fd, dev, args.detector, pool, args.need, args.dist)
+    ties_headline = tie_report(torch, fd, dev, args.detector, pool, args.need, args.dist, raster_ms=ms_per_step)
     roofline = {"kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "bytes_per_launch": k_bytes, "avg_launch_ms": round(k_ms, 5), "note": dominant_note}
@@ -861,7 +876,7 @@ def main():
         with phase(torch, "north_star_kernel"):
             kms = kernel_time_ms(torch, fd, pool2, "shi_tomasi", 40.0, reps=10)
         with phase(torch, "north_star_ties"):
-            ties_ns = tie_report(torch, fd, dev, "shi_tomasi", pool2, 200, 20, steps=4)
+            ties_ns = tie_report(torch, fd, dev, "shi_tomasi", pool2, 200, 20, steps=4, raster_ms=s2 / d2 * 1e3)
         del pool2
         with phase(torch, "north_star_kernel_checker"):
             pool3 = [make_frames(torch, "checker", ns_batch, 1080, 1920, 199 + rank + 7919 * i, dev) for i in range(2)]

@@ -577,6 +577,8 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
                int32_t out_stride, int32_t *out_counts, int outputs_on_device, int frames_on_device) {
     fdk::SelectArgs s{};
     const int batch = q.batch, rows = q.rows, cols = q.cols;
+    if (q.cap >= (int64_t(1) << 30))  // k_select reads the lists through buffer resources (byte offsets < 2^32)
+        return fail(c, FD_ERR_INVALID, "candidate list capacity must be < 2^30 entries per frame");
     s.list_resp = as<float>(c->list_resp);
     s.list_idx = as<uint32_t>(c->list_idx);
     s.list_count = sb.list_count;

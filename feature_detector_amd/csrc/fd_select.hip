@@ -144,6 +144,16 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     const int64_t n = min(static_cast<int64_t>(a.list_count[f]), a.list_cap);
     const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
     const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    // List reads through buffer resources (list_cap < 2^30, checked on the host): a 32-bit byte offset
+    // per thread plus a uniform one in an SGPR, instead of a 64-bit address per unrolled load (those were
+    // hoisted out of the loops and spilled). Entries past the capacity read 0 (masked by i < n anyway).
+    const auto rres = make_rsrc(lresp, static_cast<uint32_t>(a.list_cap) * 4u);
+    const auto ridx = make_rsrc(lidx, static_cast<uint32_t>(a.list_cap) * 4u);
+    // (the whole byte offset in the VGPR operand: the hardware range check covers the VGPR offset only,
+    // an SGPR offset would be added after it, unchecked)
+    auto lload = [](__amdgpu_buffer_rsrc_t r, uint32_t vbyte) -> uint32_t {
+        return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(vbyte), 0, 0));
+    };
     const int d = a.dist;
     const bool use_grid = d >= 1 || (d == 0 && a.grid_at_d0);
     // Occupancy grid of (d+1)-sized cells with a one-cell border (no bounds checks in the scan).
@@ -302,9 +312,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             uint32_t ix[kPassUnroll];
 #pragma unroll
             for (int u = 0; u < kPassUnroll; ++u) {
-                const int64_t i = min(b0 + static_cast<int64_t>(u) * nthr, n - 1);
-                r[u] = lresp[i];
-                ix[u] = lidx[i];
+                const uint32_t vb = 4u * static_cast<uint32_t>(b0 + static_cast<int64_t>(u) * nthr);
+                r[u] = __uint_as_float(lload(rres, vb));
+                ix[u] = lload(ridx, vb);
             }
 #pragma unroll
             for (int u = 0; u < kPassUnroll; ++u) {
@@ -393,7 +403,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         for (; base < nn; base += kRegGather * step) {
             float rr[kRegGather];
 #pragma unroll
-            for (int k = 0; k < kRegGather; ++k) rr[k] = lresp[min(base + tid + k * step, nn - 1u)];
+            for (int k = 0; k < kRegGather; ++k) rr[k] = __uint_as_float(lload(rres, 4u * (base + tid + k * step)));
             round(rr, base);
         }
         __syncthreads();
@@ -401,7 +411,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         const int ns = min(static_cast<int>(staged), kSelectChunk);
         for (int j = tid; j < ns; j += nthr) {
             const uint64_t e = buf[j];
-            const uint32_t li = lidx[static_cast<uint32_t>(e)];
+            const uint32_t li = lload(ridx, 4u * static_cast<uint32_t>(e));
             sup[j] = make_key(__uint_as_float(static_cast<uint32_t>(e >> 32)), li, a);
         }
         __syncthreads();  // sup complete; gcount read by every thread before anyone reuses it
@@ -421,7 +431,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         for (uint32_t base = 0; base < nn; base += kWideReg * step) {
             float rr[kWideReg];
 #pragma unroll
-            for (int k = 0; k < kWideReg; ++k) rr[k] = lresp[min(base + tid + k * step, nn - 1u)];
+            for (int k = 0; k < kWideReg; ++k) rr[k] = __uint_as_float(lload(rres, 4u * (base + tid + k * step)));
             uint32_t hm = 0;
 #pragma unroll
             for (int k = 0; k < kWideReg; ++k) {
@@ -457,7 +467,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
 #pragma unroll
             for (int k = 0; k < kPer; ++k) e[k] = i0 + k * step < staged ? wk[i0 + k * step] : 0ull;
 #pragma unroll
-            for (int k = 0; k < kPer; ++k) li[k] = i0 + k * step < staged ? lidx[static_cast<uint32_t>(e[k])] : 0u;
+            for (int k = 0; k < kPer; ++k) li[k] = lload(ridx, 4u * static_cast<uint32_t>(e[k]));
 #pragma unroll
             for (int k = 0; k < kPer; ++k)
                 if (i0 + k * step < staged)
@@ -525,8 +535,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 if (r == 0 && e < static_cast<uint32_t>(kSegHead)) {
                     kv[k] = pre_key[k];
                 } else {
-                    const int64_t li = min(static_cast<int64_t>(sd.x) + e, a.list_cap - 1);
-                    kv[k] = in ? make_key(lresp[li], lidx[li], a) : 0ull;
+                    const uint32_t lb = 4u * (sd.x + e);
+                    const uint64_t key = make_key(__uint_as_float(lload(rres, lb)), lload(ridx, lb), a);
+                    kv[k] = in ? key : 0ull;
                 }
                 ge[k] = in && static_cast<uint32_t>(kv[k] >> 32) >= k32lo;
                 hit[k] = ge[k] && static_cast<uint32_t>(kv[k] >> 32) <= k32hi;  // (later chunks: skip earlier ones)
@@ -694,10 +705,10 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 float r[kPassUnroll];
                 uint32_t ix[kPassUnroll];
 #pragma unroll
-                for (int u = 0; u < kPassUnroll; ++u) {  // unconditional (clamped) loads: all in flight
-                    const int64_t i = min(b0 + static_cast<int64_t>(u) * nthr + lane, n - 1);
-                    r[u] = lresp[i];
-                    ix[u] = lidx[i];
+                for (int u = 0; u < kPassUnroll; ++u) {  // unconditional loads: all in flight
+                    const uint32_t vb = 4u * static_cast<uint32_t>(b0 + static_cast<int64_t>(u) * nthr + lane);
+                    r[u] = __uint_as_float(lload(rres, vb));
+                    ix[u] = lload(ridx, vb);
                 }
 #pragma unroll
                 for (int u = 0; u < kPassUnroll; ++u) {

@@ -6,6 +6,6 @@ rc=0
 timeout -k 10 700 python3 -u -m pytest ${@:-tests} -m gpu -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/tests.log 2>&1 || rc=$?
 tail -40 gpurun_out/tests.log
-test $rc -eq 0
+[ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 cat gpurun_out/smoke.log
