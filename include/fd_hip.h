@@ -199,7 +199,8 @@ int fd_lsd_map(fd_ctx *ctx, const uint8_t *frames, int frames_on_device, int bat
 /*
  * fd_lsd_map_pitched -- fd_lsd_map with dense maps of row pitch map_pitch entries (>= cols-1): row r of
  * frame b's maps starts at entry (b * (rows-1) + r) * map_pitch of norm / angle / valid (entries past
- * cols-2 in a row are left untouched). The map indices in valid_idx stay row * (cols-1) + col. With a
+ * cols-2 in a row are left untouched, except that frames too small to scan -- rows or cols < 4 -- get
+ * their maps cleared whole). The map indices in valid_idx stay row * (cols-1) + col. With a
  * pitch that is a multiple of 16 entries every map row starts 64-byte (f32) / 16-byte (u8) aligned and
  * the map kernel's row stores are aligned (the faster layout for device outputs; host outputs are
  * always computed that way and copied to the caller's pitch). fd_lsd_map = map_pitch cols-1.
