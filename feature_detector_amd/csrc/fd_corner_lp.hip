@@ -71,6 +71,18 @@ __device__ __forceinline__ f2 corner_response_fp(f2 sxx, f2 syy, f2 sxy, float t
         gate = a + c;
         const f2 d = a - c;
         r = gate + sqrt_rn_rsq2(__builtin_elementwise_fma(b * b, f2{4.0f, 4.0f}, d * d));
+#if FD_LP_GFMA
+        // The gate as a clamp: min(2r, fl(66 gate - 64 thr)). gate > thr: 66g - 64t = 2g + 64(g - t) >=
+        // 2g + 32 ulp(g) > 2r (the tensor is positive semidefinite, so sqrt(d^2 + 4b^2) <= gate up to ~6
+        // ulp of rounding), i.e. 2r itself. gate <= thr: the value is <= 2 gate <= 2 thr, which neither
+        // wins the NMS (it needs > 2 thr) nor changes a neighbour's outcome (a winner exceeds 2 thr, so it
+        // exceeds this value exactly when it exceeds the reference's 0). Winners keep their exact 2r.
+        const f2 cl = __builtin_elementwise_fma(gate, f2{66.0f, 66.0f}, f2{-64.0f * thr, -64.0f * thr});
+        f2 res;
+        res.x = __builtin_fminf(r.x, cl.x);
+        res.y = __builtin_fminf(r.y, cl.y);
+        return res;
+#endif
     }
     const f2 g = f2{thr, thr} - gate;  // < 0 exactly when gate > thr
     f2 res;
@@ -83,7 +95,10 @@ __device__ __forceinline__ f2 corner_response_fp(f2 sxx, f2 syy, f2 sxy, float t
 #define FD_LP_FP 1
 #endif
 #ifndef FD_LP_PKQ
-#define FD_LP_PKQ 0
+#define FD_LP_PKQ 1
+#endif
+#ifndef FD_LP_GFMA
+#define FD_LP_GFMA 1
 #endif
 
 // ---------------------------------------------------------------------------------------------------
