@@ -9,6 +9,11 @@
 
 #include <type_traits>
 
+// Shi-Tomasi's gate as a clamp (corner_response_fp; A/B switch)
+#ifndef FD_LP_GFMA
+#define FD_LP_GFMA 1
+#endif
+
 namespace fdk {
 
 namespace {
@@ -97,9 +102,7 @@ __device__ __forceinline__ f2 corner_response_fp(f2 sxx, f2 syy, f2 sxy, float t
 #ifndef FD_LP_PKQ
 #define FD_LP_PKQ 1
 #endif
-#ifndef FD_LP_GFMA
-#define FD_LP_GFMA 1
-#endif
+
 
 // ---------------------------------------------------------------------------------------------------
 // K1 (list mode, lane-private emission): the per-pixel kernel of fd_points_detect / fd_points_response.
