@@ -40,6 +40,8 @@ constexpr int kRefThreads = 1024;
 constexpr int kRefWaves = kRefThreads / kWave;
 constexpr int kRefMaxRanges = 256;  // unresolved ranges (> 16) in the list; bound: DESIGN.md
 constexpr int kRefLeaf = 16;        // libstdc++ _S_threshold
+constexpr int kRefU = 4;            // 64-element rounds per wave whose global loads are issued together
+constexpr uint32_t kRefRidCap = 8192;  // flat elements per level whose range index pass 1 caches for passes 2-4
 constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 
 struct alignas(16) RefLds {
@@ -62,6 +64,7 @@ struct alignas(16) RefLds {
     // leaves produced by the level
     uint32_t leaf_lo[2 * kRefMaxRanges], leaf_hi[2 * kRefMaxRanges];
     uint32_t wsum[kRefWaves];
+    uint16_t rid[kRefRidCap];  // levels with T <= kRefRidCap: each element's active range (set by pass 1)
     int cur, m_all, m_act, n_leaf, fail;
     uint32_t T, fin;
     int s_done, s_acc;
@@ -162,6 +165,21 @@ __device__ __forceinline__ void set_active(RefLds &L, uint32_t win_end) {
     }
 }
 
+// Diagnostic phase clocks (SelectArgs::stamps, FD_SELECT_STAMPS): thread 0 adds the cycles since the
+// previous mark to slot k of the frame's stamps (slots 16-23; k_select uses 0-15).
+#define FD_REF_MARK(k)                                                                  \
+    do {                                                                                \
+        if (a.stamps && tid == 0) {                                                     \
+            const uint64_t now_ = __builtin_readcyclecounter();                         \
+            a.stamps[static_cast<int64_t>(f) * 32 + (k)] += now_ - t_mark;              \
+            t_mark = now_;                                                              \
+        }                                                                               \
+    } while (0)
+#define FD_REF_COUNT(k, v)                                                              \
+    do {                                                                                \
+        if (a.stamps && tid == 0) a.stamps[static_cast<int64_t>(f) * 32 + (k)] += (v);  \
+    } while (0)
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortArgs r) {
     static_assert(NT == kRefThreads, "k_select_reference runs 1024 threads");
@@ -169,49 +187,104 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
     const int f = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
     const uint32_t st0 = a.status[f];
     if (!(st0 & FD_FRAME_TIES) || (st0 & FD_FRAME_GUARD)) return;
+    uint64_t t_mark = a.stamps && tid == 0 ? __builtin_readcyclecounter() : 0ull;
+    if (a.stamps && tid == 0)
+        for (int k = 16; k < 32; ++k) a.stamps[static_cast<int64_t>(f) * 32 + k] = 0;  // (k_select's probe slots)
     const uint32_t n = static_cast<uint32_t>(min(static_cast<int64_t>(a.cand_n[f]), a.list_cap));
     const int rows = a.rows, cols = a.cols, d = a.dist;
     const uint32_t npx = static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols);
     const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
     const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
     uint2 *X = r.x + static_cast<int64_t>(f) * r.cap;
+    const uint32_t *Xr = reinterpret_cast<const uint32_t *>(X);  // X[p].x (response bits) = Xr[2p]
     uint32_t *lpos = r.lpos + static_cast<int64_t>(f) * r.cap;
     uint32_t *rpos = r.rpos + static_cast<int64_t>(f) * r.cap;
     uint32_t *ord = r.ord + static_cast<int64_t>(f) * r.cap;
 
     // ---- 1. the push order -------------------------------------------------------------------------
+    // (every per-candidate loop loads kRefPush candidates' data before using any: one memory round trip
+    // per kRefPush candidates instead of one or two per candidate)
+    constexpr int kRefPush = 8;
     if (r.push_order) {
-        for (uint32_t i = tid; i < n; i += NT) X[i] = make_uint2(__float_as_uint(lresp[i]), lidx[i]);
+        for (uint32_t i0 = tid; i0 < n; i0 += kRefPush * NT) {
+            float rv[kRefPush];
+            uint32_t qv[kRefPush];
+#pragma unroll
+            for (int k = 0; k < kRefPush; ++k) {
+                const uint32_t i = min(i0 + k * NT, n - 1u);
+                rv[k] = lresp[i];
+                qv[k] = lidx[i];
+            }
+#pragma unroll
+            for (int k = 0; k < kRefPush; ++k)
+                if (i0 + k * NT < n) X[i0 + k * NT] = make_uint2(__float_as_uint(rv[k]), qv[k]);
+        }
     } else {
-        // raster order of unique pixel indices: bitmap (in lpos), word prefix (in rpos), rank = prefix +
-        // set bits below. The bitmap words are read with device-scope loads (the atomics bypass L1).
+        // Raster order of unique pixel indices, a part of the frame at a time: the part's candidate bitmap
+        // in LDS (the greedy's arrays, pxy .. grid_lds, are free until the grid is initialised below; LDS
+        // atomics instead of one global atomic per candidate, which one CU issues slowly), its word prefix
+        // (offset by the earlier parts' candidates) in rpos, rank = prefix + set bits below.
+        static_assert(offsetof(RefLds, pcell) == offsetof(RefLds, pxy) + sizeof(L.pxy) &&
+                          offsetof(RefLds, cmask) == offsetof(RefLds, pcell) + sizeof(L.pcell) &&
+                          offsetof(RefLds, grid_lds) == offsetof(RefLds, cmask) + sizeof(L.cmask),
+                      "bitmap span: pxy .. grid_lds contiguous");
+        constexpr uint32_t kPartWords = (sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask) + sizeof(L.grid_lds)) / 4;
+        uint32_t *const lbits = L.pxy;
+        uint32_t *const wpre = rpos;
         const uint32_t words = (npx + 31u) >> 5;
-        uint32_t *bits = lpos, *wpre = rpos;
-        for (uint32_t w = tid; w < words; w += NT) bits[w] = 0u;
-        __syncthreads();
-        for (uint32_t i = tid; i < n; i += NT) {
-            const uint32_t q = lidx[i];
-            if (q < npx) atomicOr(&bits[q >> 5], 1u << (q & 31u));
-        }
-        __syncthreads();
-        const uint32_t per = (words + NT - 1) / NT;
-        const uint32_t w0 = min(words, tid * per), w1 = min(words, w0 + per);
-        uint32_t cnt = 0;
-        for (uint32_t w = w0; w < w1; ++w)
-            cnt += __popc(__hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        uint32_t tot;
-        uint32_t base = block_excl(cnt, L.wsum, tot);
-        for (uint32_t w = w0; w < w1; ++w) {
-            wpre[w] = base;
-            base += __popc(__hip_atomic_load(&bits[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        }
-        __syncthreads();
-        for (uint32_t i = tid; i < n; i += NT) {
-            const uint32_t q = lidx[i];
-            if (q >= npx) continue;  // (guarded upstream: k_select trips FD_FRAME_GUARD)
-            const uint32_t bw = __hip_atomic_load(&bits[q >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t rk = wpre[q >> 5] + __popc(bw & ((1u << (q & 31u)) - 1u));
-            X[FD_REF_IDX(rk, n, 1)] = make_uint2(__float_as_uint(lresp[i]), q);
+        uint32_t carry = 0;  // candidates in the earlier parts
+        for (uint32_t pw0 = 0; pw0 < words; pw0 += kPartWords) {
+            const uint32_t pw = min(kPartWords, words - pw0);
+            for (uint32_t w = tid; w < pw; w += NT) lbits[w] = 0u;
+            __syncthreads();
+            for (uint32_t i0 = tid; i0 < n; i0 += kRefPush * NT) {
+                uint32_t qv[kRefPush];
+#pragma unroll
+                for (int k = 0; k < kRefPush; ++k) qv[k] = lidx[min(i0 + k * NT, n - 1u)];
+#pragma unroll
+                for (int k = 0; k < kRefPush; ++k) {
+                    const uint32_t wl = (qv[k] >> 5) - pw0;  // (wraps past the part when below it)
+                    if (i0 + k * NT < n && qv[k] < npx && wl < pw) atomicOr(&lbits[wl], 1u << (qv[k] & 31u));
+                }
+            }
+            __syncthreads();
+            // word prefix: a run of consecutive words per thread
+            const uint32_t per = (pw + NT - 1) / NT;
+            const uint32_t w0 = min(pw, tid * per), w1 = min(pw, w0 + per);
+            uint32_t cnt = 0;
+            for (uint32_t w = w0; w < w1; ++w) cnt += __popc(lbits[w]);
+            uint32_t tot;
+            uint32_t base = carry + block_excl(cnt, L.wsum, tot);
+            for (uint32_t w = w0; w < w1; ++w) {
+                wpre[pw0 + w] = base;
+                base += __popc(lbits[w]);
+            }
+            carry += tot;
+            __syncthreads();  // (the prefix stores are read back by other threads: same workgroup, L1-coherent
+                              // through the barrier's release/acquire)
+            for (uint32_t i0 = tid; i0 < n; i0 += kRefPush * NT) {
+                uint32_t qv[kRefPush], wp[kRefPush];
+                float rv[kRefPush];
+#pragma unroll
+                for (int k = 0; k < kRefPush; ++k) {
+                    const uint32_t i = min(i0 + k * NT, n - 1u);
+                    qv[k] = lidx[i];
+                    rv[k] = lresp[i];
+                }
+#pragma unroll
+                for (int k = 0; k < kRefPush; ++k) {
+                    const uint32_t wl = min((qv[k] >> 5) - pw0, pw - 1u);
+                    wp[k] = wpre[pw0 + wl];
+                }
+#pragma unroll
+                for (int k = 0; k < kRefPush; ++k) {
+                    const uint32_t q = qv[k], wl = (q >> 5) - pw0;
+                    if (i0 + k * NT >= n || q >= npx || wl >= pw) continue;
+                    const uint32_t rk = wp[k] + __popc(lbits[wl] & ((1u << (q & 31u)) - 1u));
+                    X[FD_REF_IDX(rk, n, 1)] = make_uint2(__float_as_uint(rv[k]), q);
+                }
+            }
+            __syncthreads();  // lbits reused by the next part (and the grid below)
         }
     }
 
@@ -252,6 +325,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         }
     }
     __syncthreads();
+    FD_REF_MARK(16);  // push order (bitmap, ranks, scatter) + grid init
     if (wv == 0) set_active(L, kSelectChunk);
     __syncthreads();
 
@@ -274,31 +348,54 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 L.K[tid] = 0;
             }
             __syncthreads();
+            FD_REF_MARK(24);  // pivots
             if (L.fail) break;
             const uint32_t T = L.T;
+            const bool cached = T <= kRefRidCap;  // passes 2-4 read the range index pass 1 stored
             const uint32_t blk = ((T + kRefWaves * kWave - 1) / (kRefWaves * kWave)) * kWave;
             const uint32_t e0 = min(T, wv * blk), e1 = min(T, e0 + blk);
-            // pass 1: stopper counts per wave, local prefixes at the range heads
+            // pass 1: stopper counts per wave, local prefixes at the range heads. Each wave walks its block
+            // kRefU rounds of 64 elements at a time: the rounds' element positions first (LDS), then all
+            // their response loads at once, then the ballots in order (one global round trip per kRefU
+            // rounds instead of one per round).
             {
                 uint32_t cl = 0, cr = 0;
                 int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
-                for (uint32_t b = e0; b < e1; b += kWave) {
-                    const uint32_t e = b + lane;
-                    const bool valid = e < e1;
-                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
-                    const uint32_t p = L.r_lo[c][j] + 1u + (e - L.o[j]);
-                    const float rv = valid ? as_f(X[FD_REF_IDX(p, n, 5)].x) : 0.0f;
-                    const float pv = L.piv[j];
-                    const bool ls = valid && rv <= pv, rs = valid && rv >= pv;
-                    const uint64_t bl = ballot(ls), br = ballot(rs);
-                    if (valid && e == L.o[j]) {
-                        L.headL[j] = cl + mbcnt64(bl, 0);
-                        L.headR[j] = cr + mbcnt64(br, 0);
-                        L.headW[j] = wv;
+                for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
+                    uint32_t pu[kRefU];
+                    int ju[kRefU];
+                    bool vu[kRefU];
+                    float ru[kRefU];
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t b = b0 + u * kWave, e = b + lane;
+                        vu[u] = e < e1;
+                        while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                        ju[u] = vu[u] ? range_of(L.o, m, jw, e) : jw;
+                        pu[u] = L.r_lo[c][ju[u]] + 1u + (e - L.o[ju[u]]);
                     }
-                    cl += popc64(bl);
-                    cr += popc64(br);
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) ru[u] = vu[u] ? as_f(Xr[2u * FD_REF_IDX(pu[u], n, 5)]) : 0.0f;
+                    if (T <= kRefRidCap) {
+#pragma unroll
+                        for (int u = 0; u < kRefU; ++u)
+                            if (vu[u]) L.rid[b0 + u * kWave + lane] = static_cast<uint16_t>(ju[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t e = b0 + u * kWave + lane;
+                        const int j = ju[u];
+                        const float pv = L.piv[j];
+                        const bool ls = vu[u] && ru[u] <= pv, rs = vu[u] && ru[u] >= pv;
+                        const uint64_t bl = ballot(ls), br = ballot(rs);
+                        if (vu[u] && e == L.o[j]) {
+                            L.headL[j] = cl + mbcnt64(bl, 0);
+                            L.headR[j] = cr + mbcnt64(br, 0);
+                            L.headW[j] = wv;
+                        }
+                        cl += popc64(bl);
+                        cr += popc64(br);
+                    }
                 }
                 if (lane == 0) {
                     L.waveL[wv] = cl;
@@ -306,6 +403,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 }
             }
             __syncthreads();
+            FD_REF_MARK(25);  // pass 1
             // per range: global stopper bases and counts
             uint32_t wbL, wbR;  // exclusive wave prefixes, lane i = wave i
             {
@@ -337,66 +435,138 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 }
             }
             __syncthreads();
-            // pass 2: scatter stopper positions by rank (left stoppers from the left, right from the right)
+            FD_REF_MARK(26);  // stopper bases
+            // pass 2: scatter stopper positions by rank (left stoppers from the left, right from the right);
+            // the same kRefU-round walk as pass 1
             {
                 const uint32_t mywbL = static_cast<uint32_t>(__shfl(static_cast<int>(wbL), wv));
                 const uint32_t mywbR = static_cast<uint32_t>(__shfl(static_cast<int>(wbR), wv));
                 uint32_t cl = mywbL, cr = mywbR;
-                int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
-                for (uint32_t b = e0; b < e1; b += kWave) {
-                    const uint32_t e = b + lane;
-                    const bool valid = e < e1;
-                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
-                    const uint32_t oj = L.o[j];
-                    const uint32_t p = L.r_lo[c][j] + 1u + (e - oj);
-                    const float rv = valid ? as_f(X[FD_REF_IDX(p, n, 6)].x) : 0.0f;
-                    const float pv = L.piv[j];
-                    const bool ls = valid && rv <= pv, rs = valid && rv >= pv;
-                    const uint64_t bl = ballot(ls), br = ballot(rs);
-                    if (ls) {
-                        const uint32_t rankL = static_cast<uint32_t>(mbcnt64(bl, 0)) + cl - L.bL[j];  // 0-based
-                        lpos[FD_REF_IDX(oj + rankL, L.T, 7)] = p;
+                int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
+                for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
+                    uint32_t pu[kRefU];
+                    int ju[kRefU];
+                    bool vu[kRefU];
+                    float ru[kRefU];
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t b = b0 + u * kWave, e = b + lane;
+                        vu[u] = e < e1;
+                        if (cached) {
+                            ju[u] = vu[u] ? L.rid[e] : 0;
+                        } else {
+                            while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                            ju[u] = vu[u] ? range_of(L.o, m, jw, e) : jw;
+                        }
+                        pu[u] = L.r_lo[c][ju[u]] + 1u + (e - L.o[ju[u]]);
                     }
-                    if (rs) {
-                        const uint32_t rankR = L.eR[j] - (static_cast<uint32_t>(mbcnt64(br, 0)) + cr) - 1u;  // 0-based from the right
-                        rpos[FD_REF_IDX(oj + rankR, L.T, 8)] = p;
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) ru[u] = vu[u] ? as_f(Xr[2u * FD_REF_IDX(pu[u], n, 6)]) : 0.0f;
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const int j = ju[u];
+                        const uint32_t oj = L.o[j], p = pu[u];
+                        const float pv = L.piv[j];
+                        const bool ls = vu[u] && ru[u] <= pv, rs = vu[u] && ru[u] >= pv;
+                        const uint64_t bl = ballot(ls), br = ballot(rs);
+                        if (ls) {
+                            const uint32_t rankL = static_cast<uint32_t>(mbcnt64(bl, 0)) + cl - L.bL[j];  // 0-based
+                            lpos[FD_REF_IDX(oj + rankL, L.T, 7)] = p;
+                        }
+                        if (rs) {
+                            const uint32_t rankR = L.eR[j] - (static_cast<uint32_t>(mbcnt64(br, 0)) + cr) - 1u;  // from the right
+                            rpos[FD_REF_IDX(oj + rankR, L.T, 8)] = p;
+                        }
+                        cl += popc64(bl);
+                        cr += popc64(br);
                     }
-                    cl += popc64(bl);
-                    cr += popc64(br);
                 }
             }
             __syncthreads();
-            // pass 3: K = number of pairs with l_k < r_k (monotone in k: the last true k writes it)
+            FD_REF_MARK(27);  // pass 2
+            // pass 3: K = number of pairs with l_k < r_k (monotone in k: the last true k writes it); the
+            // kRefU rounds' stopper positions loaded together
             {
-                int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
-                for (uint32_t b = e0; b < e1; b += kWave) {
-                    const uint32_t e = b + lane;
-                    const bool valid = e < e1;
-                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
-                    const uint32_t k = e - L.o[j];  // 0-based pair index
-                    const uint32_t mn = min(L.nL[j], L.nR[j]);
-                    const bool t = valid && k < mn && lpos[FD_REF_IDX(e, L.T, 9)] < rpos[FD_REF_IDX(e, L.T, 9)];
-                    const bool tn = t && k + 1 < mn && lpos[FD_REF_IDX(e + 1, L.T, 10)] < rpos[FD_REF_IDX(e + 1, L.T, 10)];
-                    if (t && !tn) L.K[j] = k + 1;
+                int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
+                for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
+                    int ju[kRefU];
+                    bool vu[kRefU];
+                    uint32_t l0[kRefU], r0[kRefU], l1[kRefU], r1[kRefU];
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t b = b0 + u * kWave, e = b + lane;
+                        vu[u] = e < e1;
+                        if (cached) {
+                            ju[u] = vu[u] ? L.rid[e] : 0;
+                        } else {
+                            while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                            ju[u] = vu[u] ? range_of(L.o, m, jw, e) : jw;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t e = b0 + u * kWave + lane;
+                        // (clamped reads: entries past T are never used)
+                        l0[u] = lpos[FD_REF_IDX(min(e, L.T - 1u), L.T, 9)];
+                        r0[u] = rpos[FD_REF_IDX(min(e, L.T - 1u), L.T, 9)];
+                        l1[u] = lpos[FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10)];
+                        r1[u] = rpos[FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10)];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t e = b0 + u * kWave + lane;
+                        const int j = ju[u];
+                        const uint32_t k = e - L.o[j];  // 0-based pair index
+                        const uint32_t mn = min(L.nL[j], L.nR[j]);
+                        const bool t = vu[u] && k < mn && l0[u] < r0[u];
+                        const bool tn = t && k + 1 < mn && l1[u] < r1[u];
+                        if (t && !tn) L.K[j] = k + 1;
+                    }
                 }
             }
             __syncthreads();
-            // pass 4: the swaps; the cuts
+            FD_REF_MARK(28);  // pass 3
+            // pass 4: the swaps; the cuts (the kRefU rounds' stopper positions, then their elements, loaded
+            // together)
             {
-                int jw = e0 < e1 ? range_search(L.o, m, e0) : 0;
-                for (uint32_t b = e0; b < e1; b += kWave) {
-                    const uint32_t e = b + lane;
-                    const bool valid = e < e1;
-                    while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                    const int j = valid ? range_of(L.o, m, jw, e) : jw;
-                    const uint32_t k = e - L.o[j];
-                    if (valid && k < L.K[j]) {
-                        const uint32_t pl = FD_REF_IDX(lpos[FD_REF_IDX(e, L.T, 11)], n, 12), pr = FD_REF_IDX(rpos[FD_REF_IDX(e, L.T, 11)], n, 13);
-                        const uint2 vl = X[pl], vr = X[pr];
-                        X[pl] = vr;
-                        X[pr] = vl;
+                int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
+                for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
+                    bool su[kRefU];
+                    uint32_t pl[kRefU], pr[kRefU];
+                    uint2 vl[kRefU], vr[kRefU];
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t b = b0 + u * kWave, e = b + lane;
+                        const bool valid = e < e1;
+                        int j;
+                        if (cached) {
+                            j = valid ? L.rid[e] : 0;
+                        } else {
+                            while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                            j = valid ? range_of(L.o, m, jw, e) : jw;
+                        }
+                        const uint32_t k = e - L.o[j];
+                        su[u] = valid && k < L.K[j];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        const uint32_t e = b0 + u * kWave + lane;
+                        pl[u] = su[u] ? FD_REF_IDX(lpos[FD_REF_IDX(e, L.T, 11)], n, 12) : 0u;
+                        pr[u] = su[u] ? FD_REF_IDX(rpos[FD_REF_IDX(e, L.T, 11)], n, 13) : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        if (su[u]) {
+                            vl[u] = X[pl[u]];
+                            vr[u] = X[pr[u]];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < kRefU; ++u) {
+                        if (su[u]) {
+                            X[pl[u]] = vr[u];
+                            X[pr[u]] = vl[u];
+                        }
                     }
                 }
                 if (tid < m) {
@@ -408,6 +578,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 }
             }
             __syncthreads();
+            FD_REF_MARK(29);  // pass 4
             // children: ranges > 16 into the next list (in order), the rest are leaves
             if (wv == 0) {
                 const int nc = c ^ 1;
@@ -476,28 +647,31 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 set_active(L, L.fin + kSelectChunk);
             }
             __syncthreads();
+            FD_REF_MARK(30);  // children + active prefix
+            FD_REF_COUNT(18, 1u);
+            FD_REF_COUNT(19, T);
             if (L.fail) break;
         }
         // ---- leaves: the final insertion sort (stable, response descending) into the visiting order ---
-        if (tid < L.n_leaf) {
-            const uint32_t lo = L.leaf_lo[tid], hi = L.leaf_hi[tid];
+        // 16 lanes per leaf: lane q holds element q and counts the elements that precede it
+        for (int lf0 = 0; lf0 < L.n_leaf; lf0 += NT / kRefLeaf) {
+            const int lf = lf0 + tid / kRefLeaf, q = tid % kRefLeaf;
+            const bool have_leaf = lf < L.n_leaf;
+            const uint32_t lo = have_leaf ? L.leaf_lo[lf] : 0u, hi = have_leaf ? L.leaf_hi[lf] : 0u;
             const int len = min(static_cast<int>(hi - lo), kRefLeaf);
-            uint2 v[kRefLeaf];
+            const bool mine = have_leaf && q < len;
+            const uint2 v = mine ? X[FD_REF_IDX(lo + q, n, 16)] : make_uint2(0u, 0u);
+            const float ri = as_f(v.x);
+            uint32_t rk = 0;
 #pragma unroll
-            for (int i = 0; i < kRefLeaf; ++i) v[i] = i < len ? X[FD_REF_IDX(lo + i, n, 16)] : make_uint2(0u, 0u);
-#pragma unroll
-            for (int i = 0; i < kRefLeaf; ++i) {
-                const float ri = as_f(v[i].x);
-                uint32_t rk = 0;
-#pragma unroll
-                for (int q = 0; q < kRefLeaf; ++q) {
-                    const float rq = as_f(v[q].x);
-                    rk += (q < len && (rq > ri || (rq == ri && q < i))) ? 1u : 0u;
-                }
-                if (i < len) ord[FD_REF_IDX(lo + rk, n, 17)] = v[i].y;
+            for (int t = 0; t < kRefLeaf; ++t) {  // lane group's element t (every lane of the wave takes part)
+                const float rt = as_f(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), (lane & ~(kRefLeaf - 1)) + t)));
+                rk += (t < len && (rt > ri || (rt == ri && t < q))) ? 1u : 0u;
             }
+            if (mine) ord[FD_REF_IDX(lo + rk, n, 17)] = v.y;
         }
         __syncthreads();
+        FD_REF_MARK(20);  // leaves
         if (tid == 0) L.n_leaf = 0;
         if (L.m_act > 0) {
             __syncthreads();
@@ -538,6 +712,8 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             }
             __syncthreads();
         }
+        FD_REF_MARK(21);  // greedy over the finished window
+        FD_REF_COUNT(22, 1u);
         if (L.s_done || fin_new >= n) break;
         if (wv == 0) {
             if (lane == 0) L.fin = fin_new;
