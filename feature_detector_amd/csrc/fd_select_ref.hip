@@ -32,6 +32,8 @@
 // gets FD_FRAME_UNRESOLVED and keeps k_select's features (the host resolves it when it synchronises).
 #include "fd_greedy.h"
 
+#include <type_traits>
+
 namespace fdk {
 
 namespace {
@@ -298,8 +300,9 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
     const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
     const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
     const uint32_t s1 = static_cast<uint32_t>(d + 1);
-    if (use_grid)
-        for (int i = tid; i < cells; i += NT) grid[i] = grid_empty(rows, cols, d);
+    // The grid is initialised just before the first greedy scan: until then its LDS (with pxy .. cmask)
+    // holds the partition levels' element copies and stopper positions (LDS mode below).
+    bool grid_ready = false;
     if (tid == 0) {
         L.s_done = 0;
         L.s_acc = 0;
@@ -352,6 +355,13 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             if (L.fail) break;
             const uint32_t T = L.T;
             const bool cached = T <= kRefRidCap;  // passes 2-4 read the range index pass 1 stored
+            // LDS mode (small levels before the first greedy scan): pass 1 also keeps each element's
+            // response in LDS (RV) and the stopper positions live in LDS (LP, RP) instead of lpos / rpos:
+            // passes 2 and 3 make no memory round trip, pass 4 one (the swaps themselves).
+            const bool ldsm = cached && !grid_ready;
+            uint32_t *const RV = L.pxy;  // [kRefRidCap] x 3 over pxy .. grid_lds (96 KiB, see the push)
+            uint32_t *const LP = RV + kRefRidCap;
+            uint32_t *const RP = LP + kRefRidCap;
             const uint32_t blk = ((T + kRefWaves * kWave - 1) / (kRefWaves * kWave)) * kWave;
             const uint32_t e0 = min(T, wv * blk), e1 = min(T, e0 + blk);
             // pass 1: stopper counts per wave, local prefixes at the range heads. Each wave walks its block
@@ -376,10 +386,13 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                     }
 #pragma unroll
                     for (int u = 0; u < kRefU; ++u) ru[u] = vu[u] ? as_f(Xr[2u * FD_REF_IDX(pu[u], n, 5)]) : 0.0f;
-                    if (T <= kRefRidCap) {
+                    if (cached) {
 #pragma unroll
                         for (int u = 0; u < kRefU; ++u)
-                            if (vu[u]) L.rid[b0 + u * kWave + lane] = static_cast<uint16_t>(ju[u]);
+                            if (vu[u]) {
+                                L.rid[b0 + u * kWave + lane] = static_cast<uint16_t>(ju[u]);
+                                if (ldsm) RV[b0 + u * kWave + lane] = __float_as_uint(ru[u]);
+                            }
                     }
 #pragma unroll
                     for (int u = 0; u < kRefU; ++u) {
@@ -436,149 +449,172 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             }
             __syncthreads();
             FD_REF_MARK(26);  // stopper bases
-            // pass 2: scatter stopper positions by rank (left stoppers from the left, right from the right);
-            // the same kRefU-round walk as pass 1
-            {
-                const uint32_t mywbL = static_cast<uint32_t>(__shfl(static_cast<int>(wbL), wv));
-                const uint32_t mywbR = static_cast<uint32_t>(__shfl(static_cast<int>(wbR), wv));
-                uint32_t cl = mywbL, cr = mywbR;
-                int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
-                for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
-                    uint32_t pu[kRefU];
-                    int ju[kRefU];
-                    bool vu[kRefU];
-                    float ru[kRefU];
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        const uint32_t b = b0 + u * kWave, e = b + lane;
-                        vu[u] = e < e1;
-                        if (cached) {
-                            ju[u] = vu[u] ? L.rid[e] : 0;
-                        } else {
-                            while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                            ju[u] = vu[u] ? range_of(L.o, m, jw, e) : jw;
+            // passes 2-4, compiled twice: stopper positions in LDS (LDS mode) or in lpos / rpos
+            auto passes = [&](auto lm) {
+                constexpr bool LM = decltype(lm)::value;
+                auto lp_st = [&](uint32_t i, uint32_t v) {
+                    if constexpr (LM) LP[i] = v;
+                    else lpos[i] = v;
+                };
+                auto rp_st = [&](uint32_t i, uint32_t v) {
+                    if constexpr (LM) RP[i] = v;
+                    else rpos[i] = v;
+                };
+                auto lp_ld = [&](uint32_t i) -> uint32_t {
+                    if constexpr (LM) return LP[i];
+                    else return lpos[i];
+                };
+                auto rp_ld = [&](uint32_t i) -> uint32_t {
+                    if constexpr (LM) return RP[i];
+                    else return rpos[i];
+                };
+                // pass 2: scatter stopper positions by rank (left stoppers from the left, right from the right);
+                // the same kRefU-round walk as pass 1
+                {
+                    const uint32_t mywbL = static_cast<uint32_t>(__shfl(static_cast<int>(wbL), wv));
+                    const uint32_t mywbR = static_cast<uint32_t>(__shfl(static_cast<int>(wbR), wv));
+                    uint32_t cl = mywbL, cr = mywbR;
+                    int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
+                    for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
+                        uint32_t pu[kRefU];
+                        int ju[kRefU];
+                        bool vu[kRefU];
+                        float ru[kRefU];
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            const uint32_t b = b0 + u * kWave, e = b + lane;
+                            vu[u] = e < e1;
+                            if (cached) {
+                                ju[u] = vu[u] ? L.rid[e] : 0;
+                            } else {
+                                while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                                ju[u] = vu[u] ? range_of(L.o, m, jw, e) : jw;
+                            }
+                            pu[u] = L.r_lo[c][ju[u]] + 1u + (e - L.o[ju[u]]);
                         }
-                        pu[u] = L.r_lo[c][ju[u]] + 1u + (e - L.o[ju[u]]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) ru[u] = vu[u] ? as_f(Xr[2u * FD_REF_IDX(pu[u], n, 6)]) : 0.0f;
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        const int j = ju[u];
-                        const uint32_t oj = L.o[j], p = pu[u];
-                        const float pv = L.piv[j];
-                        const bool ls = vu[u] && ru[u] <= pv, rs = vu[u] && ru[u] >= pv;
-                        const uint64_t bl = ballot(ls), br = ballot(rs);
-                        if (ls) {
-                            const uint32_t rankL = static_cast<uint32_t>(mbcnt64(bl, 0)) + cl - L.bL[j];  // 0-based
-                            lpos[FD_REF_IDX(oj + rankL, L.T, 7)] = p;
-                        }
-                        if (rs) {
-                            const uint32_t rankR = L.eR[j] - (static_cast<uint32_t>(mbcnt64(br, 0)) + cr) - 1u;  // from the right
-                            rpos[FD_REF_IDX(oj + rankR, L.T, 8)] = p;
-                        }
-                        cl += popc64(bl);
-                        cr += popc64(br);
-                    }
-                }
-            }
-            __syncthreads();
-            FD_REF_MARK(27);  // pass 2
-            // pass 3: K = number of pairs with l_k < r_k (monotone in k: the last true k writes it); the
-            // kRefU rounds' stopper positions loaded together
-            {
-                int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
-                for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
-                    int ju[kRefU];
-                    bool vu[kRefU];
-                    uint32_t l0[kRefU], r0[kRefU], l1[kRefU], r1[kRefU];
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        const uint32_t b = b0 + u * kWave, e = b + lane;
-                        vu[u] = e < e1;
-                        if (cached) {
-                            ju[u] = vu[u] ? L.rid[e] : 0;
-                        } else {
-                            while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                            ju[u] = vu[u] ? range_of(L.o, m, jw, e) : jw;
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        const uint32_t e = b0 + u * kWave + lane;
-                        // (clamped reads: entries past T are never used)
-                        l0[u] = lpos[FD_REF_IDX(min(e, L.T - 1u), L.T, 9)];
-                        r0[u] = rpos[FD_REF_IDX(min(e, L.T - 1u), L.T, 9)];
-                        l1[u] = lpos[FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10)];
-                        r1[u] = rpos[FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10)];
-                    }
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        const uint32_t e = b0 + u * kWave + lane;
-                        const int j = ju[u];
-                        const uint32_t k = e - L.o[j];  // 0-based pair index
-                        const uint32_t mn = min(L.nL[j], L.nR[j]);
-                        const bool t = vu[u] && k < mn && l0[u] < r0[u];
-                        const bool tn = t && k + 1 < mn && l1[u] < r1[u];
-                        if (t && !tn) L.K[j] = k + 1;
-                    }
-                }
-            }
-            __syncthreads();
-            FD_REF_MARK(28);  // pass 3
-            // pass 4: the swaps; the cuts (the kRefU rounds' stopper positions, then their elements, loaded
-            // together)
-            {
-                int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
-                for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
-                    bool su[kRefU];
-                    uint32_t pl[kRefU], pr[kRefU];
-                    uint2 vl[kRefU], vr[kRefU];
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        const uint32_t b = b0 + u * kWave, e = b + lane;
-                        const bool valid = e < e1;
-                        int j;
-                        if (cached) {
-                            j = valid ? L.rid[e] : 0;
-                        } else {
-                            while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                            j = valid ? range_of(L.o, m, jw, e) : jw;
-                        }
-                        const uint32_t k = e - L.o[j];
-                        su[u] = valid && k < L.K[j];
-                    }
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        const uint32_t e = b0 + u * kWave + lane;
-                        pl[u] = su[u] ? FD_REF_IDX(lpos[FD_REF_IDX(e, L.T, 11)], n, 12) : 0u;
-                        pr[u] = su[u] ? FD_REF_IDX(rpos[FD_REF_IDX(e, L.T, 11)], n, 13) : 0u;
-                    }
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        if (su[u]) {
-                            vl[u] = X[pl[u]];
-                            vr[u] = X[pr[u]];
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < kRefU; ++u) {
-                        if (su[u]) {
-                            X[pl[u]] = vr[u];
-                            X[pr[u]] = vl[u];
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u)
+                            ru[u] = !vu[u] ? 0.0f : (LM ? as_f(RV[b0 + u * kWave + lane]) : as_f(Xr[2u * FD_REF_IDX(pu[u], n, 6)]));
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            const int j = ju[u];
+                            const uint32_t oj = L.o[j], p = pu[u];
+                            const float pv = L.piv[j];
+                            const bool ls = vu[u] && ru[u] <= pv, rs = vu[u] && ru[u] >= pv;
+                            const uint64_t bl = ballot(ls), br = ballot(rs);
+                            if (ls) {
+                                const uint32_t rankL = static_cast<uint32_t>(mbcnt64(bl, 0)) + cl - L.bL[j];  // 0-based
+                                lp_st(FD_REF_IDX(oj + rankL, L.T, 7), p);
+                            }
+                            if (rs) {
+                                const uint32_t rankR = L.eR[j] - (static_cast<uint32_t>(mbcnt64(br, 0)) + cr) - 1u;  // from the right
+                                rp_st(FD_REF_IDX(oj + rankR, L.T, 8), p);
+                            }
+                            cl += popc64(bl);
+                            cr += popc64(br);
                         }
                     }
                 }
-                if (tid < m) {
-                    const uint32_t K = L.K[tid], oj = L.o[tid];
-                    uint32_t cut = kNoPos;
-                    if (K < L.nL[tid]) cut = lpos[FD_REF_IDX(oj + K, L.T, 14)];
-                    if (K >= 1u) cut = min(cut, rpos[FD_REF_IDX(oj + K - 1u, L.T, 15)]);
-                    L.cut[tid] = cut;
+                __syncthreads();
+                FD_REF_MARK(27);  // pass 2
+                // pass 3: K = number of pairs with l_k < r_k (monotone in k: the last true k writes it); the
+                // kRefU rounds' stopper positions loaded together
+                {
+                    int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
+                    for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
+                        int ju[kRefU];
+                        bool vu[kRefU];
+                        uint32_t l0[kRefU], r0[kRefU], l1[kRefU], r1[kRefU];
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            const uint32_t b = b0 + u * kWave, e = b + lane;
+                            vu[u] = e < e1;
+                            if (cached) {
+                                ju[u] = vu[u] ? L.rid[e] : 0;
+                            } else {
+                                while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                                ju[u] = vu[u] ? range_of(L.o, m, jw, e) : jw;
+                            }
+                        }
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            const uint32_t e = b0 + u * kWave + lane;
+                            // (clamped reads: entries past T are never used)
+                            l0[u] = lp_ld(FD_REF_IDX(min(e, L.T - 1u), L.T, 9));
+                            r0[u] = rp_ld(FD_REF_IDX(min(e, L.T - 1u), L.T, 9));
+                            l1[u] = lp_ld(FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10));
+                            r1[u] = rp_ld(FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10));
+                        }
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            const uint32_t e = b0 + u * kWave + lane;
+                            const int j = ju[u];
+                            const uint32_t k = e - L.o[j];  // 0-based pair index
+                            const uint32_t mn = min(L.nL[j], L.nR[j]);
+                            const bool t = vu[u] && k < mn && l0[u] < r0[u];
+                            const bool tn = t && k + 1 < mn && l1[u] < r1[u];
+                            if (t && !tn) L.K[j] = k + 1;
+                        }
+                    }
                 }
-            }
-            __syncthreads();
-            FD_REF_MARK(29);  // pass 4
+                __syncthreads();
+                FD_REF_MARK(28);  // pass 3
+                // pass 4: the swaps; the cuts (the kRefU rounds' stopper positions, then their elements, loaded
+                // together)
+                {
+                    int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
+                    for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
+                        bool su[kRefU];
+                        uint32_t pl[kRefU], pr[kRefU];
+                        uint2 vl[kRefU], vr[kRefU];
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            const uint32_t b = b0 + u * kWave, e = b + lane;
+                            const bool valid = e < e1;
+                            int j;
+                            if (cached) {
+                                j = valid ? L.rid[e] : 0;
+                            } else {
+                                while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
+                                j = valid ? range_of(L.o, m, jw, e) : jw;
+                            }
+                            const uint32_t k = e - L.o[j];
+                            su[u] = valid && k < L.K[j];
+                        }
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            const uint32_t e = b0 + u * kWave + lane;
+                            pl[u] = su[u] ? FD_REF_IDX(lp_ld(FD_REF_IDX(e, L.T, 11)), n, 12) : 0u;
+                            pr[u] = su[u] ? FD_REF_IDX(rp_ld(FD_REF_IDX(e, L.T, 11)), n, 13) : 0u;
+                        }
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            if (su[u]) {
+                                vl[u] = X[pl[u]];
+                                vr[u] = X[pr[u]];
+                            }
+                        }
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            if (su[u]) {
+                                X[pl[u]] = vr[u];
+                                X[pr[u]] = vl[u];
+                            }
+                        }
+                    }
+                    if (tid < m) {
+                        const uint32_t K = L.K[tid], oj = L.o[tid];
+                        uint32_t cut = kNoPos;
+                        if (K < L.nL[tid]) cut = lp_ld(FD_REF_IDX(oj + K, L.T, 14));
+                        if (K >= 1u) cut = min(cut, rp_ld(FD_REF_IDX(oj + K - 1u, L.T, 15)));
+                        L.cut[tid] = cut;
+                    }
+                }
+                __syncthreads();
+                FD_REF_MARK(29);  // pass 4
+            };
+            if (ldsm) passes(std::true_type{});
+            else passes(std::false_type{});
             // children: ranges > 16 into the next list (in order), the rest are leaves
             if (wv == 0) {
                 const int nc = c ^ 1;
@@ -680,6 +716,12 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         // ---- window final: greedy over [fin, fin_new) -------------------------------------------------
         const uint32_t fin = L.fin;
         const uint32_t fin_new = L.m_all > 0 ? L.r_lo[L.cur][0] : n;
+        if (!grid_ready) {
+            if (use_grid)
+                for (int i = tid; i < cells; i += NT) grid[i] = grid_empty(rows, cols, d);
+            grid_ready = true;
+            __syncthreads();
+        }
         for (uint32_t base = fin; base < fin_new; base += kSelectChunk) {
             if (L.s_done) break;
             const int cn = static_cast<int>(min(static_cast<uint32_t>(kSelectChunk), fin_new - base));
