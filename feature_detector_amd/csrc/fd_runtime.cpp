@@ -700,7 +700,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
                 r.dbg = as<uint32_t>(c->dbg);
             }
             FD_HIP_TRY(c, fdk::launch_select_reference(s, r, batch, c->stream));
-            if (stamps) {  // k_select_reference's phase clocks (slots 16-23) of the flagged frames
+            if (stamps) {  // k_select_reference's phase clocks (slots 16-30) of the flagged frames
                 std::vector<uint64_t> all(static_cast<size_t>(batch) * 32);
                 FD_HIP_TRY(c, hipMemcpyAsync(all.data(), c->dbg.p, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost,
                                              c->stream));
@@ -710,11 +710,11 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
                     if (q[18])
                         std::fprintf(stderr, "k_select_reference frame %d cycles: push %llu | levels %llu sumT %llu: pivots %llu "
                                              "pass1 %llu bases %llu pass2 %llu pass3 %llu pass4 %llu children %llu | leaves %llu "
-                                             "greedy %llu windows %llu\n", b, (unsigned long long)q[16], (unsigned long long)q[18],
+                                             "wave-local %llu greedy %llu windows %llu\n", b, (unsigned long long)q[16], (unsigned long long)q[18],
                                      (unsigned long long)q[19], (unsigned long long)q[24], (unsigned long long)q[25],
                                      (unsigned long long)q[26], (unsigned long long)q[27], (unsigned long long)q[28],
                                      (unsigned long long)q[29], (unsigned long long)q[30], (unsigned long long)q[20],
-                                     (unsigned long long)q[21], (unsigned long long)q[22]);
+                                     (unsigned long long)q[23], (unsigned long long)q[21], (unsigned long long)q[22]);
                 }
             }
             if (ref_debug) {

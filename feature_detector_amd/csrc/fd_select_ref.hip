@@ -25,7 +25,9 @@
 //   2. windows of kSelectChunk positions from the front: every range overlapping the window is
 //      partitioned, level by level, all of a level's ranges at once (flat index space over their
 //      partition spans, one block of it per wave), until only leaves (<= 16) cover the window; leaves
-//      are insertion-sorted by one thread each into the visiting order;
+//      are insertion-sorted by 16 lanes each into the visiting order; before the first greedy scan,
+//      children of <= kRefWaveLocal elements leave the levels and are sorted to the end by one wave
+//      each in LDS (ref_wave_resolve), which saves the last levels' barriers;
 //   3. the greedy scan of k_select_ordered over the new positions (one wave, occupancy grid); stop at
 //      `need`, else the next window (ranges right of the window wait in the range list).
 // A range that would reach the depth limit (std::__partial_sort, heapsort) is not emulated: the frame
@@ -42,8 +44,20 @@ constexpr int kRefThreads = 1024;
 constexpr int kRefWaves = kRefThreads / kWave;
 constexpr int kRefMaxRanges = 256;  // unresolved ranges (> 16) in the list; bound: DESIGN.md
 constexpr int kRefLeaf = 16;        // libstdc++ _S_threshold
-constexpr int kRefU = 4;            // 64-element rounds per wave whose global loads are issued together
+#ifndef FD_REF_U
+#define FD_REF_U 4
+#endif
+constexpr int kRefU = FD_REF_U;     // 64-element rounds per wave whose global loads are issued together
 constexpr uint32_t kRefRidCap = 8192;  // flat elements per level whose range index pass 1 caches for passes 2-4
+// A range of <= kRefWaveLocal elements is partitioned to the end (its whole subtree) by one wave in LDS,
+// with no workgroup barriers, in 12 B per element of the 96 KiB greedy span per wave (elements + stopper
+// positions). A/B on the bench tie frames (tools/gpu_r04f.sh): off / 64 / 128 / 256 / 512 = headline
+// 52.3 / 51.3 / 50.1 / 48.4 / 52.5 us per call, north star 1.48 / 1.54 / 1.53 / 1.52 / 1.53 ms.
+#ifndef FD_REF_WL
+#define FD_REF_WL 256
+#endif
+constexpr uint32_t kRefWaveLocal = FD_REF_WL;  // (0: off)
+constexpr int kRefStack = 64;  // pending subranges per wave (depth-first: <= 2 per level)
 constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 
 struct alignas(16) RefLds {
@@ -65,9 +79,12 @@ struct alignas(16) RefLds {
     uint32_t waveL[kRefWaves], waveR[kRefWaves];
     // leaves produced by the level
     uint32_t leaf_lo[2 * kRefMaxRanges], leaf_hi[2 * kRefMaxRanges];
+    // ranges of <= kRefWaveLocal elements handed to single waves (first window only), and the waves' stacks
+    uint32_t wl_lo[kRefMaxRanges], wl_hi[kRefMaxRanges], wl_dep[kRefMaxRanges];
+    uint32_t wstk[kRefWaves][kRefStack];
     uint32_t wsum[kRefWaves];
     uint16_t rid[kRefRidCap];  // levels with T <= kRefRidCap: each element's active range (set by pass 1)
-    int cur, m_all, m_act, n_leaf, fail;
+    int cur, m_all, m_act, n_leaf, fail, n_wl;
     uint32_t T, fin;
     int s_done, s_acc;
     uint32_t tie_prev;
@@ -165,6 +182,125 @@ __device__ __forceinline__ void set_active(RefLds &L, uint32_t win_end) {
         L.o[act] = carry;
         L.T = carry;
     }
+}
+
+// One wave: libstdc++'s introsort on X[lo, hi) (<= kRefWaveLocal elements, > kRefLeaf) to the end -- the
+// same partitions as the workgroup levels (median of (first + 1, mid, last - 1) moved to first, left
+// stoppers resp <= pivot from the left paired with right stoppers resp >= pivot from the right while
+// l_k < r_k, cut = min(l_K, r_{K-1})), then the final insertion sort of every leaf (stable, response
+// descending) -- with the elements in the wave's LDS. Writes the range's visiting order into ord[lo, hi).
+// Returns false if a partition would reach the depth limit (heapsort: not emulated).
+__device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t hi, uint32_t dep, uint2 *E,
+                                 uint16_t *Lp, uint16_t *Rp, uint32_t *stk) {
+    const int lane = lane_id();
+    const uint32_t s = hi - lo;
+    for (uint32_t i = lane; i < s; i += kWave) E[i] = X[lo + i];
+    // stack entries: a (10 bits) | b (11 bits) << 10 | depth left << 21, positions relative to lo
+    int top = 0;
+    if (lane == 0) stk[0] = 0u | (s << 10) | (dep << 21);
+    top = 1;
+    bool ok = true;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    while (top > 0) {
+        --top;
+        const uint32_t ent = stk[top];
+        const uint32_t a = ent & 1023u, b = (ent >> 10) & 2047u, dp = ent >> 21;
+        if (b - a <= static_cast<uint32_t>(kRefLeaf)) {
+            // leaf: stable rank by response, descending (lanes 0-15)
+            const int len = static_cast<int>(b - a);
+            const int q = lane & (kRefLeaf - 1);
+            const uint2 v = q < len ? E[a + q] : make_uint2(0u, 0u);
+            const float ri = __uint_as_float(v.x);
+            uint32_t rk = 0;
+#pragma unroll
+            for (int t = 0; t < kRefLeaf; ++t) {
+                const float rt = __uint_as_float(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), t)));
+                rk += (t < len && (rt > ri || (rt == ri && t < q))) ? 1u : 0u;
+            }
+            if (lane < kRefLeaf && q < len) ord[lo + a + rk] = v.y;
+            continue;
+        }
+        if (dp == 0u) {  // std::__partial_sort
+            ok = false;
+            break;
+        }
+        // pivot: __move_median_to_first(a, a + 1, mid, b - 1)
+        const uint32_t mid = a + (b - a) / 2u;
+        const uint2 xa = E[a + 1], xb = E[mid], xc = E[b - 1];
+        const uint32_t ch = median_pos(__uint_as_float(xa.x), __uint_as_float(xb.x), __uint_as_float(xc.x), a + 1, mid, b - 1);
+        const uint2 xp = ch == a + 1 ? xa : (ch == mid ? xb : xc);
+        const uint2 x0 = E[a];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane == 0) {
+            E[a] = xp;
+            E[ch] = x0;
+        }
+        const float pv = __uint_as_float(xp.x);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // stoppers of [a + 1, b): left ones by rank from the left, right ones by rank from the left (reversed below)
+        uint32_t nL = 0, nR = 0;
+        for (uint32_t i0 = a + 1; i0 < b; i0 += kWave) {
+            const uint32_t i = i0 + lane;
+            const bool in = i < b;
+            const float rv = in ? __uint_as_float(E[i].x) : 0.0f;
+            const bool ls = in && rv <= pv, rs = in && rv >= pv;
+            const uint64_t bl = ballot(ls), br = ballot(rs);
+            if (ls) Lp[nL + mbcnt64(bl, 0)] = static_cast<uint16_t>(i);
+            if (rs) Rp[nR + mbcnt64(br, 0)] = static_cast<uint16_t>(i);
+            nL += popc64(bl);
+            nR += popc64(br);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // K: pairs k with l_k < r_k (r_k = the k-th right stopper from the right), monotone in k
+        const uint32_t mn = min(nL, nR);
+        uint32_t K = 0;
+        for (uint32_t k0 = 0; k0 < mn; k0 += kWave) {
+            const uint32_t k = k0 + lane;
+            const bool t = k < mn && Lp[k] < Rp[nR - 1u - min(k, nR - 1u)];
+            const uint64_t bt = ballot(t);
+            const uint32_t run = bt == ~0ull ? 64u : static_cast<uint32_t>(__builtin_ctzll(~bt));
+            K += run;
+            if (run < 64u) break;
+        }
+        // the swaps (pairs are disjoint)
+        for (uint32_t k0 = 0; k0 < K; k0 += kWave) {
+            const uint32_t k = k0 + lane;
+            if (k < K) {
+                const uint32_t pl = Lp[k], pr = Rp[nR - 1u - k];
+                const uint2 vl = E[pl], vr = E[pr];
+                E[pl] = vr;
+                E[pr] = vl;
+            }
+        }
+        uint32_t cut = 0xFFFFFFFFu;
+        if (K < nL) cut = Lp[K];
+        if (K >= 1u) cut = min(cut, static_cast<uint32_t>(Rp[nR - K]));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (cut <= a || cut >= b || top + 2 > kRefStack) {  // (cannot happen: the scans stop inside the range)
+            ok = false;
+            break;
+        }
+        // children, left one on top (depth-first; the order of resolution does not matter)
+        if (lane == 0) {
+            stk[top] = cut | (b << 10) | ((dp - 1u) << 21);
+            stk[top + 1] = a | (cut << 10) | ((dp - 1u) << 21);
+        }
+        top += 2;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return ok;
 }
 
 // Diagnostic phase clocks (SelectArgs::stamps, FD_SELECT_STAMPS): thread 0 adds the cycles since the
@@ -312,6 +448,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         L.cur = 0;
         L.n_leaf = 0;
         L.fin = 0;
+        L.n_wl = 0;
         // __introsort_loop(0, n, 2 * __lg(n)); n <= 16: the final insertion sort alone (one leaf)
         if (n > static_cast<uint32_t>(kRefLeaf)) {
             L.r_lo[0][0] = 0;
@@ -619,6 +756,10 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             if (wv == 0) {
                 const int nc = c ^ 1;
                 uint32_t w_at = 0, l_at = 0;
+                // before the first greedy scan, children of <= kRefWaveLocal elements go to the wave-local
+                // list (while it has room) instead of the next level
+                const bool wl_on = kRefWaveLocal > 0u && !grid_ready;
+                uint32_t v_at = static_cast<uint32_t>(L.n_wl);
                 for (int b = 0; b < m; b += kWave) {
                     const int j = b + lane;
                     const bool in = j < m;
@@ -633,10 +774,33 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                             ct = lo + 1;
                         }
                     }
-                    const bool bigL = in && ct - lo > static_cast<uint32_t>(kRefLeaf);
-                    const bool bigR = in && hi - ct > static_cast<uint32_t>(kRefLeaf);
+                    bool bigL = in && ct - lo > static_cast<uint32_t>(kRefLeaf);
+                    bool bigR = in && hi - ct > static_cast<uint32_t>(kRefLeaf);
+                    {
+                        const bool cL = wl_on && bigL && ct - lo <= kRefWaveLocal;
+                        const bool cR = wl_on && bigR && hi - ct <= kRefWaveLocal;
+                        const uint32_t nv = (cL ? 1u : 0u) + (cR ? 1u : 0u);
+                        const uint32_t iv = wave_incl_add(nv);
+                        uint32_t pv = v_at + iv - nv;
+                        if (cL && pv < static_cast<uint32_t>(kRefMaxRanges)) {
+                            L.wl_lo[pv] = lo;
+                            L.wl_hi[pv] = ct;
+                            L.wl_dep[pv] = dp;
+                            bigL = false;
+                        }
+                        if (cL) ++pv;
+                        if (cR && pv < static_cast<uint32_t>(kRefMaxRanges)) {
+                            L.wl_lo[pv] = ct;
+                            L.wl_hi[pv] = hi;
+                            L.wl_dep[pv] = dp;
+                            bigR = false;
+                        }
+                        v_at += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(iv), kWave - 1));
+                    }
                     const uint32_t nb = (bigL ? 1u : 0u) + (bigR ? 1u : 0u);
-                    const uint32_t nlf = in ? 2u - nb : 0u;
+                    const bool leafL = in && ct - lo <= static_cast<uint32_t>(kRefLeaf);
+                    const bool leafR = in && hi - ct <= static_cast<uint32_t>(kRefLeaf);
+                    const uint32_t nlf = (leafL ? 1u : 0u) + (leafR ? 1u : 0u);
                     const uint32_t ib = wave_incl_add(nb), il = wave_incl_add(nlf);
                     uint32_t pb = w_at + ib - nb, pl = l_at + il - nlf;
                     if (bigL && pb < kRefMaxRanges) {
@@ -650,12 +814,12 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                         L.r_hi[nc][pb] = hi;
                         L.r_dep[nc][pb] = dp;
                     }
-                    if (in && !bigL) {
+                    if (leafL) {
                         L.leaf_lo[pl] = lo;
                         L.leaf_hi[pl] = ct;
                         ++pl;
                     }
-                    if (in && !bigR) {
+                    if (leafR) {
                         L.leaf_lo[pl] = ct;
                         L.leaf_hi[pl] = hi;
                     }
@@ -678,6 +842,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                     L.m_all = static_cast<int>(min(tot, static_cast<uint32_t>(kRefMaxRanges)));
                     L.cur = nc;
                     L.n_leaf = static_cast<int>(l_at);
+                    L.n_wl = static_cast<int>(min(v_at, static_cast<uint32_t>(kRefMaxRanges)));
                 }
                 __builtin_amdgcn_s_waitcnt(0);
                 set_active(L, L.fin + kSelectChunk);
@@ -712,6 +877,25 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         if (L.m_act > 0) {
             __syncthreads();
             continue;
+        }
+        // ---- wave-local ranges: one wave each, partitioned to the end in LDS (the greedy span) -----------
+        if (L.n_wl > 0) {
+            constexpr uint32_t kWaveBytes = kRefWaveLocal * (8u + 2u + 2u);
+            static_assert(kRefWaves * kWaveBytes <= sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask) + sizeof(L.grid_lds),
+                          "wave-local buffers fit the greedy span");
+            unsigned char *const wb = reinterpret_cast<unsigned char *>(L.pxy) + wv * kWaveBytes;
+            uint2 *const E = reinterpret_cast<uint2 *>(wb);
+            uint16_t *const Lp = reinterpret_cast<uint16_t *>(wb + kRefWaveLocal * 8u);
+            uint16_t *const Rp = Lp + kRefWaveLocal;
+            const int nw = L.n_wl;
+            bool ok = true;
+            for (int j = wv; j < nw && ok; j += kRefWaves)
+                ok = ref_wave_resolve(X, ord, L.wl_lo[j], L.wl_hi[j], L.wl_dep[j], E, Lp, Rp, L.wstk[wv]);
+            if (!ok && lane == 0) L.fail = 5;
+            __syncthreads();
+            if (tid == 0) L.n_wl = 0;
+            FD_REF_MARK(23);  // wave-local ranges
+            if (L.fail) break;
         }
         // ---- window final: greedy over [fin, fin_new) -------------------------------------------------
         const uint32_t fin = L.fin;

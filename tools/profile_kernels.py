@@ -9,6 +9,9 @@ fixed number of times, on seeded uniform-noise frames generated on the GPU.
   --shape lsd        fd_lsd_map (dense) and fd_lsd_lines (compact map + host stage), 1920x1080 batch 256,
                      64-px checker + noise (BASELINE configs[3]), 3 calls each (--kind dense / compact: one;
                      dense_unpitched: dense maps with unpadded rows)
+  --shape ties       fd_points_detect with ties="reference" on the bench tie-report frames: Harris 640x480,
+                     16 seeds x 10 calls (the seeds whose frames meet a tie run k_select_reference)
+  --shape nsties     the same on the north-star batch (Shi-Tomasi 1920x1080 x256), 4 calls
 """
 import argparse
 import os
@@ -21,7 +24,8 @@ import feature_detector_amd as fd  # noqa: E402
 
 THR = {"harris": 30.0, "shi_tomasi": 40.0, "fast": 10.0}
 p = argparse.ArgumentParser()
-p.add_argument("--shape", default="bench", choices=["bench", "northstar", "nsdetect", "fast720", "fast720r", "fastbrief", "lsd"])
+p.add_argument("--shape", default="bench", choices=["bench", "northstar", "nsdetect", "fast720", "fast720r", "fastbrief", "lsd",
+                                                   "ties", "nsties"])
 p.add_argument("--kind", default=None, choices=[None, "harris", "shi_tomasi", "fast", "dense", "compact", "dense_unpitched"])
 p.add_argument("--calls", type=int, default=0)
 p.add_argument("--thr", type=float, default=None, help="response threshold override (e.g. 1e30: no candidates)")
@@ -76,6 +80,19 @@ elif a.shape == "nsdetect":  # north-star shape through fd_points_detect (K1 wit
             fd.detect_points(kind, frames, 200, 20, THR[kind], ties="raster")
         except Exception as e:  # (diagnostic builds that break the selection still time the kernels)
             print("detect:", e)
+elif a.shape in ("ties", "nsties"):  # bench.tie_report's frames (bench.make_frames)
+    import bench  # noqa: E402
+    if a.shape == "ties":
+        kind = a.kind or "harris"
+        pool = [bench.make_frames(torch, "noise", 1, 480, 640, 1234 + 7919 * i, "cuda") for i in range(16)]
+        for f in pool:
+            for _ in range(a.calls or 10):
+                fd.detect_points(kind, f, 200, 20, THR[kind], ties="reference")
+    else:
+        kind = a.kind or "shi_tomasi"
+        f = bench.make_frames(torch, "noise", 256, 1080, 1920, 99, "cuda")
+        for _ in range(a.calls or 4):
+            fd.detect_points(kind, f, 200, 20, THR[kind], ties="reference")
 elif a.shape == "fast720r":  # the FAST kernel alone (fd_points_response: no selection histogram)
     kind = "fast"
     frames = noise(64, 720, 1280)
