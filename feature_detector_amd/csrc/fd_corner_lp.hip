@@ -227,8 +227,8 @@ __device__ __forceinline__ void lp_flush(uint32_t &n, const uint32_t *sl, const 
             const float r = lp_resp<KIND>(sl, j);
             if (hist) atomicAdd(&hist[((float_key(r) - a.key_base) << a.key_lz) >> 20], 1u);
             const uint32_t pos4 = static_cast<uint32_t>(mbcnt64(b, static_cast<int>(off))) << 2;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rr, static_cast<int>(pos4), 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(sl[j * 128 + 64], ri, static_cast<int>(pos4), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r), rr, static_cast<int>(pos4), 0, FD_LIST_NT ? 2 : 0);
+            __builtin_amdgcn_raw_buffer_store_b32(sl[j * 128 + 64], ri, static_cast<int>(pos4), 0, FD_LIST_NT ? 2 : 0);
         }
         off += static_cast<uint32_t>(popc64(b));
     }

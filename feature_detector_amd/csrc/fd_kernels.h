@@ -11,6 +11,9 @@ namespace fdk {
 constexpr int kTileW = 248;
 constexpr int kSegCorner = kTileW / 2;  // strict 4-neighbour NMS: <= 1 candidate per 2 columns
 constexpr int kSegFast = kTileW;        // FAST has no NMS
+#ifndef FD_LIST_NT
+#define FD_LIST_NT 0  // candidate list stores with the nt (streaming) cache policy
+#endif
 constexpr int kSelectChunk = 2048;      // candidates sorted per greedy chunk (LDS)
 constexpr int kGridLdsCells = 16384;    // occupancy grid kept in LDS up to this many cells
 constexpr int kMaxOffsetSegs = 48;

@@ -188,6 +188,9 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
     const auto ra = make_rsrc(amap, amap ? 4 * mbytes : 0u);
     const auto rv = make_rsrc(a.valid ? a.valid + mbase : nullptr, a.valid ? mbytes : 0u);
 
+#ifndef FD_LSD_STORE_AUX
+#define FD_LSD_STORE_AUX 2  // nt: streaming map stores (1.55 -> 1.43 ms at 1080p x256, profiles/r04_lsd_nt_ab.txt)
+#endif
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     struct alignas(4) F4 { float x, y, z, w; };
     // one map row's 4 angle entries of this lane
@@ -195,7 +198,7 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
         if constexpr (INTERIOR) {
             __builtin_amdgcn_raw_buffer_store_b128(
                 u4{__float_as_uint(av[0]), __float_as_uint(av[1]), __float_as_uint(av[2]), __float_as_uint(av[3])}, ra,
-                4 * (r * mp + c0), 0, 0);
+                4 * (r * mp + c0), 0, FD_LSD_STORE_AUX);
             return;
         }
         if (!a.angle) return;
@@ -215,8 +218,8 @@ __device__ __forceinline__ void lsd_map_tile(const LsdArgs &a, const int f, cons
             const int o = r * mp + c0;  // < 2^31: checked on the host
             __builtin_amdgcn_raw_buffer_store_b128(
                 u4{__float_as_uint(nv[0]), __float_as_uint(nv[1]), __float_as_uint(nv[2]), __float_as_uint(nv[3])}, rn,
-                4 * o, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(vb, rv, o, 0, 0);
+                4 * o, 0, FD_LSD_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(vb, rv, o, 0, FD_LSD_STORE_AUX);
             return;
         }
         const int64_t i = mbase + static_cast<int64_t>(r) * mp + c0;

@@ -53,8 +53,13 @@ __device__ __forceinline__ void sink_flush(Sink &sk, const PointsArgs &a, int f)
         if (sk.hist) atomicAdd(&sk.hist[((float_key(r) - a.key_base) << a.key_lz) >> 20], 1u);
         const int64_t pos = static_cast<int64_t>(base) + i;
         if (pos < a.list_cap) {
+#if FD_LIST_NT
+            __builtin_nontemporal_store(r, &dr[pos]);
+            __builtin_nontemporal_store(sk.idx[i], &di[pos]);
+#else
             dr[pos] = r;
             di[pos] = sk.idx[i];
+#endif
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -184,8 +189,13 @@ __device__ __forceinline__ void seg_flush(Sink &sk, const PointsArgs &a, int f, 
         const uint32_t lp = atomicAdd(&L.hist[k32 >> 20], 1u);
         const int64_t pos = base + lp;
         if (pos < a.list_cap) {
+#if FD_LIST_NT
+            __builtin_nontemporal_store(r, &dr[pos]);
+            __builtin_nontemporal_store(sk.idx[i], &di[pos]);
+#else
             dr[pos] = r;
             di[pos] = sk.idx[i];
+#endif
         }
         // the segment's head as selection keys (k32, ~idx): k_select's first read, no list hop
         if (lp < static_cast<uint32_t>(kSegHead)) head[lp] = (static_cast<uint64_t>(k32) << 32) | static_cast<uint64_t>(~sk.idx[i]);
