@@ -133,6 +133,20 @@ struct OrderedArgs {
     const int32_t *frame;   // [n_frames] frame index (into SelectArgs' per-frame arrays)
 };
 
+// Wide prelude of k_select_reference (large frames, launch_select_reference with wide): the push order
+// and the first partition levels of the frame's leftmost range, each spread over kRefWideGroups
+// workgroups per flagged frame, while that range has more than kRefWideMin elements.
+constexpr int kRefWideLevels = 8;
+constexpr int kRefWideGroups = 32;
+constexpr uint32_t kRefWideMin = 8192;
+struct RefCtl {  // per frame, written by the prelude, read by k_select_reference
+    uint32_t n, nlev, bad;
+    uint32_t h[kRefWideLevels + 1], dep[kRefWideLevels + 1], act[kRefWideLevels + 1];  // level l: range [0, h[l])
+    uint32_t sib_lo[kRefWideLevels], sib_hi[kRefWideLevels];  // level l's right child [sib_lo, sib_hi), depth dep[l] - 1
+    uint32_t ch, pv, nL, nR, chL, chR;  // the current level's pivot position / response bits, stopper counts, ranks of ch
+    uint2 x0, xch;                      // its elements at 0 and ch before the pivot swap
+};
+
 // k_select_reference (FD_TIES_REFERENCE on the GPU): per-frame scratch of cap entries each (cap >= the
 // list capacity and >= rows * cols / 32: the raster-order bitmap and its word prefix live in lpos / rpos).
 struct RefSortArgs {
@@ -143,6 +157,9 @@ struct RefSortArgs {
     int64_t cap;
     int push_order;  // the list is already in push order (fd_points_select); else unique raster indices
     uint32_t *dbg;   // [batch][8] first broken invariant per frame (FD_REF_DEBUG), or null
+    RefCtl *ctl;     // [batch] wide prelude state (launch_select_reference with wide), else unused
+    uint32_t *wcnt;  // [batch][kRefWideGroups][2] per-workgroup counts of the prelude
+    int wide;        // set by the launcher: the prelude ran (push order and the first levels are done)
 };
 
 // fd_points_select: caller candidates (response, x, y at [f * stride], counts[f]) -> list format.
@@ -272,7 +289,8 @@ hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off,
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
 hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);
 // libstdc++ std::sort order emulated on the GPU for the frames k_select flagged (FD_FRAME_TIES)
-hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r, int batch, hipStream_t s);
+// wide: run the multi-workgroup prelude first (r.ctl, r.wcnt set): frames of >= 1 Mpx
+hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r, int batch, bool wide, hipStream_t s);
 hipError_t launch_cand_lists(const CandInArgs &a, int64_t max_count, hipStream_t s);
 hipError_t launch_nn_pick(const NnPickArgs &a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);

@@ -58,7 +58,7 @@ struct fd_ctx {
     int status_batch = 0;
     int tie_order = FD_TIES_RASTER;
     DevBuf ord, ord_meta;  // FD_TIES_REFERENCE host path: host-computed visiting orders of flagged frames
-    DevBuf r_x, r_lpos, r_rpos, r_ord;  // FD_TIES_REFERENCE on the GPU (k_select_reference scratch)
+    DevBuf r_x, r_lpos, r_rpos, r_ord, r_ctl, r_wcnt;  // FD_TIES_REFERENCE on the GPU (k_select_reference scratch)
     DevBuf run_lut;        // FAST score per 16-bit ring mask (FastOffsets::run_lut), filled once
     // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
     DevBuf l_lnorm, l_langle, l_fbase;
@@ -450,6 +450,10 @@ int ref_buffers(fd_ctx *c, int batch, int rows, int cols, int64_t cap, fdk::RefS
     FD_HIP_TRY(c, ensure(c, c->r_lpos, sizeof(uint32_t) * n));
     FD_HIP_TRY(c, ensure(c, c->r_rpos, sizeof(uint32_t) * n));
     FD_HIP_TRY(c, ensure(c, c->r_ord, sizeof(uint32_t) * n));
+    FD_HIP_TRY(c, ensure(c, c->r_ctl, sizeof(fdk::RefCtl) * static_cast<size_t>(batch)));
+    FD_HIP_TRY(c, ensure(c, c->r_wcnt, sizeof(uint32_t) * 2 * fdk::kRefWideGroups * static_cast<size_t>(batch)));
+    r.ctl = as<fdk::RefCtl>(c->r_ctl);
+    r.wcnt = as<uint32_t>(c->r_wcnt);
     r.x = as<uint2>(c->r_x);
     r.lpos = as<uint32_t>(c->r_lpos);
     r.rpos = as<uint32_t>(c->r_rpos);
@@ -699,7 +703,12 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
                 FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint32_t) * 8 * batch, c->stream));
                 r.dbg = as<uint32_t>(c->dbg);
             }
-            FD_HIP_TRY(c, fdk::launch_select_reference(s, r, batch, c->stream));
+            // frames of >= 1 Mpx: the multi-workgroup prelude (push order, first levels); FD_REF_WIDE=0/1
+            // forces it off / on (A/B)
+            const char *wide_env = std::getenv("FD_REF_WIDE");
+            const bool wide = wide_env ? std::atoi(wide_env) != 0
+                                       : static_cast<int64_t>(rows) * cols >= (int64_t{1} << 20);
+            FD_HIP_TRY(c, fdk::launch_select_reference(s, r, batch, wide, c->stream));
             if (stamps) {  // k_select_reference's phase clocks (slots 16-30) of the flagged frames
                 std::vector<uint64_t> all(static_cast<size_t>(batch) * 32);
                 FD_HIP_TRY(c, hipMemcpyAsync(all.data(), c->dbg.p, sizeof(uint64_t) * all.size(), hipMemcpyDeviceToHost,

@@ -343,7 +343,9 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
     // (every per-candidate loop loads kRefPush candidates' data before using any: one memory round trip
     // per kRefPush candidates instead of one or two per candidate)
     constexpr int kRefPush = 8;
-    if (r.push_order) {
+    if (r.wide) {
+        // (the prelude built X)
+    } else if (r.push_order) {
         for (uint32_t i0 = tid; i0 < n; i0 += kRefPush * NT) {
             float rv[kRefPush];
             uint32_t qv[kRefPush];
@@ -450,7 +452,30 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         L.fin = 0;
         L.n_wl = 0;
         // __introsort_loop(0, n, 2 * __lg(n)); n <= 16: the final insertion sort alone (one leaf)
-        if (n > static_cast<uint32_t>(kRefLeaf)) {
+        if (r.wide) {
+            // the prelude's state: [0, h) of its last level, then the levels' right children, in position
+            // order; ranges of <= 16 elements are leaves
+            const RefCtl &C = r.ctl[f];
+            const uint32_t nlev = min(C.nlev, static_cast<uint32_t>(kRefWideLevels));
+            if (C.n != n || C.bad) L.fail = 6;
+            int m = 0, nl = 0;
+            auto add = [&](uint32_t lo, uint32_t hi, uint32_t dep) {
+                if (hi > lo + static_cast<uint32_t>(kRefLeaf)) {
+                    L.r_lo[0][m] = lo;
+                    L.r_hi[0][m] = hi;
+                    L.r_dep[0][m] = dep;
+                    ++m;
+                } else if (hi > lo) {
+                    L.leaf_lo[nl] = lo;
+                    L.leaf_hi[nl] = hi;
+                    ++nl;
+                }
+            };
+            add(0u, min(C.h[nlev], n), C.dep[nlev]);
+            for (int l = static_cast<int>(nlev) - 1; l >= 0; --l) add(C.sib_lo[l], min(C.sib_hi[l], n), C.dep[l] - 1u);
+            L.m_all = m;
+            L.n_leaf = nl;
+        } else if (n > static_cast<uint32_t>(kRefLeaf)) {
             L.r_lo[0][0] = 0;
             L.r_hi[0][0] = n;
             L.r_dep[0][0] = 2u * (31u - __clz(n));
@@ -958,10 +983,417 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
     }
 }
 
+// ---- wide prelude (frames of >= 1 Mpx) --------------------------------------------------------------
+// One flagged 1080p frame holds ~10^5-10^6 candidates, and a single workgroup walks its push order and
+// its first partition levels (the window's leftmost range [0, h) halves per level) through chains of
+// memory round trips on one CU. The prelude spreads exactly that work over kRefWideGroups workgroups per
+// frame, one kernel per step (the kernel boundary is the only cross-workgroup hand-off):
+//   push: k_refw_init (state, bitmap cleared) -> k_refw_bits (raster bitmap, global atomics) ->
+//         k_refw_wcount (set bits per word slice) -> k_refw_wprefix (word prefix) -> k_refw_place
+//         (X[rank] = candidate);
+//   per level l while h > kRefWideMin: k_refw_lcount (pivot = median of X[1], X[h/2], X[h-1]; stopper
+//         counts per block of [1, h)) -> k_refw_lscatter (stopper positions by rank) -> k_refw_lswap
+//         (pairs with l_k < r_k swapped, the cut found where that stops holding, the pivot moved to 0).
+// The pivot swap is applied virtually until k_refw_lswap (position ch reads the old X[0]), so no step
+// writes what another workgroup of the same kernel reads. k_select_reference then starts from the state
+// (RefCtl): range [0, h), the right children of the levels in position order, no push.
+constexpr int kWT = 256;        // threads per prelude workgroup
+constexpr int kWChunk = 8192;   // k_refw_lscatter: responses staged in LDS per chunk
+constexpr int kWUnroll = 8;     // loads issued before use
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool wide_frame(const SelectArgs &a, int f) {
+    const uint32_t st = a.status[f];
+    return (st & FD_FRAME_TIES) && !(st & FD_FRAME_GUARD);
+}
+
+// [s, e) = workgroup g's share of [0, len) (blocks of ceil(len / G))
+__device__ __forceinline__ void wide_share(uint32_t len, int g, uint32_t &s, uint32_t &e) {
+    const uint32_t b = (len + kRefWideGroups - 1) / kRefWideGroups;
+    s = min(len, static_cast<uint32_t>(g) * b);
+    e = min(len, s + b);
+}
+
+// workgroup (kWT threads) sum; every thread gets it. ws: LDS [kWT / 64]
+__device__ __forceinline__ uint32_t wg_sum(uint32_t v, uint32_t *ws) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t t = wave_incl_add(v);
+    if (lane == kWave - 1) ws[w] = t;
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (int i = 0; i < kWT / kWave; ++i) tot += ws[i];
+    __syncthreads();
+    return tot;
+}
+
+// workgroup exclusive prefix of v; total in tot. ws: LDS [kWT / 64]
+__device__ __forceinline__ uint32_t wg_excl(uint32_t v, uint32_t *ws, uint32_t &tot) {
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_add(v);
+    if (lane == kWave - 1) ws[w] = incl;
+    __syncthreads();
+    uint32_t wb = 0;
+    tot = 0;
+#pragma unroll
+    for (int i = 0; i < kWT / kWave; ++i) {
+        const uint32_t t = ws[i];
+        wb += i < w ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    return wb + incl - v;
+}
+
+__global__ __launch_bounds__(kWT) void k_refw_init(SelectArgs a, RefSortArgs r) {
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f)) return;
+    if (g == 0 && threadIdx.x == 0) {
+        RefCtl &C = r.ctl[f];
+        const uint32_t n = static_cast<uint32_t>(min(static_cast<int64_t>(a.cand_n[f]), a.list_cap));
+        C.n = n;
+        C.nlev = 0;
+        C.bad = 0;
+        C.h[0] = n;
+        C.dep[0] = n > static_cast<uint32_t>(kRefLeaf) ? 2u * (31u - __clz(n)) : 0u;
+        C.act[0] = n > kRefWideMin && C.dep[0] > 0u ? 1u : 0u;
+        for (int l = 1; l <= kRefWideLevels; ++l) C.act[l] = 0u;
+    }
+    if (r.push_order) return;
+    const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
+    uint32_t s, e;
+    wide_share((npx + 31u) >> 5, g, s, e);
+    uint32_t *bits = r.lpos + static_cast<int64_t>(f) * r.cap;
+    for (uint32_t w = s + threadIdx.x; w < e; w += kWT) bits[w] = 0u;
+}
+
+__global__ __launch_bounds__(kWT) void k_refw_bits(SelectArgs a, RefSortArgs r) {
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f)) return;
+    const uint32_t n = r.ctl[f].n;
+    const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
+    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    uint2 *X = r.x + static_cast<int64_t>(f) * r.cap;
+    uint32_t *bits = r.lpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t s, e;
+    wide_share(n, g, s, e);
+    for (uint32_t i0 = s + threadIdx.x; i0 < e; i0 += kWUnroll * kWT) {
+        uint32_t qv[kWUnroll];
+        float rv[kWUnroll];
+#pragma unroll
+        for (int k = 0; k < kWUnroll; ++k) {
+            const uint32_t i = min(i0 + k * kWT, e - 1u);
+            qv[k] = lidx[i];
+            rv[k] = r.push_order ? lresp[i] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < kWUnroll; ++k) {
+            if (i0 + k * kWT >= e) continue;
+            if (r.push_order) X[i0 + k * kWT] = make_uint2(__float_as_uint(rv[k]), qv[k]);
+            else if (qv[k] < npx) atomicOr(&bits[qv[k] >> 5], 1u << (qv[k] & 31u));
+        }
+    }
+}
+
+__global__ __launch_bounds__(kWT) void k_refw_wcount(SelectArgs a, RefSortArgs r) {
+    __shared__ uint32_t ws[kWT / kWave];
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f) || r.push_order) return;
+    const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
+    const uint32_t *bits = r.lpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t s, e;
+    wide_share((npx + 31u) >> 5, g, s, e);
+    uint32_t cnt = 0;
+    for (uint32_t w = s + threadIdx.x; w < e; w += kWT) cnt += __popc(bits[w]);
+    const uint32_t tot = wg_sum(cnt, ws);
+    if (threadIdx.x == 0) r.wcnt[(static_cast<int64_t>(f) * kRefWideGroups + g) * 2] = tot;
+}
+
+__global__ __launch_bounds__(kWT) void k_refw_wprefix(SelectArgs a, RefSortArgs r) {
+    __shared__ uint32_t ws[kWT / kWave];
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f) || r.push_order) return;
+    const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
+    const uint32_t *bits = r.lpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t *wpre = r.rpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t base = 0;
+    for (int i = 0; i < g; ++i) base += r.wcnt[(static_cast<int64_t>(f) * kRefWideGroups + i) * 2];
+    uint32_t s, e;
+    wide_share((npx + 31u) >> 5, g, s, e);
+    // a run of consecutive words per thread
+    const uint32_t per = (e - s + kWT - 1) / kWT;
+    const uint32_t w0 = min(e, s + threadIdx.x * per), w1 = min(e, w0 + per);
+    uint32_t cnt = 0;
+    for (uint32_t w = w0; w < w1; ++w) cnt += __popc(bits[w]);
+    uint32_t tot;
+    uint32_t at = base + wg_excl(cnt, ws, tot);
+    for (uint32_t w = w0; w < w1; ++w) {
+        wpre[w] = at;
+        at += __popc(bits[w]);
+    }
+}
+
+__global__ __launch_bounds__(kWT) void k_refw_place(SelectArgs a, RefSortArgs r) {
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f) || r.push_order) return;
+    const uint32_t n = r.ctl[f].n;
+    const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
+    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    uint2 *X = r.x + static_cast<int64_t>(f) * r.cap;
+    const uint32_t *bits = r.lpos + static_cast<int64_t>(f) * r.cap;
+    const uint32_t *wpre = r.rpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t s, e;
+    wide_share(n, g, s, e);
+    for (uint32_t i0 = s + threadIdx.x; i0 < e; i0 += kWUnroll * kWT) {
+        uint32_t qv[kWUnroll], wp[kWUnroll], wb[kWUnroll];
+        float rv[kWUnroll];
+#pragma unroll
+        for (int k = 0; k < kWUnroll; ++k) {
+            const uint32_t i = min(i0 + k * kWT, e - 1u);
+            qv[k] = lidx[i];
+            rv[k] = lresp[i];
+        }
+#pragma unroll
+        for (int k = 0; k < kWUnroll; ++k) {
+            const uint32_t w = min(qv[k], npx - 1u) >> 5;
+            wp[k] = wpre[w];
+            wb[k] = bits[w];
+        }
+#pragma unroll
+        for (int k = 0; k < kWUnroll; ++k) {
+            const uint32_t q = qv[k];
+            if (i0 + k * kWT >= e || q >= npx) continue;
+            const uint32_t rk = wp[k] + __popc(wb[k] & ((1u << (q & 31u)) - 1u));
+            if (rk < n) X[rk] = make_uint2(__float_as_uint(rv[k]), q);
+        }
+    }
+}
+
+// level l, step 1: the pivot, stopper counts of workgroup g's block of [1, h)
+__global__ __launch_bounds__(kWT) void k_refw_lcount(SelectArgs a, RefSortArgs r, int l) {
+    __shared__ uint32_t ws[kWT / kWave];
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f)) return;
+    RefCtl &C = r.ctl[f];
+    if (!C.act[l]) return;
+    const uint32_t h = C.h[l];
+    const uint2 *X = r.x + static_cast<int64_t>(f) * r.cap;
+    const uint32_t *Xr = reinterpret_cast<const uint32_t *>(X);
+    const uint32_t mid = h / 2u;
+    const uint2 xa = X[1], xb = X[mid], xc = X[h - 1u], x0 = X[0];
+    const uint32_t ch = median_pos(as_f(xa.x), as_f(xb.x), as_f(xc.x), 1u, mid, h - 1u);
+    const uint2 xch = ch == 1u ? xa : (ch == mid ? xb : xc);
+    const float pv = as_f(xch.x);
+    if (g == 0 && threadIdx.x == 0) {
+        C.ch = ch;
+        C.pv = xch.x;
+        C.x0 = x0;
+        C.xch = xch;
+    }
+    uint32_t s, e;
+    wide_share(h - 1u, g, s, e);
+    s += 1u;
+    e += 1u;
+    uint32_t cl = 0, cr = 0;
+    for (uint32_t p0 = s + threadIdx.x; p0 < e; p0 += kWUnroll * kWT) {
+        float rv[kWUnroll];
+#pragma unroll
+        for (int k = 0; k < kWUnroll; ++k) {
+            const uint32_t p = min(p0 + k * kWT, e - 1u);
+            rv[k] = p == ch ? as_f(x0.x) : as_f(Xr[2u * p]);
+        }
+#pragma unroll
+        for (int k = 0; k < kWUnroll; ++k)
+            if (p0 + k * kWT < e) {
+                cl += rv[k] <= pv ? 1u : 0u;
+                cr += rv[k] >= pv ? 1u : 0u;
+            }
+    }
+    const uint32_t tl = wg_sum(cl, ws), tr = wg_sum(cr, ws);
+    if (threadIdx.x == 0) {
+        r.wcnt[(static_cast<int64_t>(f) * kRefWideGroups + g) * 2] = tl;
+        r.wcnt[(static_cast<int64_t>(f) * kRefWideGroups + g) * 2 + 1] = tr;
+    }
+}
+
+// level l, step 2: stopper positions by rank (left stoppers from the left into lpos, right stoppers from
+// the right into rpos); the block is staged in LDS a chunk at a time and each thread ranks a run of it
+__global__ __launch_bounds__(kWT) void k_refw_lscatter(SelectArgs a, RefSortArgs r, int l) {
+    __shared__ uint32_t ws[kWT / kWave];
+    __shared__ uint32_t sres[kWChunk];
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f)) return;
+    RefCtl &C = r.ctl[f];
+    if (!C.act[l]) return;
+    const uint32_t h = C.h[l], ch = C.ch, x0r = C.x0.x;
+    const float pv = as_f(C.pv);
+    const uint32_t *Xr = reinterpret_cast<const uint32_t *>(r.x + static_cast<int64_t>(f) * r.cap);
+    uint32_t *lpos = r.lpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t *rpos = r.rpos + static_cast<int64_t>(f) * r.cap;
+    // bases of this block, totals
+    uint32_t bL = 0, bR = 0, nL = 0, nR = 0;
+    for (int i = 0; i < kRefWideGroups; ++i) {
+        const uint32_t vl = r.wcnt[(static_cast<int64_t>(f) * kRefWideGroups + i) * 2];
+        const uint32_t vr = r.wcnt[(static_cast<int64_t>(f) * kRefWideGroups + i) * 2 + 1];
+        bL += i < g ? vl : 0u;
+        bR += i < g ? vr : 0u;
+        nL += vl;
+        nR += vr;
+    }
+    if (g == 0 && threadIdx.x == 0) {
+        C.nL = nL;
+        C.nR = nR;
+    }
+    uint32_t s, e;
+    wide_share(h - 1u, g, s, e);
+    s += 1u;
+    e += 1u;
+    for (uint32_t cs = s; cs < e; cs += kWChunk) {
+        const uint32_t len = min(static_cast<uint32_t>(kWChunk), e - cs);
+        for (uint32_t j0 = threadIdx.x; j0 < len; j0 += kWUnroll * kWT) {
+            uint32_t v[kWUnroll];
+#pragma unroll
+            for (int k = 0; k < kWUnroll; ++k) {
+                const uint32_t j = min(j0 + k * kWT, len - 1u);
+                v[k] = cs + j == ch ? x0r : Xr[2u * (cs + j)];
+            }
+#pragma unroll
+            for (int k = 0; k < kWUnroll; ++k)
+                if (j0 + k * kWT < len) sres[j0 + k * kWT] = v[k];
+        }
+        __syncthreads();
+        const uint32_t per = (len + kWT - 1) / kWT;
+        const uint32_t j0 = min(len, threadIdx.x * per), j1 = min(len, j0 + per);
+        uint32_t cl = 0, cr = 0;
+        for (uint32_t j = j0; j < j1; ++j) {
+            const float rv = as_f(sres[j]);
+            cl += rv <= pv ? 1u : 0u;
+            cr += rv >= pv ? 1u : 0u;
+        }
+        uint32_t tot;
+        const uint32_t ex = wg_excl(cl | (cr << 16), ws, tot);  // (each field < 2^16: len <= 8192)
+        uint32_t rl = bL + (ex & 0xFFFFu), rr = bR + (ex >> 16);
+        for (uint32_t j = j0; j < j1; ++j) {
+            const uint32_t p = cs + j;
+            const float rv = as_f(sres[j]);
+            const bool ls = rv <= pv, rs = rv >= pv;
+            uint32_t kl = kNone, kr = kNone;
+            if (ls) {
+                kl = rl++;
+                lpos[kl] = p;
+            }
+            if (rs) {
+                kr = nR - 1u - rr++;
+                rpos[kr] = p;
+            }
+            if (p == ch) {
+                C.chL = kl;
+                C.chR = kr;
+            }
+        }
+        bL += tot & 0xFFFFu;
+        bR += tot >> 16;
+        __syncthreads();  // (sres reused by the next chunk)
+    }
+}
+
+// level l, step 3: pairs k < K swapped (t_k = l_k < r_k holds exactly for k < K); the item where t
+// stops holding gives K, the cut and the next level; workgroup 0 moves the pivot to position 0
+__global__ __launch_bounds__(kWT) void k_refw_lswap(SelectArgs a, RefSortArgs r, int l) {
+    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+    if (!wide_frame(a, f)) return;
+    RefCtl &C = r.ctl[f];
+    if (!C.act[l]) return;
+    const uint32_t h = C.h[l], ch = C.ch, nL = C.nL, nR = C.nR;
+    const uint2 x0 = C.x0, xch = C.xch;
+    const uint32_t mn = min(nL, nR);
+    if (mn == 0u) {  // (cannot happen: the median of three leaves a stopper of each kind in [1, h))
+        if (g == 0 && threadIdx.x == 0) C.bad = 1u;
+        return;
+    }
+    uint2 *X = r.x + static_cast<int64_t>(f) * r.cap;
+    const uint32_t *lpos = r.lpos + static_cast<int64_t>(f) * r.cap;
+    const uint32_t *rpos = r.rpos + static_cast<int64_t>(f) * r.cap;
+    uint32_t s, e;
+    wide_share(mn + 1u, g, s, e);  // items k in [0, mn]
+    for (uint32_t k0 = s + threadIdx.x; k0 < e; k0 += 4 * kWT) {
+        uint32_t pl[4], pr[4], ql[4], qr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = min(k0 + u * kWT, mn - 1u);
+            const uint32_t kp = k0 + u * kWT == 0u ? 0u : min(k0 + u * kWT - 1u, mn - 1u);
+            pl[u] = lpos[k];
+            pr[u] = rpos[k];
+            ql[u] = lpos[kp];
+            qr[u] = rpos[kp];
+        }
+        bool t[4];
+        uint2 vl[4], vr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + u * kWT;
+            t[u] = k < e && k < mn && pl[u] < pr[u];
+            if (t[u]) {
+                vl[u] = pl[u] == ch ? x0 : X[pl[u]];
+                vr[u] = pr[u] == ch ? x0 : X[pr[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t k = k0 + u * kWT;
+            if (t[u]) {
+                X[pl[u]] = vr[u];
+                X[pr[u]] = vl[u];
+            }
+            const bool tp = k == 0u || ql[u] < qr[u];
+            if (k < e && tp && !t[u]) {  // K = k
+                uint32_t cut = k < nL ? lpos[k] : kNone;
+                if (k >= 1u) cut = min(cut, qr[u]);
+                const uint32_t d1 = C.dep[l] - 1u;
+                if (cut == 0u || cut >= h) {  // (cannot happen: the scans stop inside the range)
+                    C.bad = 1u;
+                    cut = h;
+                }
+                C.sib_lo[l] = cut;
+                C.sib_hi[l] = h;
+                C.h[l + 1] = cut;
+                C.dep[l + 1] = d1;
+                C.act[l + 1] = l + 1 < kRefWideLevels && cut > kRefWideMin && d1 > 0u && !C.bad ? 1u : 0u;
+                C.nlev = static_cast<uint32_t>(l + 1);
+            }
+        }
+    }
+    if (g == 0 && threadIdx.x == 0) {
+        const uint32_t cl = C.chL, cr = C.chR;
+        const bool swapped = (cl < mn && lpos[cl] < rpos[cl]) || (cr < mn && lpos[cr] < rpos[cr]);
+        X[0] = xch;
+        if (!swapped) X[ch] = x0;
+    }
+}
+
 }  // namespace
 
-hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r, int batch, hipStream_t s) {
+hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r0, int batch, bool wide, hipStream_t s) {
     if (batch <= 0) return hipSuccess;
+    RefSortArgs r = r0;
+    r.wide = wide ? 1 : 0;
+    if (wide) {
+        const dim3 grid(static_cast<unsigned>(batch) * kRefWideGroups), blk(kWT);
+        hipLaunchKernelGGL(k_refw_init, grid, blk, 0, s, a, r);
+        hipLaunchKernelGGL(k_refw_bits, grid, blk, 0, s, a, r);
+        if (!r.push_order) {
+            hipLaunchKernelGGL(k_refw_wcount, grid, blk, 0, s, a, r);
+            hipLaunchKernelGGL(k_refw_wprefix, grid, blk, 0, s, a, r);
+            hipLaunchKernelGGL(k_refw_place, grid, blk, 0, s, a, r);
+        }
+        for (int l = 0; l < kRefWideLevels; ++l) {
+            hipLaunchKernelGGL(k_refw_lcount, grid, blk, 0, s, a, r, l);
+            hipLaunchKernelGGL(k_refw_lscatter, grid, blk, 0, s, a, r, l);
+            hipLaunchKernelGGL(k_refw_lswap, grid, blk, 0, s, a, r, l);
+        }
+    }
     hipLaunchKernelGGL(k_select_reference<kRefThreads>, dim3(static_cast<unsigned>(batch)), dim3(kRefThreads), 0, s, a, r);
     return hipGetLastError();
 }

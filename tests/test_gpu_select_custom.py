@@ -79,13 +79,17 @@ def _dev_lists(lists):
     return tuple(x.cuda() for x in (*t, counts))
 
 
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("seed", range(6))
-def test_reference_order_emulation_stress(fd, oracle, seed):
+def test_reference_order_emulation_stress(fd, oracle, seed, wide, monkeypatch):
     """libstdc++'s introsort emulated on the GPU (k_select_reference) on lists with heavy ties: sizes
     around the 16-element threshold and up to 60k, responses from small integer sets (most comparisons
     meet equal keys) or continuous, needs that stop in the first window or run through several (dist 0:
     every visited candidate is kept), with and without the occupancy grid. Device lists, so the GPU
-    result stands alone; against the oracle's std::sort (sort_mode 0)."""
+    result stands alone; against the oracle's std::sort (sort_mode 0). wide: the multi-workgroup
+    prelude forced on (FD_REF_WIDE=1; by default it runs for frames of >= 1 Mpx only): the 60k list
+    goes through three prelude levels before k_select_reference."""
+    monkeypatch.setenv("FD_REF_WIDE", "1" if wide else "0")
     rng = np.random.default_rng(seed)
     rows, cols = 480, 640
     sizes = [0, 1, 2, 15, 16, 17, 18, 33, 300, 2047, 2049, 5000, 60000]

@@ -26,6 +26,15 @@ def fd():
     return fd
 
 
+@pytest.fixture(autouse=True, params=["auto", "wide", "narrow"])
+def ref_wide(request, monkeypatch):
+    """k_select_reference's multi-workgroup prelude (push order and the first partition levels of large
+    frames): by frame size (>= 1 Mpx, "auto"), forced on or forced off (FD_REF_WIDE)."""
+    if request.param != "auto":
+        monkeypatch.setenv("FD_REF_WIDE", "1" if request.param == "wide" else "0")
+    return request.param
+
+
 def _both(fd, oracle, name, frames, need, dist, prior=None):
     ref = fd.detect_points(name, frames, need, dist, THR[name], prior=prior)
     ras = fd.detect_points(name, frames, need, dist, THR[name], prior=prior, ties="raster")
