@@ -138,6 +138,7 @@ struct OrderedArgs {
 // workgroups per flagged frame, while that range has more than kRefWideMin elements.
 constexpr int kRefWideLevels = 8;
 constexpr int kRefWideGroups = 32;
+constexpr int kRefWideSlots = 32;  // flagged frames in flight per prelude kernel (more: each workgroup loops)
 constexpr uint32_t kRefWideMin = 8192;
 struct RefCtl {  // per frame, written by the prelude, read by k_select_reference
     uint32_t n, nlev, bad;
@@ -159,6 +160,7 @@ struct RefSortArgs {
     uint32_t *dbg;   // [batch][8] first broken invariant per frame (FD_REF_DEBUG), or null
     RefCtl *ctl;     // [batch] wide prelude state (launch_select_reference with wide), else unused
     uint32_t *wcnt;  // [batch][kRefWideGroups][2] per-workgroup counts of the prelude
+    uint32_t *wfr;   // [1 + batch] the prelude's compact list: count, flagged frames
     int wide;        // set by the launcher: the prelude ran (push order and the first levels are done)
 };
 

@@ -58,7 +58,7 @@ struct fd_ctx {
     int status_batch = 0;
     int tie_order = FD_TIES_RASTER;
     DevBuf ord, ord_meta;  // FD_TIES_REFERENCE host path: host-computed visiting orders of flagged frames
-    DevBuf r_x, r_lpos, r_rpos, r_ord, r_ctl, r_wcnt;  // FD_TIES_REFERENCE on the GPU (k_select_reference scratch)
+    DevBuf r_x, r_lpos, r_rpos, r_ord, r_ctl, r_wcnt, r_wfr;  // FD_TIES_REFERENCE on the GPU (k_select_reference scratch)
     DevBuf run_lut;        // FAST score per 16-bit ring mask (FastOffsets::run_lut), filled once
     // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
     DevBuf l_lnorm, l_langle, l_fbase;
@@ -454,6 +454,8 @@ int ref_buffers(fd_ctx *c, int batch, int rows, int cols, int64_t cap, fdk::RefS
     FD_HIP_TRY(c, ensure(c, c->r_wcnt, sizeof(uint32_t) * 2 * fdk::kRefWideGroups * static_cast<size_t>(batch)));
     r.ctl = as<fdk::RefCtl>(c->r_ctl);
     r.wcnt = as<uint32_t>(c->r_wcnt);
+    FD_HIP_TRY(c, ensure(c, c->r_wfr, sizeof(uint32_t) * (1 + static_cast<size_t>(batch))));
+    r.wfr = as<uint32_t>(c->r_wfr);
     r.x = as<uint2>(c->r_x);
     r.lpos = as<uint32_t>(c->r_lpos);
     r.rpos = as<uint32_t>(c->r_rpos);

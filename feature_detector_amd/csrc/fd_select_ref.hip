@@ -34,6 +34,7 @@
 // gets FD_FRAME_UNRESOLVED and keeps k_select's features (the host resolves it when it synchronises).
 #include "fd_greedy.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace fdk {
@@ -988,7 +989,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
 // its first partition levels (the window's leftmost range [0, h) halves per level) through chains of
 // memory round trips on one CU. The prelude spreads exactly that work over kRefWideGroups workgroups per
 // frame, one kernel per step (the kernel boundary is the only cross-workgroup hand-off):
-//   push: k_refw_init (state, bitmap cleared) -> k_refw_bits (raster bitmap, global atomics) ->
+//   push: k_refw_init (state; the flagged frames into a compact list) -> k_refw_clear -> k_refw_bits (raster bitmap, global atomics) ->
 //         k_refw_wcount (set bits per word slice) -> k_refw_wprefix (word prefix) -> k_refw_place
 //         (X[rank] = candidate);
 //   per level l while h > kRefWideMin: k_refw_lcount (pivot = median of X[1], X[h/2], X[h-1]; stopper
@@ -1045,20 +1046,25 @@ __device__ __forceinline__ uint32_t wg_excl(uint32_t v, uint32_t *ws, uint32_t &
     return wb + incl - v;
 }
 
+// one workgroup per frame: the state of a flagged frame, and the frame into the compact list the other
+// prelude kernels walk (their grids cover min(batch, kRefWideSlots) frames x kRefWideGroups)
 __global__ __launch_bounds__(kWT) void k_refw_init(SelectArgs a, RefSortArgs r) {
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
-    if (!wide_frame(a, f)) return;
-    if (g == 0 && threadIdx.x == 0) {
-        RefCtl &C = r.ctl[f];
-        const uint32_t n = static_cast<uint32_t>(min(static_cast<int64_t>(a.cand_n[f]), a.list_cap));
-        C.n = n;
-        C.nlev = 0;
-        C.bad = 0;
-        C.h[0] = n;
-        C.dep[0] = n > static_cast<uint32_t>(kRefLeaf) ? 2u * (31u - __clz(n)) : 0u;
-        C.act[0] = n > kRefWideMin && C.dep[0] > 0u ? 1u : 0u;
-        for (int l = 1; l <= kRefWideLevels; ++l) C.act[l] = 0u;
-    }
+    const int f = blockIdx.x;
+    if (!wide_frame(a, f) || threadIdx.x != 0) return;
+    RefCtl &C = r.ctl[f];
+    const uint32_t n = static_cast<uint32_t>(min(static_cast<int64_t>(a.cand_n[f]), a.list_cap));
+    C.n = n;
+    C.nlev = 0;
+    C.bad = 0;
+    C.h[0] = n;
+    C.dep[0] = n > static_cast<uint32_t>(kRefLeaf) ? 2u * (31u - __clz(n)) : 0u;
+    C.act[0] = n > kRefWideMin && C.dep[0] > 0u ? 1u : 0u;
+    for (int l = 1; l <= kRefWideLevels; ++l) C.act[l] = 0u;
+    const uint32_t j = atomicAdd(&r.wfr[0], 1u);
+    r.wfr[1 + j] = static_cast<uint32_t>(f);
+}
+
+__device__ __forceinline__ void refw_clear(const SelectArgs &a, const RefSortArgs &r, int f, int g, int) {
     if (r.push_order) return;
     const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
     uint32_t s, e;
@@ -1067,8 +1073,7 @@ __global__ __launch_bounds__(kWT) void k_refw_init(SelectArgs a, RefSortArgs r) 
     for (uint32_t w = s + threadIdx.x; w < e; w += kWT) bits[w] = 0u;
 }
 
-__global__ __launch_bounds__(kWT) void k_refw_bits(SelectArgs a, RefSortArgs r) {
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+__device__ __forceinline__ void refw_bits(const SelectArgs &a, const RefSortArgs &r, int f, int g, int) {
     if (!wide_frame(a, f)) return;
     const uint32_t n = r.ctl[f].n;
     const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
@@ -1096,9 +1101,8 @@ __global__ __launch_bounds__(kWT) void k_refw_bits(SelectArgs a, RefSortArgs r) 
     }
 }
 
-__global__ __launch_bounds__(kWT) void k_refw_wcount(SelectArgs a, RefSortArgs r) {
+__device__ __forceinline__ void refw_wcount(const SelectArgs &a, const RefSortArgs &r, int f, int g, int) {
     __shared__ uint32_t ws[kWT / kWave];
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
     if (!wide_frame(a, f) || r.push_order) return;
     const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
     const uint32_t *bits = r.lpos + static_cast<int64_t>(f) * r.cap;
@@ -1110,9 +1114,8 @@ __global__ __launch_bounds__(kWT) void k_refw_wcount(SelectArgs a, RefSortArgs r
     if (threadIdx.x == 0) r.wcnt[(static_cast<int64_t>(f) * kRefWideGroups + g) * 2] = tot;
 }
 
-__global__ __launch_bounds__(kWT) void k_refw_wprefix(SelectArgs a, RefSortArgs r) {
+__device__ __forceinline__ void refw_wprefix(const SelectArgs &a, const RefSortArgs &r, int f, int g, int) {
     __shared__ uint32_t ws[kWT / kWave];
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
     if (!wide_frame(a, f) || r.push_order) return;
     const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
     const uint32_t *bits = r.lpos + static_cast<int64_t>(f) * r.cap;
@@ -1134,8 +1137,7 @@ __global__ __launch_bounds__(kWT) void k_refw_wprefix(SelectArgs a, RefSortArgs 
     }
 }
 
-__global__ __launch_bounds__(kWT) void k_refw_place(SelectArgs a, RefSortArgs r) {
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+__device__ __forceinline__ void refw_place(const SelectArgs &a, const RefSortArgs &r, int f, int g, int) {
     if (!wide_frame(a, f) || r.push_order) return;
     const uint32_t n = r.ctl[f].n;
     const uint32_t npx = static_cast<uint32_t>(a.rows) * static_cast<uint32_t>(a.cols);
@@ -1172,9 +1174,8 @@ __global__ __launch_bounds__(kWT) void k_refw_place(SelectArgs a, RefSortArgs r)
 }
 
 // level l, step 1: the pivot, stopper counts of workgroup g's block of [1, h)
-__global__ __launch_bounds__(kWT) void k_refw_lcount(SelectArgs a, RefSortArgs r, int l) {
+__device__ __forceinline__ void refw_lcount(const SelectArgs &a, const RefSortArgs &r, int f, int g, int l) {
     __shared__ uint32_t ws[kWT / kWave];
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
     if (!wide_frame(a, f)) return;
     RefCtl &C = r.ctl[f];
     if (!C.act[l]) return;
@@ -1220,10 +1221,9 @@ __global__ __launch_bounds__(kWT) void k_refw_lcount(SelectArgs a, RefSortArgs r
 
 // level l, step 2: stopper positions by rank (left stoppers from the left into lpos, right stoppers from
 // the right into rpos); the block is staged in LDS a chunk at a time and each thread ranks a run of it
-__global__ __launch_bounds__(kWT) void k_refw_lscatter(SelectArgs a, RefSortArgs r, int l) {
+__device__ __forceinline__ void refw_lscatter(const SelectArgs &a, const RefSortArgs &r, int f, int g, int l) {
     __shared__ uint32_t ws[kWT / kWave];
     __shared__ uint32_t sres[kWChunk];
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
     if (!wide_frame(a, f)) return;
     RefCtl &C = r.ctl[f];
     if (!C.act[l]) return;
@@ -1301,8 +1301,7 @@ __global__ __launch_bounds__(kWT) void k_refw_lscatter(SelectArgs a, RefSortArgs
 
 // level l, step 3: pairs k < K swapped (t_k = l_k < r_k holds exactly for k < K); the item where t
 // stops holding gives K, the cut and the next level; workgroup 0 moves the pivot to position 0
-__global__ __launch_bounds__(kWT) void k_refw_lswap(SelectArgs a, RefSortArgs r, int l) {
-    const int f = blockIdx.x / kRefWideGroups, g = blockIdx.x % kRefWideGroups;
+__device__ __forceinline__ void refw_lswap(const SelectArgs &a, const RefSortArgs &r, int f, int g, int l) {
     if (!wide_frame(a, f)) return;
     RefCtl &C = r.ctl[f];
     if (!C.act[l]) return;
@@ -1373,6 +1372,24 @@ __global__ __launch_bounds__(kWT) void k_refw_lswap(SelectArgs a, RefSortArgs r,
     }
 }
 
+// the prelude kernels: workgroup (slot, g) takes flagged frames slot, slot + slots, ... of the list
+#define FD_REFW_KERNEL(name)                                                                         \
+    __global__ __launch_bounds__(kWT) void k_##name(SelectArgs a, RefSortArgs r, int l) {          \
+        const int g = static_cast<int>(blockIdx.x % kRefWideGroups);                                \
+        const uint32_t slots = gridDim.x / kRefWideGroups, cnt = r.wfr[0];                          \
+        for (uint32_t j = blockIdx.x / kRefWideGroups; j < cnt; j += slots)                         \
+            name(a, r, static_cast<int>(r.wfr[1 + j]), g, l);                                       \
+    }
+FD_REFW_KERNEL(refw_clear)
+FD_REFW_KERNEL(refw_bits)
+FD_REFW_KERNEL(refw_wcount)
+FD_REFW_KERNEL(refw_wprefix)
+FD_REFW_KERNEL(refw_place)
+FD_REFW_KERNEL(refw_lcount)
+FD_REFW_KERNEL(refw_lscatter)
+FD_REFW_KERNEL(refw_lswap)
+#undef FD_REFW_KERNEL
+
 }  // namespace
 
 hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r0, int batch, bool wide, hipStream_t s) {
@@ -1380,13 +1397,16 @@ hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r0, i
     RefSortArgs r = r0;
     r.wide = wide ? 1 : 0;
     if (wide) {
-        const dim3 grid(static_cast<unsigned>(batch) * kRefWideGroups), blk(kWT);
-        hipLaunchKernelGGL(k_refw_init, grid, blk, 0, s, a, r);
-        hipLaunchKernelGGL(k_refw_bits, grid, blk, 0, s, a, r);
+        const dim3 grid(static_cast<unsigned>(std::min(batch, kRefWideSlots)) * kRefWideGroups), blk(kWT);
+        hipError_t e = hipMemsetAsync(r.wfr, 0, sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_refw_init, dim3(static_cast<unsigned>(batch)), blk, 0, s, a, r);
+        if (!r.push_order) hipLaunchKernelGGL(k_refw_clear, grid, blk, 0, s, a, r, 0);
+        hipLaunchKernelGGL(k_refw_bits, grid, blk, 0, s, a, r, 0);
         if (!r.push_order) {
-            hipLaunchKernelGGL(k_refw_wcount, grid, blk, 0, s, a, r);
-            hipLaunchKernelGGL(k_refw_wprefix, grid, blk, 0, s, a, r);
-            hipLaunchKernelGGL(k_refw_place, grid, blk, 0, s, a, r);
+            hipLaunchKernelGGL(k_refw_wcount, grid, blk, 0, s, a, r, 0);
+            hipLaunchKernelGGL(k_refw_wprefix, grid, blk, 0, s, a, r, 0);
+            hipLaunchKernelGGL(k_refw_place, grid, blk, 0, s, a, r, 0);
         }
         for (int l = 0; l < kRefWideLevels; ++l) {
             hipLaunchKernelGGL(k_refw_lcount, grid, blk, 0, s, a, r, l);
