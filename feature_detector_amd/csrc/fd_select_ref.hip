@@ -185,6 +185,93 @@ __device__ __forceinline__ void set_active(RefLds &L, uint32_t win_end) {
     }
 }
 
+// Position of the k-th set bit (0-based) of m; m must hold more than k bits.
+__device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t k) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t c = static_cast<uint32_t>(__popcll(m & ((1ull << step) - 1ull)));
+        if (k >= c) {
+            k -= c;
+            m >>= step;
+            pos += static_cast<uint32_t>(step);
+        }
+    }
+    return pos;
+}
+
+// One wave, one element per lane: libstdc++'s introsort on a range of 17..64 elements (E[0, len), in
+// LDS) to the end, every subrange of a level partitioned at once. Lane p keeps its subrange [sa, sb);
+// stopper ranks are popcounts of the subrange's ballot, the k-th stopper's position a bit select, the
+// exchanges and the pivot move shuffles. Leaves: stable rank by response, descending, into ordp.
+// Returns false if a subrange would reach the depth limit.
+__device__ bool ref_wave_small(const uint2 *E, uint32_t len, uint32_t dep, uint32_t *ordp) {
+    const uint32_t p = static_cast<uint32_t>(lane_id());
+    uint2 v = p < len ? E[p] : make_uint2(0u, 0u);
+    uint32_t sa = 0, sb = len, dp = dep;
+    for (int it = 0; it < 64; ++it) {
+        const bool big = p < len && sb - sa > static_cast<uint32_t>(kRefLeaf);
+        if (ballot(big) == 0ull) break;
+        if (ballot(big && dp == 0u) != 0ull) return false;  // std::__partial_sort
+        // pivot: __move_median_to_first(sa, sa + 1, mid, sb - 1)
+        const uint32_t mid = sa + (sb - sa) / 2u;
+        const uint32_t i1 = min(sa + 1u, 63u), i2 = min(mid, 63u), i3 = sb >= 1u ? min(sb - 1u, 63u) : 0u;
+        const float ra = __uint_as_float(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(i1))));
+        const float rb = __uint_as_float(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(i2))));
+        const float rc = __uint_as_float(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(i3))));
+        const uint32_t ch = median_pos(ra, rb, rc, sa + 1u, mid, sb - 1u);
+        uint32_t src = p;
+        if (big) src = p == sa ? ch : (p == ch ? sa : p);
+        v.x = static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(min(src, 63u))));
+        v.y = static_cast<uint32_t>(__shfl(static_cast<int>(v.y), static_cast<int>(min(src, 63u))));
+        const float pv = __uint_as_float(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(min(sa, 63u)))));
+        // stoppers of (sa, sb)
+        const bool in = big && p > sa && p < sb;
+        const float rv = __uint_as_float(v.x);
+        const uint64_t BL = ballot(in && rv <= pv), BR = ballot(in && rv >= pv);
+        const uint64_t hiMask = sb >= 64u ? ~0ull : ((1ull << sb) - 1ull);
+        const uint64_t seg = hiMask & ~((2ull << min(sa, 62u)) - 1ull);  // bits (sa, sb)
+        const uint64_t bl = BL & seg, br = BR & seg;
+        const uint32_t nL = static_cast<uint32_t>(__popcll(bl)), nR = static_cast<uint32_t>(__popcll(br));
+        // pair k = p - (sa + 1): t_k = l_k < r_k (r_k: the k-th right stopper from the right)
+        const uint32_t k = p - (sa + 1u);
+        const uint32_t mn = min(nL, nR);
+        const bool tk = in && k < mn && select_bit(bl, k) < select_bit(br, nR - 1u - k);
+        const uint64_t T = ballot(tk) & seg;
+        const uint32_t K = static_cast<uint32_t>(__builtin_ctzll(~(T >> min(sa + 1u, 63u))));
+        // exchanges
+        const uint64_t below = (1ull << p) - 1ull;
+        const uint64_t above = p >= 63u ? 0ull : ~((2ull << p) - 1ull);
+        const uint32_t rankL = static_cast<uint32_t>(__popcll(bl & below));
+        const uint32_t rankR = static_cast<uint32_t>(__popcll(br & above));
+        const bool isL = ((bl >> p) & 1ull) != 0ull, isR = ((br >> p) & 1ull) != 0ull;
+        uint32_t s2 = p;
+        if (isL && rankL < K) s2 = select_bit(br, nR - 1u - rankL);
+        else if (isR && rankR < K) s2 = select_bit(bl, rankR);
+        v.x = static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(s2)));
+        v.y = static_cast<uint32_t>(__shfl(static_cast<int>(v.y), static_cast<int>(s2)));
+        if (big) {
+            uint32_t cut = 0xFFFFFFFFu;
+            if (K < nL) cut = select_bit(bl, K);
+            if (K >= 1u) cut = min(cut, select_bit(br, nR - K));
+            if (p < cut) sb = cut;
+            else sa = cut;
+            --dp;
+        }
+    }
+    // leaves: stable rank within [sa, sb)
+    const float ri = __uint_as_float(v.x);
+    uint32_t rk = 0;
+#pragma unroll
+    for (int j = 0; j < kRefLeaf; ++j) {
+        const uint32_t t = sa + static_cast<uint32_t>(j);
+        const float rt = __uint_as_float(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(min(t, 63u)))));
+        rk += (t < sb && (rt > ri || (rt == ri && t < p))) ? 1u : 0u;
+    }
+    if (p < len) ordp[sa + rk] = v.y;
+    return true;
+}
+
 // One wave: libstdc++'s introsort on X[lo, hi) (<= kRefWaveLocal elements, > kRefLeaf) to the end -- the
 // same partitions as the workgroup levels (median of (first + 1, mid, last - 1) moved to first, left
 // stoppers resp <= pivot from the left paired with right stoppers resp >= pivot from the right while
@@ -206,8 +293,15 @@ __device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     while (top > 0) {
         --top;
-        const uint32_t ent = stk[top];
+        const uint32_t ent = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(stk[top])));
         const uint32_t a = ent & 1023u, b = (ent >> 10) & 2047u, dp = ent >> 21;
+        if (b - a <= static_cast<uint32_t>(kWave) && b - a > static_cast<uint32_t>(kRefLeaf)) {
+            if (!ref_wave_small(E + a, b - a, dp, ord + lo + a)) {
+                ok = false;
+                break;
+            }
+            continue;
+        }
         if (b - a <= static_cast<uint32_t>(kRefLeaf)) {
             // leaf: stable rank by response, descending (lanes 0-15)
             const int len = static_cast<int>(b - a);
