@@ -82,6 +82,8 @@ struct alignas(16) RefLds {
     uint32_t leaf_lo[2 * kRefMaxRanges], leaf_hi[2 * kRefMaxRanges];
     // ranges of <= kRefWaveLocal elements handed to single waves (first window only), and the waves' stacks
     uint32_t wl_lo[kRefMaxRanges], wl_hi[kRefMaxRanges], wl_dep[kRefMaxRanges];
+    uint32_t wl_ord[kRefMaxRanges];  // the list by size, largest first
+    int wl_next;                     // next entry of wl_ord for a free wave
     uint32_t wstk[kRefWaves][kRefStack];
     uint32_t wsum[kRefWaves];
     uint16_t rid[kRefRidCap];  // levels with T <= kRefRidCap: each element's active range (set by pass 1)
@@ -1008,9 +1010,26 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             uint16_t *const Lp = reinterpret_cast<uint16_t *>(wb + kRefWaveLocal * 8u);
             uint16_t *const Rp = Lp + kRefWaveLocal;
             const int nw = L.n_wl;
+            // largest ranges first, each to whichever wave is free (longest-processing-time order)
+            if (tid < nw) {
+                const uint32_t st = L.wl_hi[tid] - L.wl_lo[tid];
+                uint32_t rk = 0;
+                for (int u = 0; u < nw; ++u) {
+                    const uint32_t su = L.wl_hi[u] - L.wl_lo[u];
+                    rk += (su > st || (su == st && u < tid)) ? 1u : 0u;
+                }
+                L.wl_ord[rk] = static_cast<uint32_t>(tid);
+            }
+            if (tid == 0) L.wl_next = kRefWaves;
+            __syncthreads();
             bool ok = true;
-            for (int j = wv; j < nw && ok; j += kRefWaves)
-                ok = ref_wave_resolve(X, ord, L.wl_lo[j], L.wl_hi[j], L.wl_dep[j], E, Lp, Rp, L.wstk[wv]);
+            for (int j = wv; j < nw && ok;) {
+                const uint32_t q = L.wl_ord[j];
+                ok = ref_wave_resolve(X, ord, L.wl_lo[q], L.wl_hi[q], L.wl_dep[q], E, Lp, Rp, L.wstk[wv]);
+                int nj = 0;
+                if (lane == 0) nj = atomicAdd(&L.wl_next, 1);
+                j = __builtin_amdgcn_readfirstlane(__shfl(nj, 0));
+            }
             if (!ok && lane == 0) L.fail = 5;
             __syncthreads();
             if (tid == 0) L.n_wl = 0;
