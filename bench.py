@@ -35,8 +35,8 @@ MFMA_PEAK_TFLOPS_FP16 = 2500.0  # dense BF16/FP16 MFMA (MI355X_MICROARCH.md: ~2.
 # HBM traffic per launch measured with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) and
 # corrected by the calibrated gfx950 factor (tools/gpu_traffic.sh, tools/calib/fetch_calib.hip).
 # (tools/gpu_round_pmc.sh + tools/make_round_profiles.py write both files)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r03_traffic.json")
-SQ_FILE = os.path.join(ROOT, "profiles", "r03_sq.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04_traffic.json")
+SQ_FILE = os.path.join(ROOT, "profiles", "r04_sq.json")
 
 
 def north_star_issue():
