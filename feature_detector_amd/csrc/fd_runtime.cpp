@@ -726,6 +726,13 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
                                      (unsigned long long)q[26], (unsigned long long)q[27], (unsigned long long)q[28],
                                      (unsigned long long)q[29], (unsigned long long)q[30], (unsigned long long)q[20],
                                      (unsigned long long)q[23], (unsigned long long)q[21], (unsigned long long)q[22]);
+                    if (q[18]) {
+                        std::fprintf(stderr, "  levels (T:cycles):");
+                        for (int l = 0; l < 16 && l < static_cast<int>(q[18]); ++l)
+                            std::fprintf(stderr, " %llu:%llu", (unsigned long long)(q[l] >> 40),
+                                         (unsigned long long)(q[l] & ((1ull << 40) - 1)));
+                        std::fprintf(stderr, "\n");
+                    }
                 }
             }
             if (ref_debug) {

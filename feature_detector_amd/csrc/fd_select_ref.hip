@@ -424,7 +424,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
     if (!(st0 & FD_FRAME_TIES) || (st0 & FD_FRAME_GUARD)) return;
     uint64_t t_mark = a.stamps && tid == 0 ? __builtin_readcyclecounter() : 0ull;
     if (a.stamps && tid == 0)
-        for (int k = 16; k < 32; ++k) a.stamps[static_cast<int64_t>(f) * 32 + k] = 0;  // (k_select's probe slots)
+        for (int k = 0; k < 32; ++k) a.stamps[static_cast<int64_t>(f) * 32 + k] = 0;  // (after k_select's printout)
     const uint32_t n = static_cast<uint32_t>(min(static_cast<int64_t>(a.cand_n[f]), a.list_cap));
     const int rows = a.rows, cols = a.cols, d = a.dist;
     const uint32_t npx = static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols);
@@ -596,6 +596,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         if (m > 0) {
             // ---- one partition level over the active ranges ----------------------------------------------
             const int c = L.cur;
+            const uint64_t t_level = a.stamps && tid == 0 ? __builtin_readcyclecounter() : 0ull;
             if (tid < m) {
                 const uint32_t lo = L.r_lo[c][tid], hi = L.r_hi[c][tid];
                 if (L.r_dep[c][tid] == 0u) L.fail = 1;  // std::__partial_sort: not emulated
@@ -971,6 +972,12 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             }
             __syncthreads();
             FD_REF_MARK(30);  // children + active prefix
+            if (a.stamps && tid == 0) {  // per level (slots 0-15): T << 40 | cycles
+                const uint64_t lv = a.stamps[static_cast<int64_t>(f) * 32 + 18];
+                if (lv < 16u)
+                    a.stamps[static_cast<int64_t>(f) * 32 + lv] =
+                        (static_cast<uint64_t>(T) << 40) | (__builtin_readcyclecounter() - t_level);
+            }
             FD_REF_COUNT(18, 1u);
             FD_REF_COUNT(19, T);
             if (L.fail) break;
