@@ -70,7 +70,86 @@ __global__ __launch_bounds__(256) void k_bias_relu_pool(const u4 *x, const u4 *b
     }
 }
 
+// First layer of the NN encoders (SuperPoint conv1a: one input channel, 3x3, stride 1, zero padding 1)
+// with its bias and ReLU, written straight to the channels-last fp16 activation. The 3x3 x 1 filter has
+// 9 MACs per output, so the layer is write-bound (64 halves per pixel out, one in): the library
+// convolution takes 1.3 ms per 64 640x480 frames and the bias + ReLU pass another 1 ms
+// (tools/sp_miopen_probe.py); here one pass writes the 2.5 GB once. Each thread keeps one 8-channel
+// group's 72 weights in registers (cv fixed per thread: the grid stride is a multiple of the channel
+// groups) and produces that group for one pixel per step: 9 input halves (from the block's LDS copy of
+// the three input rows; direct 2-byte global gathers left the layer bound by the address unit),
+// float FMA accumulation in tap order, the sum rounded to half, then + bias in float rounded to half and
+// the ReLU (as the bias-free convolution + fd_nn_bias_relu path rounds), one 16-byte store.
+constexpr int kConv1MaxW = 4096;  // frame width the row staging holds
+
+__global__ __launch_bounds__(256) void k_conv3x3_c1_bias_relu(const _Float16 *x, const _Float16 *wt,
+                                                              const _Float16 *bias, u4 *y, int n, int h, int w,
+                                                              int cvec) {
+    const int per = 256 / cvec;  // pixels per block step
+    const int cv = static_cast<int>(threadIdx.x) % cvec;
+    float wf[8][9], bf[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wf[k][t] = static_cast<float>(wt[(cv * 8 + k) * 9 + t]);
+        bf[k] = static_cast<float>(bias[cv * 8 + k]);
+    }
+    // one image row per block step (no per-pixel index division): its three input rows staged in LDS
+    // (zero outside the frame) by 16-byte-per-thread loads where aligned, then the row's pixels over the
+    // threads reading their 9 taps from LDS (8 threads of a pixel read the same words: broadcast)
+    __shared__ _Float16 rin[3][kConv1MaxW + 2];
+    const int rows = n * h;  // (< 2^31: checked on the host)
+    for (int fr = static_cast<int>(blockIdx.x); fr < rows; fr += static_cast<int>(gridDim.x)) {
+        const int yy = fr % h;
+        const _Float16 *f = x + static_cast<int64_t>(fr - yy) * w;  // frame base
+        for (int i = static_cast<int>(threadIdx.x); i < 3 * (w + 2); i += 256) {
+            const int dy = i / (w + 2), c = i - dy * (w + 2) - 1, r = yy + dy - 1;
+            rin[dy][c + 1] = (r >= 0 && r < h && c >= 0 && c < w) ? f[static_cast<int64_t>(r) * w + c]
+                                                                   : static_cast<_Float16>(0.0f);
+        }
+        __syncthreads();
+        u4 *yrow = y + static_cast<int64_t>(fr) * w * cvec;
+        for (int xx = static_cast<int>(threadIdx.x) / cvec; xx < w; xx += per) {
+            float in[9];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) in[dy * 3 + dx] = static_cast<float>(rin[dy][xx + dx]);
+            u4 o;
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) {
+                uint32_t packed = 0;
+#pragma unroll
+                for (int hlf = 0; hlf < 2; ++hlf) {
+                    const int k = k2 * 2 + hlf;
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) acc = __builtin_fmaf(wf[k][t], in[t], acc);
+                    _Float16 v = static_cast<_Float16>(static_cast<float>(static_cast<_Float16>(acc)) + bf[k]);
+                    v = v > static_cast<_Float16>(0.0f) ? v : static_cast<_Float16>(0.0f);
+                    packed |= static_cast<uint32_t>(__builtin_bit_cast(uint16_t, v)) << (16 * hlf);
+                }
+                o[k2] = packed;
+            }
+            yrow[xx * cvec + cv] = o;
+        }
+        __syncthreads();  // (rin reused by the next row)
+    }
+}
+
 }  // namespace
+
+hipError_t launch_conv3x3_c1_bias_relu(const void *x, const void *wt, const void *bias, void *y, int n, int h, int w,
+                                       int c, hipStream_t s) {
+    const int cvec = c / 8;
+    const int64_t rows = static_cast<int64_t>(n) * h;
+    if (rows == 0 || w == 0) return hipSuccess;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(rows, 256 * 32));
+    hipLaunchKernelGGL(k_conv3x3_c1_bias_relu, dim3(grid), dim3(256), 0, s, static_cast<const _Float16 *>(x),
+                       static_cast<const _Float16 *>(wt), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h,
+                       w, cvec);
+    return hipGetLastError();
+}
 
 hipError_t launch_bias_relu(const void *x, const void *bias, void *y, int n, int h, int w, int c, int pool,
                             hipStream_t s) {

@@ -1887,6 +1887,23 @@ int fd_nn_bias_relu(fd_ctx *c, const void *x, const void *bias, int64_t bias_len
     return FD_OK;
 }
 
+int fd_nn_conv3x3_c1(fd_ctx *c, const void *x, const void *weight, const void *bias, int64_t channels, void *y, int n,
+                     int h, int w) {
+    if (!c) return FD_ERR_INVALID;
+    if (!x || !weight || !bias || !y) return fail(c, FD_ERR_INVALID, "bad arguments");
+    if (channels < 8 || channels > 256 || channels % 8 || 256 % (channels / 8))
+        return fail(c, FD_ERR_INVALID, "channels must be 8, 16, 32, 64, 128 or 256");
+    if (n < 0 || h < 0 || w < 0) return fail(c, FD_ERR_INVALID, "need n, h, w >= 0");
+    if (static_cast<int64_t>(n) * h >= (int64_t(1) << 31)) return fail(c, FD_ERR_INVALID, "n * h must be < 2^31");
+    if (w > 4096) return fail(c, FD_ERR_INVALID, "w must be <= 4096");
+    if ((reinterpret_cast<uintptr_t>(y) & 15) || (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weight) |
+                                                  reinterpret_cast<uintptr_t>(bias)) & 1)
+        return fail(c, FD_ERR_INVALID, "y must be 16-byte aligned, x / weight / bias 2-byte aligned");
+    FD_HIP_TRY(c, hipSetDevice(c->device));
+    FD_HIP_TRY(c, fdk::launch_conv3x3_c1_bias_relu(x, weight, bias, y, n, h, w, static_cast<int>(channels), c->stream));
+    return FD_OK;
+}
+
 int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int map_layout, int batch, int channels,
                       int map_rows, int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
                       int io_on_device) {

@@ -206,6 +206,35 @@ def bias_relu(x, bias, pool: bool = False, out=None, ctx: Context | None = None)
     return out
 
 
+def conv1_bias_relu(x, weight, bias, out=None, ctx: Context | None = None):
+    """fd_nn_conv3x3_c1: the encoder's first layer (1 input channel, 3x3, stride 1, padding 1) with its bias
+    and ReLU in one pass: x [N, 1, H, W] fp16 on the device -> [N, C, H, W] fp16 channels-last. The 9
+    products are summed in float and rounded to half, then the bias is added in float and rounded (as the
+    bias-free convolution followed by bias_relu); within fp16 rounding of PyTorch's convolution + ReLU."""
+    import torch
+
+    if not (x.is_cuda and x.dtype == torch.float16 and x.dim() == 4 and x.shape[1] == 1
+            and (x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last))):
+        raise ValueError("conv1_bias_relu: x must be a [N, 1, H, W] float16 device tensor")
+    n, _, h, w = x.shape
+    c = weight.shape[0]
+    if tuple(weight.shape) != (c, 1, 3, 3) or weight.dtype != torch.float16 or bias.numel() != c:
+        raise ValueError("conv1_bias_relu: weight must be [C, 1, 3, 3] float16 and bias C values")
+    if out is None:
+        out = torch.empty((n, c, h, w), dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
+    elif not (out.dtype == torch.float16 and tuple(out.shape) == (n, c, h, w)
+              and out.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError(f"conv1_bias_relu: out must be a channels-last float16 {[n, c, h, w]} tensor")
+    ctx = _resolve_ctx(ctx, x)
+    _bind_stream(ctx, True)
+    wt = weight.detach().contiguous()
+    b = bias.detach().to(device=x.device, dtype=torch.float16).contiguous()
+    rc = _lib.load().fd_nn_conv3x3_c1(ctx.ptr, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wt.data_ptr()),
+                                       ctypes.c_void_p(b.data_ptr()), c, ctypes.c_void_p(out.data_ptr()), n, h, w)
+    _lib.check(ctx.ptr, rc)
+    return out
+
+
 def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = None):
     """fd_nn_descriptors: desc_map [B, C, h, w] float32, xy [B, S, 2] -> descriptors [B, S, C].
 
@@ -313,6 +342,12 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             """conv -> ReLU (-> MaxPool2d(2, 2)): fp16 channels-last activations run the convolution
             without its bias and fd_nn_bias_relu for bias, ReLU and pooling in one pass (PyTorch would make
             three or four elementwise passes over the activation); other inputs take the torch modules."""
+            if x.dtype == torch.float16 and x.is_cuda and conv.in_channels == 1 and conv.kernel_size == (3, 3) \
+                    and conv.stride == (1, 1) and conv.padding == (1, 1) and conv.out_channels in (8, 16, 32, 64, 128, 256) \
+                    and x.dim() == 4 and x.shape[1] == 1 and not pool and not os.environ.get("FD_SP_UNFUSED") \
+                    and not os.environ.get("FD_SP_NO_CONV1"):  # (A/B switches)
+                # first layer: write-bound (9 MACs per output), one pass instead of convolution + bias pass
+                return conv1_bias_relu(x.contiguous(), conv.weight, conv.bias)
             if x.dtype == torch.float16 and x.is_cuda and x.is_contiguous(memory_format=torch.channels_last) \
                     and conv.out_channels % 8 == 0 and not os.environ.get("FD_SP_UNFUSED"):  # (A/B switch)
                 y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding)

@@ -365,6 +365,17 @@ int fd_nn_descriptors(fd_ctx *ctx, const float *map, int map_on_device, int map_
 int fd_nn_bias_relu(fd_ctx *ctx, const void *x, const void *bias, int64_t bias_len, void *y, int n, int h, int w,
                     int c, int pool);
 
+/*
+ * fd_nn_conv3x3_c1 -- the NN encoders' first layer (one input channel, 3x3 filter, stride 1, zero padding
+ * 1; SuperPoint conv1a) with its bias and ReLU, in one pass: y [n][h][w][channels] (channels-last fp16) =
+ * relu(conv(x) + bias) for x [n][h][w] fp16 and weight [channels][1][3][3] fp16, all on the device. The
+ * convolution sums its 9 products in float (FMA, tap order) and rounds to half; the bias is then added in
+ * float and rounded (as a bias-free convolution followed by fd_nn_bias_relu). channels in {8, 16, 32, 64,
+ * 128, 256}; w <= 4096; y 16-byte aligned. Runs on the context's stream.
+ */
+int fd_nn_conv3x3_c1(fd_ctx *ctx, const void *x, const void *weight, const void *bias, int64_t channels, void *y,
+                     int n, int h, int w);
+
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);
 

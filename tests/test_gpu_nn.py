@@ -257,6 +257,43 @@ def _reference_forward(net, x):
 
 
 @pytest.mark.gpu
+def test_conv1_bias_relu_matches_torch(sp):
+    """fd_nn_conv3x3_c1 (first layer: 1 input channel, 3x3, padding 1, + bias + ReLU) against PyTorch's
+    float32 convolution of the same fp16 tensors: within two fp16 rounding steps (the kernel rounds the
+    convolution to half, then the biased sum), on frame edges and ragged sizes; argument checks."""
+    import torch
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    for n, h, w, c in ((2, 17, 23, 64), (1, 480, 640, 64), (3, 8, 9, 8), (1, 5, 300, 256)):
+        x = torch.rand((n, 1, h, w), generator=g, device="cuda").half()
+        wt = (torch.randn((c, 1, 3, 3), generator=g, device="cuda") * 0.5).half()
+        b = (torch.randn(c, generator=g, device="cuda") * 0.2).half()
+        got = sp.conv1_bias_relu(x.contiguous(memory_format=torch.channels_last), wt, b)
+        assert got.is_contiguous(memory_format=torch.channels_last)
+        conv = torch.nn.functional.conv2d(x.float(), wt.float(), None, 1, 1)
+        ref = torch.relu(conv + b.float().view(1, -1, 1, 1))
+        err = (got.float() - ref).abs()
+        tol = (conv.abs() + ref.abs()) * 2.0 ** -10 + 2.0 ** -14  # one half rounding of each sum (+ margin)
+        assert bool((err <= tol).all()), (n, h, w, c, err.max().item())
+        assert bool((got >= 0).all())
+    x = torch.zeros((1, 2, 4, 4), device="cuda", dtype=torch.float16)
+    with pytest.raises(ValueError):
+        sp.conv1_bias_relu(x, torch.zeros((8, 1, 3, 3), device="cuda", dtype=torch.float16),
+                           torch.zeros(8, device="cuda", dtype=torch.float16))  # two input channels
+    x = torch.zeros((1, 1, 4, 4), device="cuda", dtype=torch.float16)
+    with pytest.raises(ValueError):
+        sp.conv1_bias_relu(x, torch.zeros((8, 1, 3, 3), device="cuda", dtype=torch.float16),
+                           torch.zeros(4, device="cuda", dtype=torch.float16))  # short bias
+    import ctypes
+    from feature_detector_amd import _lib
+    ctx = sp._resolve_ctx(None, x)
+    rc = _lib.load().fd_nn_conv3x3_c1(ctx.ptr, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(x.data_ptr()),
+                                       ctypes.c_void_p(x.data_ptr()), 12, ctypes.c_void_p(x.data_ptr()), 1, 4, 4)
+    assert rc != 0  # 12 channels: not a supported group count
+
+
+@pytest.mark.gpu
 def test_bias_relu_matches_torch(sp):
     """fd_nn_bias_relu (bias + ReLU, and + 2x2 max pool, on channels-last fp16) equals PyTorch's separate
     half-precision ops bit for bit. The fused SuperPoint forward runs the convolutions without their bias,

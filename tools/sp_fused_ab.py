@@ -1,5 +1,6 @@
 """A/B of the SuperPoint forward (BASELINE configs[4] shape: 64 x 640x480 fp16, channels last): the fused
-bias + ReLU (+ pool) kernel (fd_nn_bias_relu) against PyTorch's separate elementwise passes
+bias + ReLU (+ pool) kernel (fd_nn_bias_relu) and the one-pass first layer (fd_nn_conv3x3_c1) against
+the fused path without the first-layer kernel (FD_SP_NO_CONV1=1) and PyTorch's separate elementwise passes
 (FD_SP_UNFUSED=1), interleaved in one process; prints ms per 64-frame forward."""
 import os
 import sys
@@ -32,9 +33,12 @@ def timed(reps=10):
 
 
 for rnd in range(2):
-    for mode in ("fused", "unfused"):
+    for mode in ("fused", "no_conv1", "unfused"):
+        os.environ.pop("FD_SP_UNFUSED", None)
+        os.environ.pop("FD_SP_NO_CONV1", None)
         if mode == "unfused":
             os.environ["FD_SP_UNFUSED"] = "1"
-        else:
-            os.environ.pop("FD_SP_UNFUSED", None)
+        elif mode == "no_conv1":
+            os.environ["FD_SP_NO_CONV1"] = "1"
         print(f"round {rnd} {mode}: {timed():.3f} ms per 64-frame forward", flush=True)
+
