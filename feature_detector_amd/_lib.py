@@ -19,7 +19,7 @@ EXPORTS = (
     "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_ctx_set_tie_order", "fd_ctx_frame_status", "fd_points_detect", "fd_points_candidates", "fd_points_response",
     "fd_points_response_append", "fd_points_select",
     "fd_lsd_map", "fd_lsd_map_pitched", "fd_lsd_lines", "fd_lsd_lines_state", "fd_brief_compute", "fd_nn_select", "fd_nn_select_list", "fd_nn_descriptors",
-    "fd_nn_bias_relu", "fd_nn_conv3x3_c1",
+    "fd_nn_bias_relu", "fd_nn_conv3x3_c1", "fd_nn_conv3x3_c64",
     "fd_build_info", "fd_png_info", "fd_png_decode", "fd_png_frames",
     "fd_ingest_create", "fd_ingest_destroy", "fd_ingest_frames", "fd_ingest_submit", "fd_ingest_wait",
 )
@@ -107,6 +107,7 @@ def load() -> ctypes.CDLL:
         "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
         "fd_nn_bias_relu": (i32, [P, P, P, i64, P, i32, i32, i32, i32, i32]),
         "fd_nn_conv3x3_c1": (i32, [P, P, P, P, i64, P, i32, i32, i32]),
+        "fd_nn_conv3x3_c64": (i32, [P, P, P, P, P, i32, i32, i32, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
         "fd_png_info": (i32, [P, ctypes.c_size_t, P, P, P]),
         "fd_png_decode": (i32, [P, ctypes.c_size_t, P, ctypes.c_size_t, P, P]),

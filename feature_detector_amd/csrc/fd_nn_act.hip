@@ -137,7 +137,171 @@ __global__ __launch_bounds__(256) void k_conv3x3_c1_bias_relu(const _Float16 *x,
     }
 }
 
+// 3x3 convolution, 64 -> 64 channels (SuperPoint conv1b, conv2a, conv2b: stride 1, padding 1), with its
+// bias and ReLU and, for the layers a MaxPool2d(2, 2) follows, the pooling, as an implicit GEMM on the
+// matrix cores: M = pixels, N = 64 output channels, K = 9 taps x 64 input channels, in
+// mfma_f32_16x16x32_f16 steps (fp16 products, f32 sums). One workgroup (4 waves) per CU keeps the packed
+// filter ([tap][co][ci], 72 KiB) in LDS and walks tiles of kCvRows rows x 64 columns: the tile's input
+// pixels are staged in LDS (16-byte chunks of 8 channels, XOR-swizzled by column so that 16 lanes reading
+// 16 pixels hit 8 distinct bank groups), each wave computes 16 columns x 4 rows x 64 channels (16
+// accumulators: 4 A and 4 B fragments per K step), and the epilogue rounds the sum to half, adds the
+// bias in float and rounds (as a bias-free convolution + fd_nn_bias_relu), applies the ReLU and the 2x2
+// max within the lane (the accumulator rows are adjacent pixels, the four row blocks adjacent rows),
+// stages the tile in LDS and writes it as whole 128-byte pixels.
+#ifndef FD_C64_UNROLL
+#define FD_C64_UNROLL 1  // the 9 taps unrolled (conv1b + conv2b 1.20 -> 0.96 ms, conv2a 556 -> 459 us per call)
+#endif
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+#ifndef FD_C64_ROWS
+#define FD_C64_ROWS 4
+#endif
+constexpr int kCvRows = FD_C64_ROWS, kCvCols = 64, kCvInRows = kCvRows + 2, kCvInCols = kCvCols + 2;
+
+__device__ __forceinline__ float cv_epilogue(float acc, float b) {
+    const _Float16 v = static_cast<_Float16>(static_cast<float>(static_cast<_Float16>(acc)) + b);
+    return v > static_cast<_Float16>(0.0f) ? static_cast<float>(v) : 0.0f;
+}
+
+template <bool POOL>
+__global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 *wpk, const _Float16 *bias, u4 *y,
+                                                          int n, int h, int w) {
+    __shared__ u4 Wl[9 * 64 * 8];
+    __shared__ u4 In[kCvInRows * kCvInCols * 8];  // (also the output staging after the K loop)
+    const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
+    for (int i = tid; i < 9 * 64 * 8; i += 256) {
+        const int ch = i & 7, row = i >> 3, co = row & 63;
+        Wl[row * 8 + (ch ^ (co & 7))] = wpk[i];
+    }
+    float bv[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) bv[nb] = static_cast<float>(bias[nb * 16 + (lane & 15)]);
+    const int th = (h + kCvRows - 1) / kCvRows, tw = (w + kCvCols - 1) / kCvCols;
+    const int total = n * th * tw;  // (< 2^31: checked on the host)
+    // the input tile goes through registers: the next tile's loads are issued before this tile's K loop
+    // and stored to LDS after it, so their latency hides behind the matrix work
+    constexpr int kChunks = kCvInRows * kCvInCols * 8, kPer = (kChunks + 255) / 256;
+    u4 pre[kPer];
+    auto fetch = [&](int tile) {
+        const int tx = tile % tw, t2 = tile / tw, ty = t2 % th, f = t2 / th;
+        const int r0 = ty * kCvRows, c0 = tx * kCvCols;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = tid + k * 256;
+            const int ch = i & 7, px = i >> 3, pc = px % kCvInCols, pr = px / kCvInCols;
+            const int gy = r0 - 1 + pr, gx = c0 - 1 + pc;
+            pre[k] = u4{0u, 0u, 0u, 0u};
+            if (i < kChunks && tile < total && gy >= 0 && gy < h && gx >= 0 && gx < w)
+                pre[k] = x[((static_cast<int64_t>(f) * h + gy) * w + gx) * 8 + ch];
+        }
+    };
+    fetch(static_cast<int>(blockIdx.x));
+    for (int tile = static_cast<int>(blockIdx.x); tile < total; tile += static_cast<int>(gridDim.x)) {
+        const int tx = tile % tw, t2 = tile / tw, ty = t2 % th, f = t2 / th;
+        const int r0 = ty * kCvRows, c0 = tx * kCvCols;
+        __syncthreads();  // (the previous tile's staging is read out; the filter is in place)
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int i = tid + k * 256;
+            const int px = i >> 3, pc = px % kCvInCols;
+            if (i < kChunks) In[px * 8 + ((i & 7) ^ (pc & 7))] = pre[k];
+        }
+        __syncthreads();
+        fetch(tile + static_cast<int>(gridDim.x));
+        f4 acc[kCvRows][4];
+#pragma unroll
+        for (int m = 0; m < kCvRows; ++m)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) acc[m][nb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#if FD_C64_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dy = tap / 3, dx = tap - dy * 3;
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh) {
+                const int chunk = kh * 4 + (lane >> 4);
+                h8 A[kCvRows], B[4];
+                const int pc = wv * 16 + (lane & 15) + dx;
+#pragma unroll
+                for (int m = 0; m < kCvRows; ++m)
+                    A[m] = __builtin_bit_cast(h8, In[((m + dy) * kCvInCols + pc) * 8 + (chunk ^ (pc & 7))]);
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) {
+                    const int co = nb * 16 + (lane & 15);
+                    B[nb] = __builtin_bit_cast(h8, Wl[(tap * 64 + co) * 8 + (chunk ^ (co & 7))]);
+                }
+#pragma unroll
+                for (int m = 0; m < kCvRows; ++m)
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[m], B[nb], acc[m][nb], 0, 0, 0);
+            }
+        }
+        __syncthreads();  // (In is reused as the output staging)
+        _Float16 *st = reinterpret_cast<_Float16 *>(In);
+        const int col4 = wv * 16 + (lane >> 4) * 4;  // the accumulator's first pixel column in the tile
+        if constexpr (POOL) {
+            // staging [kCvRows / 2 pooled rows][32 pooled columns][64 channels]
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                const int co = nb * 16 + (lane & 15);
+#pragma unroll
+                for (int pr = 0; pr < kCvRows / 2; ++pr)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        const float v = fmaxf(fmaxf(cv_epilogue(acc[2 * pr][nb][2 * q], bv[nb]),
+                                                    cv_epilogue(acc[2 * pr][nb][2 * q + 1], bv[nb])),
+                                              fmaxf(cv_epilogue(acc[2 * pr + 1][nb][2 * q], bv[nb]),
+                                                    cv_epilogue(acc[2 * pr + 1][nb][2 * q + 1], bv[nb])));
+                        st[(pr * 32 + col4 / 2 + q) * 64 + co] = static_cast<_Float16>(v);
+                    }
+            }
+            __syncthreads();
+            const int ho = h >> 1, wo = w >> 1;
+            for (int i = tid; i < kCvRows / 2 * 32 * 8; i += 256) {
+                const int ch = i & 7, px = i >> 3, pc = px & 31, pr = px >> 5;
+                const int gy = r0 / 2 + pr, gx = c0 / 2 + pc;
+                if (gy < ho && gx < wo) y[((static_cast<int64_t>(f) * ho + gy) * wo + gx) * 8 + ch] = In[px * 8 + ch];
+            }
+        } else {
+            // staging [kCvRows rows][64 columns][64 channels]
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                const int co = nb * 16 + (lane & 15);
+#pragma unroll
+                for (int m = 0; m < kCvRows; ++m)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        st[(m * kCvCols + col4 + r) * 64 + co] = static_cast<_Float16>(cv_epilogue(acc[m][nb][r], bv[nb]));
+            }
+            __syncthreads();
+            for (int i = tid; i < kCvRows * kCvCols * 8; i += 256) {
+                const int ch = i & 7, px = i >> 3, pc = px % kCvCols, pr = px / kCvCols;
+                const int gy = r0 + pr, gx = c0 + pc;
+                if (gy < h && gx < w) y[((static_cast<int64_t>(f) * h + gy) * w + gx) * 8 + ch] = In[px * 8 + ch];
+            }
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
+                              hipStream_t s) {
+    const int64_t tiles = static_cast<int64_t>(n) * ((h + kCvRows - 1) / kCvRows) * ((w + kCvCols - 1) / kCvCols);
+    if (tiles == 0) return hipSuccess;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(tiles, 1024));
+    if (pool)
+        hipLaunchKernelGGL(k_conv3x3_c64_mfma<true>, dim3(grid), dim3(256), 0, s, static_cast<const u4 *>(x),
+                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w);
+    else
+        hipLaunchKernelGGL(k_conv3x3_c64_mfma<false>, dim3(grid), dim3(256), 0, s, static_cast<const u4 *>(x),
+                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w);
+    return hipGetLastError();
+}
 
 hipError_t launch_conv3x3_c1_bias_relu(const void *x, const void *wt, const void *bias, void *y, int n, int h, int w,
                                        int c, hipStream_t s) {

@@ -1,6 +1,7 @@
 """A/B of the SuperPoint forward (BASELINE configs[4] shape: 64 x 640x480 fp16, channels last): the fused
 bias + ReLU (+ pool) kernel (fd_nn_bias_relu) and the one-pass first layer (fd_nn_conv3x3_c1) against
-the fused path without the first-layer kernel (FD_SP_NO_CONV1=1) and PyTorch's separate elementwise passes
+the fused path without the 64 -> 64 matrix-core convolutions (FD_SP_NO_C64=1), without both
+(FD_SP_NO_CONV1=1 FD_SP_NO_C64=1: round-3's path) and PyTorch's separate elementwise passes
 (FD_SP_UNFUSED=1), interleaved in one process; prints ms per 64-frame forward."""
 import os
 import sys
@@ -33,12 +34,15 @@ def timed(reps=10):
 
 
 for rnd in range(2):
-    for mode in ("fused", "no_conv1", "unfused"):
-        os.environ.pop("FD_SP_UNFUSED", None)
-        os.environ.pop("FD_SP_NO_CONV1", None)
+    for mode in ("fused", "no_c64", "no_conv1", "unfused"):
+        for k in ("FD_SP_UNFUSED", "FD_SP_NO_CONV1", "FD_SP_NO_C64"):
+            os.environ.pop(k, None)
         if mode == "unfused":
             os.environ["FD_SP_UNFUSED"] = "1"
         elif mode == "no_conv1":
             os.environ["FD_SP_NO_CONV1"] = "1"
+            os.environ["FD_SP_NO_C64"] = "1"
+        elif mode == "no_c64":
+            os.environ["FD_SP_NO_C64"] = "1"
         print(f"round {rnd} {mode}: {timed():.3f} ms per 64-frame forward", flush=True)
 
