@@ -720,7 +720,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
                     const uint64_t *q = all.data() + static_cast<size_t>(b) * 32;
                     if (q[18])
                         std::fprintf(stderr, "k_select_reference frame %d cycles: push %llu | levels %llu sumT %llu: pivots %llu "
-                                             "pass1 %llu bases %llu pass2 %llu pass3 %llu pass4 %llu children %llu | leaves %llu "
+                                             "pass1 %llu bases %llu pass2 %llu (K) %llu pass3 %llu children %llu | leaves %llu "
                                              "wave-local %llu greedy %llu windows %llu\n", b, (unsigned long long)q[16], (unsigned long long)q[18],
                                      (unsigned long long)q[19], (unsigned long long)q[24], (unsigned long long)q[25],
                                      (unsigned long long)q[26], (unsigned long long)q[27], (unsigned long long)q[28],

@@ -49,7 +49,7 @@ constexpr int kRefLeaf = 16;        // libstdc++ _S_threshold
 #define FD_REF_U 4
 #endif
 constexpr int kRefU = FD_REF_U;     // 64-element rounds per wave whose global loads are issued together
-constexpr uint32_t kRefRidCap = 8192;  // flat elements per level whose range index pass 1 caches for passes 2-4
+constexpr uint32_t kRefRidCap = 8192;  // flat elements per level whose range index pass 1 caches for passes 2-3
 // A range of <= kRefWaveLocal elements is partitioned to the end (its whole subtree) by one wave in LDS,
 // with no workgroup barriers, in 12 B per element of the 96 KiB greedy span per wave (elements + stopper
 // positions). A/B on the bench tie frames (tools/gpu_r04f.sh): off / 64 / 128 / 256 / 512 = headline
@@ -76,7 +76,7 @@ struct alignas(16) RefLds {
     float piv[kRefMaxRanges];
     uint32_t headL[kRefMaxRanges], headR[kRefMaxRanges], headW[kRefMaxRanges];
     uint32_t bL[kRefMaxRanges], nL[kRefMaxRanges], eR[kRefMaxRanges], nR[kRefMaxRanges];
-    uint32_t K[kRefMaxRanges], cut[kRefMaxRanges];
+    uint32_t cut[kRefMaxRanges];
     uint32_t waveL[kRefWaves], waveR[kRefWaves];
     // leaves produced by the level
     uint32_t leaf_lo[2 * kRefMaxRanges], leaf_hi[2 * kRefMaxRanges];
@@ -608,16 +608,16 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 X[FD_REF_IDX(lo, n, 3)] = xp;
                 X[FD_REF_IDX(ch, n, 3)] = x0;
                 L.piv[tid] = as_f(xp.x);
-                L.K[tid] = 0;
+                L.cut[tid] = kNoPos;  // (written by the element where l_k < r_k stops holding)
             }
             __syncthreads();
             FD_REF_MARK(24);  // pivots
             if (L.fail) break;
             const uint32_t T = L.T;
-            const bool cached = T <= kRefRidCap;  // passes 2-4 read the range index pass 1 stored
+            const bool cached = T <= kRefRidCap;  // passes 2-3 read the range index pass 1 stored
             // LDS mode (small levels before the first greedy scan): pass 1 also keeps each element's
             // response in LDS (RV) and the stopper positions live in LDS (LP, RP) instead of lpos / rpos:
-            // passes 2 and 3 make no memory round trip, pass 4 one (the swaps themselves).
+            // pass 2 makes no memory round trip, pass 3 one (the swaps themselves).
             const bool ldsm = cached && !grid_ready;
             uint32_t *const RV = L.pxy;  // [kRefRidCap] x 3 over pxy .. grid_lds (96 KiB, see the push)
             uint32_t *const LP = RV + kRefRidCap;
@@ -709,7 +709,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             }
             __syncthreads();
             FD_REF_MARK(26);  // stopper bases
-            // passes 2-4, compiled twice: stopper positions in LDS (LDS mode) or in lpos / rpos
+            // passes 2-3, compiled twice: stopper positions in LDS (LDS mode) or in lpos / rpos
             auto passes = [&](auto lm) {
                 constexpr bool LM = decltype(lm)::value;
                 auto lp_st = [&](uint32_t i, uint32_t v) {
@@ -777,14 +777,18 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 }
                 __syncthreads();
                 FD_REF_MARK(27);  // pass 2
-                // pass 3: K = number of pairs with l_k < r_k (monotone in k: the last true k writes it); the
-                // kRefU rounds' stopper positions loaded together
+                // pass 3 (swaps and cuts in one pass): pair k is exchanged iff t_k = l_k < r_k (monotone in k,
+                // so these are exactly the pairs k < K); the element where t stops holding finds K and writes
+                // the range's cut -- K = k + 1 at the last true pair (cut = min(l_{K}, r_{K-1})), K = 0 at a
+                // false first pair (cut = l_0). The kRefU rounds' stopper positions, then their elements,
+                // loaded together.
                 {
                     int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
                     for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
                         int ju[kRefU];
                         bool vu[kRefU];
                         uint32_t l0[kRefU], r0[kRefU], l1[kRefU], r1[kRefU];
+                        uint2 vl[kRefU], vr[kRefU];
     #pragma unroll
                         for (int u = 0; u < kRefU; ++u) {
                             const uint32_t b = b0 + u * kWave, e = b + lane;
@@ -805,73 +809,46 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                             l1[u] = lp_ld(FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10));
                             r1[u] = rp_ld(FD_REF_IDX(min(e + 1u, L.T - 1u), L.T, 10));
                         }
+                        bool su[kRefU];
     #pragma unroll
                         for (int u = 0; u < kRefU; ++u) {
                             const uint32_t e = b0 + u * kWave + lane;
                             const int j = ju[u];
                             const uint32_t k = e - L.o[j];  // 0-based pair index
-                            const uint32_t mn = min(L.nL[j], L.nR[j]);
+                            const uint32_t nLj = L.nL[j], mn = min(nLj, L.nR[j]);
                             const bool t = vu[u] && k < mn && l0[u] < r0[u];
                             const bool tn = t && k + 1 < mn && l1[u] < r1[u];
-                            if (t && !tn) L.K[j] = k + 1;
-                        }
-                    }
-                }
-                __syncthreads();
-                FD_REF_MARK(28);  // pass 3
-                // pass 4: the swaps; the cuts (the kRefU rounds' stopper positions, then their elements, loaded
-                // together)
-                {
-                    int jw = !cached && e0 < e1 ? range_search(L.o, m, e0) : 0;
-                    for (uint32_t b0 = e0; b0 < e1; b0 += kRefU * kWave) {
-                        bool su[kRefU];
-                        uint32_t pl[kRefU], pr[kRefU];
-                        uint2 vl[kRefU], vr[kRefU];
-    #pragma unroll
-                        for (int u = 0; u < kRefU; ++u) {
-                            const uint32_t b = b0 + u * kWave, e = b + lane;
-                            const bool valid = e < e1;
-                            int j;
-                            if (cached) {
-                                j = valid ? L.rid[e] : 0;
-                            } else {
-                                while (jw + 1 < m && L.o[jw + 1] <= b) ++jw;
-                                j = valid ? range_of(L.o, m, jw, e) : jw;
+                            su[u] = t;
+                            if (t && !tn) {  // K = k + 1
+                                uint32_t cut = r0[u];
+                                if (k + 1 < nLj) cut = min(cut, l1[u]);
+                                L.cut[j] = cut;
+                            } else if (vu[u] && k == 0u && !t) {  // K = 0 (nL >= 1: the median leaves a stopper)
+                                L.cut[j] = l0[u];
                             }
-                            const uint32_t k = e - L.o[j];
-                            su[u] = valid && k < L.K[j];
-                        }
-    #pragma unroll
-                        for (int u = 0; u < kRefU; ++u) {
-                            const uint32_t e = b0 + u * kWave + lane;
-                            pl[u] = su[u] ? FD_REF_IDX(lp_ld(FD_REF_IDX(e, L.T, 11)), n, 12) : 0u;
-                            pr[u] = su[u] ? FD_REF_IDX(rp_ld(FD_REF_IDX(e, L.T, 11)), n, 13) : 0u;
-                        }
-    #pragma unroll
-                        for (int u = 0; u < kRefU; ++u) {
-                            if (su[u]) {
-                                vl[u] = X[pl[u]];
-                                vr[u] = X[pr[u]];
+                            if (t) {
+                                l0[u] = FD_REF_IDX(l0[u], n, 12);
+                                r0[u] = FD_REF_IDX(r0[u], n, 13);
                             }
                         }
     #pragma unroll
                         for (int u = 0; u < kRefU; ++u) {
                             if (su[u]) {
-                                X[pl[u]] = vr[u];
-                                X[pr[u]] = vl[u];
+                                vl[u] = X[l0[u]];
+                                vr[u] = X[r0[u]];
+                            }
+                        }
+    #pragma unroll
+                        for (int u = 0; u < kRefU; ++u) {
+                            if (su[u]) {
+                                X[l0[u]] = vr[u];
+                                X[r0[u]] = vl[u];
                             }
                         }
                     }
-                    if (tid < m) {
-                        const uint32_t K = L.K[tid], oj = L.o[tid];
-                        uint32_t cut = kNoPos;
-                        if (K < L.nL[tid]) cut = lp_ld(FD_REF_IDX(oj + K, L.T, 14));
-                        if (K >= 1u) cut = min(cut, rp_ld(FD_REF_IDX(oj + K - 1u, L.T, 15)));
-                        L.cut[tid] = cut;
-                    }
                 }
                 __syncthreads();
-                FD_REF_MARK(29);  // pass 4
+                FD_REF_MARK(29);  // pass 3 (swaps + cuts)
             };
             if (ldsm) passes(std::true_type{});
             else passes(std::false_type{});
