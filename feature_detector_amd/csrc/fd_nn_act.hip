@@ -213,32 +213,39 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
         for (int m = 0; m < kCvRows; ++m)
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) acc[m][nb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-#if FD_C64_UNROLL
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
-        for (int tap = 0; tap < 9; ++tap) {
+        // the 18 K steps (tap, channel half) with the next step's fragments read from LDS before this
+        // step's matrix instructions, so the LDS latency hides behind them (one wave per SIMD: no other
+        // wave would cover it)
+        auto frag = [&](int step, h8 (&A)[kCvRows], h8 (&B)[4]) {
+            const int tap = step >> 1, kh = step & 1;
             const int dy = tap / 3, dx = tap - dy * 3;
+            const int chunk = kh * 4 + (lane >> 4);
+            const int pc = wv * 16 + (lane & 15) + dx;
 #pragma unroll
-            for (int kh = 0; kh < 2; ++kh) {
-                const int chunk = kh * 4 + (lane >> 4);
-                h8 A[kCvRows], B[4];
-                const int pc = wv * 16 + (lane & 15) + dx;
+            for (int m = 0; m < kCvRows; ++m)
+                A[m] = __builtin_bit_cast(h8, In[((m + dy) * kCvInCols + pc) * 8 + (chunk ^ (pc & 7))]);
 #pragma unroll
-                for (int m = 0; m < kCvRows; ++m)
-                    A[m] = __builtin_bit_cast(h8, In[((m + dy) * kCvInCols + pc) * 8 + (chunk ^ (pc & 7))]);
-#pragma unroll
-                for (int nb = 0; nb < 4; ++nb) {
-                    const int co = nb * 16 + (lane & 15);
-                    B[nb] = __builtin_bit_cast(h8, Wl[(tap * 64 + co) * 8 + (chunk ^ (co & 7))]);
-                }
-#pragma unroll
-                for (int m = 0; m < kCvRows; ++m)
-#pragma unroll
-                    for (int nb = 0; nb < 4; ++nb)
-                        acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[m], B[nb], acc[m][nb], 0, 0, 0);
+            for (int nb = 0; nb < 4; ++nb) {
+                const int co = nb * 16 + (lane & 15);
+                B[nb] = __builtin_bit_cast(h8, Wl[(tap * 64 + co) * 8 + (chunk ^ (co & 7))]);
             }
+        };
+        h8 A0[kCvRows], B0[4], A1[kCvRows], B1[4];
+        frag(0, A0, B0);
+#pragma unroll
+        for (int step = 0; step < 18; step += 2) {
+            frag(step + 1, A1, B1);
+#pragma unroll
+            for (int m = 0; m < kCvRows; ++m)
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0[m], B0[nb], acc[m][nb], 0, 0, 0);
+            if (step + 2 < 18) frag(step + 2, A0, B0);
+#pragma unroll
+            for (int m = 0; m < kCvRows; ++m)
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+                    acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[m], B1[nb], acc[m][nb], 0, 0, 0);
         }
         __syncthreads();  // (In is reused as the output staging)
         _Float16 *st = reinterpret_cast<_Float16 *>(In);

@@ -1,4 +1,4 @@
-# 64 -> 64 matrix-core convolution: tiles in column-band order, contiguous per workgroup (libfdhip) vs the previous build (abvar/head.so)
+# 64 -> 64 matrix-core convolution A/B: the working build (libfdhip) vs the previous build (abvar/head.so)
 set -e
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out/r04p
 timeout -k 10 300 python3 -u -m pytest tests/test_gpu_nn.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r04p/nn.log 2>&1 || { tail -30 gpurun_out/r04p/nn.log; exit 1; }
