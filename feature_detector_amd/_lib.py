@@ -107,7 +107,7 @@ def load() -> ctypes.CDLL:
         "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
         "fd_nn_bias_relu": (i32, [P, P, P, i64, P, i32, i32, i32, i32, i32]),
         "fd_nn_conv3x3_c1": (i32, [P, P, P, P, i64, P, i32, i32, i32]),
-        "fd_nn_conv3x3_c64": (i32, [P, P, P, P, P, i32, i32, i32, i32]),
+        "fd_nn_conv3x3_c64": (i32, [P, P, P, P, P, i32, i32, i32, i32, i32, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
         "fd_png_info": (i32, [P, ctypes.c_size_t, P, P, P]),
         "fd_png_decode": (i32, [P, ctypes.c_size_t, P, ctypes.c_size_t, P, P]),

@@ -304,7 +304,7 @@ hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s);
 int heat_blocks_per_frame(int64_t npx);
 hipError_t launch_nn_desc(const NnDescArgs &a, hipStream_t s);
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
-                              hipStream_t s);
+                              int y_channels, int y_offset, hipStream_t s);
 hipError_t launch_conv3x3_c1_bias_relu(const void *x, const void *wt, const void *bias, void *y, int n, int h, int w,
                                        int c, hipStream_t s);
 hipError_t launch_bias_relu(const void *x, const void *bias, void *y, int n, int h, int w, int c, int pool,

@@ -165,7 +165,7 @@ __device__ __forceinline__ float cv_epilogue(float acc, float b) {
 
 template <bool POOL>
 __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 *wpk, const _Float16 *bias, u4 *y,
-                                                          int n, int h, int w) {
+                                                          int n, int h, int w, int ystride, int yoff) {
     __shared__ u4 Wl[9 * 64 * 8];
     __shared__ u4 In[kCvInRows * kCvInCols * 8];  // (also the output staging after the K loop)
     const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
             for (int i = tid; i < kCvRows / 2 * 32 * 8; i += 256) {
                 const int ch = i & 7, px = i >> 3, pc = px & 31, pr = px >> 5;
                 const int gy = r0 / 2 + pr, gx = c0 / 2 + pc;
-                if (gy < ho && gx < wo) y[((static_cast<int64_t>(f) * ho + gy) * wo + gx) * 8 + ch] = In[px * 8 + ch];
+                if (gy < ho && gx < wo) y[((static_cast<int64_t>(f) * ho + gy) * wo + gx) * ystride + yoff + ch] = In[px * 8 + ch];
             }
         } else {
             // staging [kCvRows rows][64 columns][64 channels]
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
             for (int i = tid; i < kCvRows * kCvCols * 8; i += 256) {
                 const int ch = i & 7, px = i >> 3, pc = px % kCvCols, pr = px / kCvCols;
                 const int gy = r0 + pr, gx = c0 + pc;
-                if (gy < h && gx < w) y[((static_cast<int64_t>(f) * h + gy) * w + gx) * 8 + ch] = In[px * 8 + ch];
+                if (gy < h && gx < w) y[((static_cast<int64_t>(f) * h + gy) * w + gx) * ystride + yoff + ch] = In[px * 8 + ch];
             }
         }
     }
@@ -297,16 +297,17 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
 }  // namespace
 
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
-                              hipStream_t s) {
+                              int y_channels, int y_offset, hipStream_t s) {
+    const int ystride = y_channels / 8, yoff = y_offset / 8;
     const int64_t tiles = static_cast<int64_t>(n) * ((h + kCvRows - 1) / kCvRows) * ((w + kCvCols - 1) / kCvCols);
     if (tiles == 0) return hipSuccess;
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(tiles, 1024));
     if (pool)
         hipLaunchKernelGGL(k_conv3x3_c64_mfma<true>, dim3(grid), dim3(256), 0, s, static_cast<const u4 *>(x),
-                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w);
+                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w, ystride, yoff);
     else
         hipLaunchKernelGGL(k_conv3x3_c64_mfma<false>, dim3(grid), dim3(256), 0, s, static_cast<const u4 *>(x),
-                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w);
+                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w, ystride, yoff);
     return hipGetLastError();
 }
 

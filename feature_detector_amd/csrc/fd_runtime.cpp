@@ -1905,18 +1905,20 @@ int fd_nn_conv3x3_c1(fd_ctx *c, const void *x, const void *weight, const void *b
 }
 
 int fd_nn_conv3x3_c64(fd_ctx *c, const void *x, const void *weight_packed, const void *bias, void *y, int n, int h,
-                      int w, int pool) {
+                      int w, int pool, int y_channels, int y_offset) {
     if (!c) return FD_ERR_INVALID;
     if (!x || !weight_packed || !bias || !y) return fail(c, FD_ERR_INVALID, "bad arguments");
     if (n < 0 || h < 0 || w < 0) return fail(c, FD_ERR_INVALID, "need n, h, w >= 0");
     if (pool && ((h | w) & 1)) return fail(c, FD_ERR_INVALID, "pooling needs even h and w");
+    if (y_channels < 64 || y_channels % 64 || y_offset < 0 || y_offset % 64 || y_offset + 64 > y_channels)
+        return fail(c, FD_ERR_INVALID, "y_channels must be a multiple of 64 holding [y_offset, y_offset + 64)");
     if (static_cast<int64_t>(n) * ((h + 1) / 2) * ((w + 63) / 64) >= (int64_t(1) << 31))
         return fail(c, FD_ERR_INVALID, "too many tiles");
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weight_packed) | reinterpret_cast<uintptr_t>(y)) & 15 ||
         reinterpret_cast<uintptr_t>(bias) & 1)
         return fail(c, FD_ERR_INVALID, "x, weight, y must be 16-byte aligned");
     FD_HIP_TRY(c, hipSetDevice(c->device));
-    FD_HIP_TRY(c, fdk::launch_conv3x3_c64(x, weight_packed, bias, y, n, h, w, pool, c->stream));
+    FD_HIP_TRY(c, fdk::launch_conv3x3_c64(x, weight_packed, bias, y, n, h, w, pool, y_channels, y_offset, c->stream));
     return FD_OK;
 }
 

@@ -241,35 +241,40 @@ def pack_conv3x3_weight(weight):
 
 
 def conv64_bias_relu(x, weight, bias, pool: bool = False, out=None, ctx: Context | None = None, packed=None):
-    """fd_nn_conv3x3_c64: 3x3 convolution 64 -> 64 channels (stride 1, padding 1) + bias + ReLU (+ 2x2 max
-    pool) on the matrix cores, x [N, 64, H, W] fp16 channels-last on the device -> [N, 64, H(/2), W(/2)]
-    fp16 channels-last. fp16 products summed in float, the sum rounded to half, then the bias added in
-    float and rounded (as the bias-free convolution + bias_relu path). packed: the filter already in
-    pack_conv3x3_weight's layout (reused across calls)."""
+    """fd_nn_conv3x3_c64: 3x3 convolution from 64 channels to a multiple of 64 (stride 1, padding 1) + bias +
+    ReLU (+ 2x2 max pool) on the matrix cores, one call per 64-output-channel block: x [N, 64, H, W] fp16
+    channels-last on the device -> [N, C_out, H(/2), W(/2)] fp16 channels-last. fp16 products summed in
+    float, the sum rounded to half, then the bias added in float and rounded (as the bias-free
+    convolution + bias_relu path). packed: the filter's blocks already in pack_conv3x3_weight's layout
+    (a list, one per 64 output channels; reused across calls)."""
     import torch
 
     if not (x.is_cuda and x.dtype == torch.float16 and x.dim() == 4 and x.shape[1] == 64
             and x.is_contiguous(memory_format=torch.channels_last)):
         raise ValueError("conv64_bias_relu: x must be a channels-last float16 [N, 64, H, W] device tensor")
     n, c, h, w = x.shape
-    if tuple(weight.shape) != (64, 64, 3, 3) or bias.numel() != 64:
-        raise ValueError("conv64_bias_relu: weight must be [64, 64, 3, 3] and bias 64 values")
+    co = weight.shape[0]
+    if co % 64 or tuple(weight.shape) != (co, 64, 3, 3) or bias.numel() != co:
+        raise ValueError("conv64_bias_relu: weight must be [64 k, 64, 3, 3] and bias as many values")
     if pool and (h % 2 or w % 2):
         raise ValueError("conv64_bias_relu: pooling needs even H and W")
-    shape = (n, 64, h // 2, w // 2) if pool else (n, 64, h, w)
+    shape = (n, co, h // 2, w // 2) if pool else (n, co, h, w)
     if out is None:
         out = torch.empty(shape, dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
     elif not (out.dtype == torch.float16 and tuple(out.shape) == shape
               and out.is_contiguous(memory_format=torch.channels_last)):
         raise ValueError(f"conv64_bias_relu: out must be a channels-last float16 {list(shape)} tensor")
-    wp = packed if packed is not None else pack_conv3x3_weight(weight.to(torch.float16))
+    if packed is None:
+        packed = [pack_conv3x3_weight(weight[k:k + 64].to(torch.float16)) for k in range(0, co, 64)]
     b = bias.detach().to(device=x.device, dtype=torch.float16).contiguous()
     ctx = _resolve_ctx(ctx, x)
     _bind_stream(ctx, True)
-    rc = _lib.load().fd_nn_conv3x3_c64(ctx.ptr, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wp.data_ptr()),
-                                        ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(out.data_ptr()), n, h, w,
-                                        1 if pool else 0)
-    _lib.check(ctx.ptr, rc)
+    for blk, wp in enumerate(packed):
+        bb = b[blk * 64:(blk + 1) * 64]
+        rc = _lib.load().fd_nn_conv3x3_c64(ctx.ptr, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wp.data_ptr()),
+                                            ctypes.c_void_p(bb.data_ptr()), ctypes.c_void_p(out.data_ptr()), n, h, w,
+                                            1 if pool else 0, co, blk * 64)
+        _lib.check(ctx.ptr, rc)
     return out
 
 
@@ -386,16 +391,18 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
                     and not os.environ.get("FD_SP_NO_CONV1"):  # (A/B switches)
                 # first layer: write-bound (9 MACs per output), one pass instead of convolution + bias pass
                 return conv1_bias_relu(x.contiguous(), conv.weight, conv.bias)
-            if x.dtype == torch.float16 and x.is_cuda and conv.in_channels == 64 and conv.out_channels == 64 \
+            if x.dtype == torch.float16 and x.is_cuda and conv.in_channels == 64 and conv.out_channels % 64 == 0 \
                     and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1) \
                     and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) \
                     and (not pool or (x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)) \
-                    and not os.environ.get("FD_SP_UNFUSED") and not os.environ.get("FD_SP_NO_C64"):  # (A/B switches)
-                # 64 -> 64 layers on the matrix cores with bias, ReLU and pooling in the epilogue
+                    and not os.environ.get("FD_SP_UNFUSED") and not os.environ.get("FD_SP_NO_C64") \
+                    and (conv.out_channels == 64 or not os.environ.get("FD_SP_C64_ONLY64")):  # (A/B switches)
+                # 64 -> 64 k layers on the matrix cores with bias, ReLU and pooling in the epilogue
                 key = f"_fd_packed_{conv.weight.data_ptr()}_{conv.weight._version}"  # (in-place updates repack)
                 wp = getattr(self, key, None)
                 if wp is None:
-                    wp = pack_conv3x3_weight(conv.weight.to(torch.float16))
+                    wp = [pack_conv3x3_weight(conv.weight[k:k + 64].to(torch.float16))
+                          for k in range(0, conv.out_channels, 64)]
                     setattr(self, key, wp)
                 return conv64_bias_relu(x, conv.weight, conv.bias, pool, packed=wp)
             if x.dtype == torch.float16 and x.is_cuda and x.is_contiguous(memory_format=torch.channels_last) \

@@ -379,13 +379,15 @@ int fd_nn_conv3x3_c1(fd_ctx *ctx, const void *x, const void *weight, const void 
 /*
  * fd_nn_conv3x3_c64 -- a 3x3 convolution from 64 to 64 channels (stride 1, zero padding 1; SuperPoint
  * conv1b / conv2a / conv2b) with its bias and ReLU and, with pool = 1, the 2x2 / stride-2 max pool, on the
- * matrix cores: x [n][h][w][64] channels-last fp16 -> y [n][h][w][64] (or [n][h/2][w/2][64]) fp16, with
- * weight_packed [9 taps (ky, kx)][64 out][64 in] fp16 and bias [64] fp16, all on the device. fp16 products
- * summed in float; the sum rounded to half, the bias added in float and rounded (as a bias-free
- * convolution followed by fd_nn_bias_relu). x, weight_packed, y 16-byte aligned; pool needs even h, w.
+ * matrix cores: x [n][h][w][64] channels-last fp16 -> channels [y_offset, y_offset + 64) of y
+ * [n][h][w][y_channels] (or [n][h/2][w/2][y_channels]) fp16, with weight_packed [9 taps (ky, kx)][64 out][64 in]
+ * fp16 and bias [64] fp16 (that block of output channels), all on the device; wider outputs (64 -> 128,
+ * SuperPoint conv3a) are one call per 64-channel block. fp16 products summed in float; the sum rounded to
+ * half, the bias added in float and rounded (as a bias-free convolution followed by fd_nn_bias_relu).
+ * x, weight_packed, y 16-byte aligned; y_channels a multiple of 64; pool needs even h, w.
  */
 int fd_nn_conv3x3_c64(fd_ctx *ctx, const void *x, const void *weight_packed, const void *bias, void *y, int n, int h,
-                      int w, int pool);
+                      int w, int pool, int y_channels, int y_offset);
 
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);

@@ -295,7 +295,7 @@ def test_conv1_bias_relu_matches_torch(sp):
 
 @pytest.mark.gpu
 def test_conv64_bias_relu_matches_torch(sp):
-    """fd_nn_conv3x3_c64 (64 -> 64 channels, 3x3, padding 1, + bias + ReLU, with and without the 2x2 max pool,
+    """fd_nn_conv3x3_c64 (64 -> 64 / 128 channels, 3x3, padding 1, + bias + ReLU, with and without the 2x2 max pool,
     on the matrix cores) against PyTorch's float32 convolution of the same fp16 tensors, within one fp16
     rounding of the convolution and one of the biased sum; ragged tiles (sizes not multiples of the 4 x 64
     tile), a 640x480 frame, and argument checks."""
@@ -303,10 +303,10 @@ def test_conv64_bias_relu_matches_torch(sp):
 
     g = torch.Generator(device="cuda")
     g.manual_seed(9)
-    for n, h, w in ((2, 8, 64), (1, 6, 130), (3, 10, 18), (1, 480, 640)):
+    for n, h, w, co in ((2, 8, 64, 64), (1, 6, 130, 128), (3, 10, 18, 64), (1, 480, 640, 64), (2, 120, 160, 128)):
         x = torch.rand((n, 64, h, w), generator=g, device="cuda").half().contiguous(memory_format=torch.channels_last)
-        wt = (torch.randn((64, 64, 3, 3), generator=g, device="cuda") * 0.06).half()
-        b = (torch.randn(64, generator=g, device="cuda") * 0.2).half()
+        wt = (torch.randn((co, 64, 3, 3), generator=g, device="cuda") * 0.06).half()
+        b = (torch.randn(co, generator=g, device="cuda") * 0.2).half()
         conv = torch.nn.functional.conv2d(x.float(), wt.float(), None, 1, 1)
         ref = torch.relu(conv + b.float().view(1, -1, 1, 1))
         tol = (conv.abs() + ref.abs()) * 2.0 ** -10 + 2.0 ** -14
@@ -317,7 +317,7 @@ def test_conv64_bias_relu_matches_torch(sp):
         gp = sp.conv64_bias_relu(x, wt, b, pool=True)
         refp = torch.nn.functional.max_pool2d(ref, 2, 2)
         tolp = torch.nn.functional.max_pool2d(tol, 2, 2)
-        assert tuple(gp.shape) == (n, 64, h // 2, w // 2)
+        assert tuple(gp.shape) == (n, co, h // 2, w // 2)
         assert bool(((gp.float() - refp).abs() <= tolp).all()), (n, h, w, (gp.float() - refp).abs().max().item())
     x = torch.zeros((1, 64, 5, 8), device="cuda", dtype=torch.float16).contiguous(memory_format=torch.channels_last)
     wt = torch.zeros((64, 64, 3, 3), device="cuda", dtype=torch.float16)

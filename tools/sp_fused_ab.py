@@ -1,6 +1,7 @@
 """A/B of the SuperPoint forward (BASELINE configs[4] shape: 64 x 640x480 fp16, channels last): the fused
 bias + ReLU (+ pool) kernel (fd_nn_bias_relu) and the one-pass first layer (fd_nn_conv3x3_c1) against
-the fused path without the 64 -> 64 matrix-core convolutions (FD_SP_NO_C64=1), without both
+the fused path with the matrix-core convolution for 64 -> 64 layers only (FD_SP_C64_ONLY64=1: conv3a,
+64 -> 128, on the library), without the matrix-core convolutions (FD_SP_NO_C64=1), without both
 (FD_SP_NO_CONV1=1 FD_SP_NO_C64=1: round-3's path) and PyTorch's separate elementwise passes
 (FD_SP_UNFUSED=1), interleaved in one process; prints ms per 64-frame forward."""
 import os
@@ -34,9 +35,11 @@ def timed(reps=10):
 
 
 for rnd in range(2):
-    for mode in ("fused", "no_c64", "no_conv1", "unfused"):
-        for k in ("FD_SP_UNFUSED", "FD_SP_NO_CONV1", "FD_SP_NO_C64"):
+    for mode in ("fused", "c64_only64", "no_c64", "no_conv1", "unfused"):
+        for k in ("FD_SP_UNFUSED", "FD_SP_NO_CONV1", "FD_SP_NO_C64", "FD_SP_C64_ONLY64"):
             os.environ.pop(k, None)
+        if mode == "c64_only64":
+            os.environ["FD_SP_C64_ONLY64"] = "1"
         if mode == "unfused":
             os.environ["FD_SP_UNFUSED"] = "1"
         elif mode == "no_conv1":
