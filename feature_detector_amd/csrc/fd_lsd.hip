@@ -104,16 +104,6 @@ __device__ __forceinline__ float fd_atan2f(float y, float x) {
     }
 }
 
-__device__ __forceinline__ void lsd_tile(const LsdArgs &a, int &f, int &strip, int &chunk) {
-    // wave-uniform (readfirstlane): row/column bounds derived from it stay in SGPRs, and the
-    // per-row bound checks are scalar branches (no exec masking around the DPP moves)
-    int w = __builtin_amdgcn_readfirstlane(static_cast<int>(blockIdx.x * 4 + (threadIdx.x >> 6)));
-    strip = w % a.strips;
-    w /= a.strips;
-    chunk = w % a.chunks;
-    f = w / a.chunks;
-}
-
 // Pass 1: maps + per (column, row-chunk) valid counts and valid-row bitmasks. A wave owns a strip of
 // 256 map columns (4 per lane, read as one dword per lane and row; the fifth column comes from the
 // right neighbour lane by DPP, lane 63 loads it) and walks chunk_h rows. Every map entry is written
@@ -427,44 +417,86 @@ __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
 
 // Pass 3: scatter valid map indices in scan order, from the per-(column, chunk) row bitmasks of
 // pass 1 (a few words per lane instead of re-reading the valid map row by row).
+// Pass 3: the column-major valid list. The list holds each column's valid rows in order, chunk after
+// chunk, so one column's entries (all chunks) are one contiguous run starting at its chunk-0 base. A wave
+// owns 64 columns and writes them one column at a time: its lanes take the column's (chunk, row word)
+// items in row order, a wave prefix of their popcounts places every lane's entries inside the run, so
+// each store instruction covers a few adjacent cache lines (a lane per column, as before, made every
+// store touch 64 lines; the row-bit words of adjacent columns share lines, so the per-column loads hit
+// L1 after the first column of a line).
 __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
-    int f, strip, chunk;
-    lsd_tile(a, f, strip, chunk);
+    const int w4 = static_cast<int>(blockIdx.x) * 4 + (static_cast<int>(threadIdx.x) >> 6);
+    const int strip = __builtin_amdgcn_readfirstlane(w4 % a.strips), f = __builtin_amdgcn_readfirstlane(w4 / a.strips);
     if (f >= a.batch) return;
     const int lane = lane_id();
-    const int rows = a.rows, cols = a.cols, mc = cols - 1;
-    const int col = strip * kWave + lane;
-    if (!(col >= 1 && col <= cols - 3)) return;
-    const int r0 = 1 + chunk * a.chunk_h;
-    const int r1 = min(r0 + a.chunk_h, rows - 2);
-    const int64_t fc = static_cast<int64_t>(f) * a.chunks + chunk;
-    int64_t pos = a.col_base[fc * mc + col];
-    const uint32_t *bits = a.rowbits + fc * a.words * mc + col;  // word w at bits[w * mc]
-    const int nw = (r1 - r0 + 31) >> 5;
-    if (a.frame_base) {
-        // Compact mode: all frames' lists back to back (frame_base); norm and angle follow in
-        // k_lsd_values, one thread per entry (here a column with many valid rows would keep its whole
-        // wave in the atan2f loop).
-        int32_t *out = a.idx + a.frame_base[f];
-        for (int w = 0; w < nw; ++w) {
-            uint32_t m = bits[static_cast<int64_t>(w) * mc];
-            while (m) {
-                const int rr = r0 + 32 * w + __builtin_ctz(m);
-                m &= m - 1u;
-                out[pos++] = static_cast<int32_t>(static_cast<int64_t>(rr) * mc + col);
+    const int rows = a.rows, cols = a.cols, mc = cols - 1, words = a.words, chunks = a.chunks;
+    const int items = chunks * words;
+    const int64_t n = static_cast<int64_t>(mc) * chunks;
+    const int32_t *cbase = a.col_base + static_cast<int64_t>(f) * n;  // [chunk][column] of this frame
+    const uint32_t *fbits = a.rowbits + static_cast<int64_t>(f) * chunks * words * mc;
+    int32_t *out = a.frame_base ? a.idx + a.frame_base[f] : a.idx + static_cast<int64_t>(f) * a.idx_cap;
+    const int64_t cap = a.frame_base ? INT64_MAX : a.idx_cap;
+    // the 64 columns' run starts (lane = column), read once
+    const int coll = strip * kWave + lane;
+    const int64_t basel = coll >= 1 && coll <= cols - 3 ? cbase[coll] : 0;
+    auto put = [&](int col, int i, uint32_t m, int64_t &run) {
+        const int c = i / words, w = i - c * words;
+        const int r0 = 1 + c * a.chunk_h;
+        const uint32_t cnt = static_cast<uint32_t>(__popc(m));
+        const uint32_t incl = wave_incl_add(cnt);
+        int64_t pos = run + (incl - cnt);
+        while (m) {
+            const int rr = r0 + 32 * w + __builtin_ctz(m);
+            m &= m - 1u;
+            if (pos < cap) out[pos] = static_cast<int32_t>(static_cast<int64_t>(rr) * mc + col);
+            ++pos;
+        }
+        run += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), kWave - 1));
+    };
+    auto word = [&](int col, int i) -> uint32_t {
+        const int c = i / words, w = i - c * words;
+        const int r0 = 1 + c * a.chunk_h;
+        if (col < 1 || col > cols - 3 || i >= items || r0 + 32 * w >= min(r0 + a.chunk_h, rows - 2)) return 0u;
+        return fbits[(static_cast<int64_t>(c) * words + w) * mc + col];
+    };
+    if (items <= kWave) {
+        // the wave's row-bit words, [item][column], read row by row (lane = column: 256 contiguous bytes per
+        // load) into LDS, 16 loads in flight; then one item per lane and column from LDS
+        __shared__ uint32_t sb[4][kWave][kWave + 1];
+        uint32_t(*const wb)[kWave + 1] = sb[threadIdx.x >> 6];
+        for (int i0 = 0; i0 < items; i0 += 16) {
+            uint32_t v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = word(coll, i0 + k);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (i0 + k < kWave) wb[i0 + k][lane] = v[k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr int kG = 8;
+        for (int g = 0; g < kWave; g += kG) {
+            uint32_t mv[kG];
+#pragma unroll
+            for (int k = 0; k < kG; ++k) mv[k] = lane < items ? wb[lane][g + k] : 0u;
+#pragma unroll
+            for (int k = 0; k < kG; ++k) {
+                const int col = strip * kWave + g + k;
+                if (col < 1 || col > cols - 3) continue;  // (wave-uniform)
+                const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(basel), g + k));
+                const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(basel >> 32), g + k));
+                int64_t run = static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+                put(col, lane, mv[k], run);
             }
         }
         return;
     }
-    int32_t *out = a.idx + static_cast<int64_t>(f) * a.idx_cap;
-    for (int w = 0; w < nw; ++w) {
-        uint32_t m = bits[static_cast<int64_t>(w) * mc];
-        while (m) {
-            const int rr = r0 + 32 * w + __builtin_ctz(m);
-            m &= m - 1u;
-            if (pos < a.idx_cap) out[pos] = static_cast<int32_t>(static_cast<int64_t>(rr) * mc + col);
-            ++pos;
-        }
+    for (int cc = 0; cc < kWave; ++cc) {
+        const int col = strip * kWave + cc;
+        if (col < 1 || col > cols - 3) continue;  // (wave-uniform)
+        int64_t run = cbase[col];
+        for (int i0 = 0; i0 < items; i0 += kWave) put(col, i0 + lane, word(col, i0 + lane), run);
     }
 }
 
@@ -519,7 +551,7 @@ hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_lsd_scatter(const LsdArgs &a, hipStream_t s) {
-    const int64_t waves = static_cast<int64_t>(a.batch) * a.chunks * a.strips;
+    const int64_t waves = static_cast<int64_t>(a.batch) * a.strips;
     hipLaunchKernelGGL(k_lsd_scatter, dim3(static_cast<unsigned>((waves + 3) / 4)), dim3(256), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || !a.frame_base || a.idx_cap <= 0) return e;
@@ -540,7 +572,8 @@ hipError_t launch_lsd(const LsdArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_lsd_scan, dim3(a.batch), dim3(1024), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lsd_scatter, grid, block, 0, s, a);
+    hipLaunchKernelGGL(k_lsd_scatter, dim3(static_cast<unsigned>((static_cast<int64_t>(a.batch) * a.strips + 3) / 4)),
+                       block, 0, s, a);
     return hipGetLastError();
 }
 
