@@ -121,6 +121,7 @@ struct SelectArgs {
     int first_sub;     // sorted-segment corner frames: first chunk cut at one sub-chunk (kSubChunk keys)
     int grid_at_d0;    // distance 0 still tests the grid (1-pixel cells): caller lists may name a pixel twice
     int dup_keys;      // equal selection keys possible (caller lists): the orderings rank them stably
+    int par_greedy;    // workgroup-parallel greedy (greedy_block: sparse NMS candidates) instead of the wave scan
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
 };
 

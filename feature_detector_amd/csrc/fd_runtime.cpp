@@ -76,7 +76,19 @@ struct fd_ctx {
     fdk::FastOffsets off{};
 };
 
+#ifndef FD_PAR_GREEDY
+#define FD_PAR_GREEDY 0  // 1: corner detectors take the workgroup-parallel greedy (greedy_block; A/B build)
+#endif
+
 namespace {
+
+// A/B and diagnostic switches (FD_PX, FD_TILE_H, FD_SELECT_STAMPS, ...) take effect only when FD_DEBUG_AB is
+// set as well, so a stray variable in a user's environment cannot change the library's code path.
+const char *ab_env(const char *name) {
+    const char *on = std::getenv("FD_DEBUG_AB");
+    if (!on || !*on || std::strcmp(on, "0") == 0) return nullptr;
+    return std::getenv(name);
+}
 
 int fail(fd_ctx *c, int code, const std::string &msg) {
     if (c) c->err = msg;
@@ -149,8 +161,8 @@ T *as(DevBuf &b) {
 // enough waves to fill 256 CUs, capped so halo rows stay a small overhead.
 int choose_tile_h(int64_t batch, int tiles_x, int out_rows, int period, int max_mult) {
     int64_t target_waves = 10240;  // ~2 rounds of resident waves at 256 CUs (measured sweep)
-    if (const char *e = std::getenv("FD_TARGET_WAVES")) target_waves = std::max<int64_t>(1, std::atoll(e));  // tuning
-    if (const char *e = std::getenv("FD_TILE_MULT")) max_mult = std::max(1, std::atoi(e));                   // tuning
+    if (const char *e = ab_env("FD_TARGET_WAVES")) target_waves = std::max<int64_t>(1, std::atoll(e));  // tuning
+    if (const char *e = ab_env("FD_TILE_MULT")) max_mult = std::max(1, std::atoi(e));                   // tuning
     int64_t h = (batch * tiles_x * static_cast<int64_t>(out_rows)) / target_waves;
     if (h < period && period == 6) {
         // small launches: the tile's serial row chain is the latency; 3 rows (9 steps of the 6-row
@@ -162,7 +174,7 @@ int choose_tile_h(int64_t batch, int tiles_x, int out_rows, int period, int max_
         h = ((h + period - 1) / period) * period;
     }
     h = std::min<int64_t>(h, static_cast<int64_t>(period) * max_mult);
-    if (const char *e = std::getenv("FD_TILE_H")) h = std::max(1, std::atoi(e));  // tuning (A/B)
+    if (const char *e = ab_env("FD_TILE_H")) h = std::max(1, std::atoi(e));  // tuning (A/B)
     return static_cast<int>(h);
 }
 
@@ -325,7 +337,7 @@ int corner_px(int kind, int batch, int rows, int cols, float thr) {
     if (kind == FD_FAST || !(thr >= 0.0f)) return 0;
     // k_corner_lp addresses a frame's list through a buffer resource: list_cap * 4 bytes < 2^32
     if (static_cast<int64_t>(rows) * cols >= (int64_t(1) << 30)) return 0;
-    if (const char *e = std::getenv("FD_PX")) {
+    if (const char *e = ab_env("FD_PX")) {
         const int v = std::atoi(e);
         if (v == 0 || v == 2 || v == 4 || v == 8) return v;
     }
@@ -422,6 +434,7 @@ struct SelectCall {
     const uint64_t *seghead = nullptr;
     int nseg = 0;
     bool push_order = false;  // lists hold the caller's push order (fd_points_select), not raster order
+    bool par_greedy = false;  // sparse candidates (strict 4-neighbour NMS): the workgroup-parallel greedy
     bool dup_keys = false;    // a pixel may be listed twice with one response (caller lists): equal keys
     bool grid_at_d0 = false;  // distance 0 tests the grid too (1-pixel cells; set with push_order)
     const char *value_msg = "a value above the declared maximum (fd_nn_opts::max_response)";
@@ -431,7 +444,7 @@ struct SelectCall {
 // workgroup segment of a frame its own threads (<= kSelectThreads segments per frame) and that would
 // otherwise gather their first chunk inside k_select (no k_gather kernel). FD_SEG_LISTS=0: off (A/B).
 bool use_seg_lists(int blocks_per_frame, int rows, int cols) {
-    if (const char *e = std::getenv("FD_SEG_LISTS"); e && std::atoi(e) == 0) return false;
+    if (const char *e = ab_env("FD_SEG_LISTS"); e && std::atoi(e) == 0) return false;
     return blocks_per_frame <= 1024 && static_cast<int64_t>(rows) * cols < (1 << 20);
 }
 
@@ -559,7 +572,7 @@ int resolve_ties(fd_ctx *c, fdk::SelectArgs s, int batch, const SelectBufs &sb, 
 }
 
 bool host_ties_env() {  // FD_TIES_HOST=1: the round-3 host path for every flagged frame (A/B and checker)
-    static const bool v = std::getenv("FD_TIES_HOST") && std::atoi(std::getenv("FD_TIES_HOST")) != 0;
+    static const bool v = ab_env("FD_TIES_HOST") && std::atoi(ab_env("FD_TIES_HOST")) != 0;
     return v;
 }
 
@@ -601,6 +614,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.dist = q.dist;
     s.grid_at_d0 = (q.push_order || q.grid_at_d0) ? 1 : 0;  // caller lists may name a pixel twice: distance 0 tests it
     s.dup_keys = q.dup_keys ? 1 : 0;
+    s.par_greedy = q.par_greedy ? 1 : 0;
     if (s.dist >= 1 || (s.dist == 0 && s.grid_at_d0)) {
         s.grid_w = (cols + s.dist) / (s.dist + 1);
         s.grid_h = (rows + s.dist) / (s.dist + 1);
@@ -630,12 +644,12 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     // from about a megapixel per frame; measured at 640x480: break-even).
     const bool big = static_cast<int64_t>(rows) * cols >= (1 << 20);
     s.gather_groups = big ? std::max(1, std::min(64, 256 / std::max(batch, 1))) : 1;
-    if (const char *e = std::getenv("FD_GATHER_GROUPS")) s.gather_groups = std::max(1, std::atoi(e));  // A/B
+    if (const char *e = ab_env("FD_GATHER_GROUPS")) s.gather_groups = std::max(1, std::atoi(e));  // A/B
     if (q.value_flag) s.gather_groups = 1;  // pre_count carries the candidate kernel's flag instead
     s.pre_count = sb.pre_count;
     s.pre_keys = s.gather_groups > 1 ? sb.pre_keys : nullptr;
     s.seg_bad = sb.seg_bad;
-    s.wide_keys = std::getenv("FD_NO_WIDE") ? nullptr : sb.wide_keys;  // (A/B switch)
+    s.wide_keys = ab_env("FD_NO_WIDE") ? nullptr : sb.wide_keys;  // (A/B switch)
     // FAST's top responses are scores plus a slowly growing offset: thousands of candidates share the
     // top bins and the greedy scan runs over several chunks (1280x720 noise: ~5k), so the wide pass
     // comes with the first chunk; the corner detectors usually finish within it (wide pass deferred).
@@ -646,8 +660,8 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         s.nseg = q.nseg;
     }
     s.first_sub = 1;
-    if (const char *e = std::getenv("FD_FIRST_SUB")) s.first_sub = std::atoi(e) != 0;  // (A/B switch)
-    static const bool stamps = std::getenv("FD_SELECT_STAMPS") != nullptr;
+    if (const char *e = ab_env("FD_FIRST_SUB")) s.first_sub = std::atoi(e) != 0;  // (A/B switch)
+    static const bool stamps = ab_env("FD_SELECT_STAMPS") != nullptr;
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
         FD_HIP_TRY(c, ensure(c, c->dbg, sizeof(uint64_t) * 32 * batch));
         FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 32 * batch, c->stream));
@@ -699,7 +713,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
             const int rc = ref_buffers(c, batch, rows, cols, q.cap, r);
             if (rc) return rc;
             r.push_order = q.push_order ? 1 : 0;
-            static const bool ref_debug = std::getenv("FD_REF_DEBUG") != nullptr;  // diagnostic: broken invariants
+            static const bool ref_debug = ab_env("FD_REF_DEBUG") != nullptr;  // diagnostic: broken invariants
             if (ref_debug) {
                 FD_HIP_TRY(c, ensure(c, c->dbg, sizeof(uint32_t) * 8 * batch));
                 FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint32_t) * 8 * batch, c->stream));
@@ -707,7 +721,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
             }
             // frames of >= 1 Mpx: the multi-workgroup prelude (push order, first levels); FD_REF_WIDE=0/1
             // forces it off / on (A/B)
-            const char *wide_env = std::getenv("FD_REF_WIDE");
+            const char *wide_env = ab_env("FD_REF_WIDE");
             const bool wide = wide_env ? std::atoi(wide_env) != 0
                                        : static_cast<int64_t>(rows) * cols >= (int64_t{1} << 20);
             FD_HIP_TRY(c, fdk::launch_select_reference(s, r, batch, wide, c->stream));
@@ -783,7 +797,7 @@ void lsd_geometry(fdk::LsdArgs &a, int batch, int rows, int cols, const uint8_t 
     a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
     a.pitch = cols - 1;  // dense maps: unpitched unless the caller gives a pitch (fd_lsd_map_pitched)
     int64_t target = 32768;  // waves of the map kernel (with nt map stores: map + scan + scatter 1.56-1.57 -> 1.54 ms vs 16384)
-    if (const char *e = std::getenv("FD_LSD_WAVES")) target = std::max<int64_t>(64, std::atoll(e));  // A/B
+    if (const char *e = ab_env("FD_LSD_WAVES")) target = std::max<int64_t>(64, std::atoll(e));  // A/B
     int64_t ch = (static_cast<int64_t>(batch) * a.strips4 * work_rows) / target;
     ch = std::max<int64_t>(16, std::min<int64_t>(ch, 256));
     a.chunk_h = static_cast<int>(ch);
@@ -808,6 +822,8 @@ const char *fd_build_info(void) {
     return "libfdhip gfx950 (MI355X); kernels: corner response+NMS, FAST-12, greedy select, LSD map; "
            "flags: -O3 -ffp-contract=off";
 }
+
+int fd_abi_version(void) { return FD_ABI_VERSION; }
 
 int fd_ctx_create(int device, fd_ctx **out) {
     if (!out) return FD_ERR_INVALID;
@@ -840,7 +856,7 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
                       &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
                       &c->l_lnorm,  &c->l_langle, &c->l_fbase, &c->wide_keys, &c->r_x, &c->r_lpos,
-                      &c->r_rpos,   &c->r_ord};
+                      &c->r_rpos,   &c->r_ord,    &c->r_ctl,       &c->r_wcnt,      &c->r_wfr};
     for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle, &c->h_png}) release(*b);
     release(c->d_png);
     for (DevBuf *b : bufs) release(*b);
@@ -1050,6 +1066,7 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     sc.seghead = a.seghead;
     sc.nseg = g.blocks_per_frame;
     sc.wide_eager = kind == FD_FAST;
+    sc.par_greedy = FD_PAR_GREEDY && kind != FD_FAST;  // (FAST candidates cluster: no NMS)
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
 }
 
@@ -1443,7 +1460,7 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     c->st_used.clear();
     for (int b = 0; b < batch; ++b) out_counts[b] = 0;
     if (needed == 0) return FD_OK;  // :15
-    static const bool timing = std::getenv("FD_LINES_TIMING") != nullptr;  // diagnostic: phase times to stderr
+    static const bool timing = ab_env("FD_LINES_TIMING") != nullptr;  // diagnostic: phase times to stderr
     const auto t_start = std::chrono::steady_clock::now();
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const uint8_t *dframes = nullptr;

@@ -104,8 +104,8 @@ struct alignas(16) SelectLds {
     uint32_t pxy[kSelectChunk];
     uint32_t pcell[kSelectChunk];
     uint32_t pk32[kSelectChunk];  // 32-bit response keys in scan order (tie check)
-    uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor
-    uint32_t prev_min;                         // smallest 32-bit key of the previous sub-chunk (prefilter)
+    uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor (wave scan)
+    uint32_t prev_min;                        // smallest 32-bit key of the previous sub-chunk (prefilter)
     int have_prev_min;
     uint32_t grid_lds[kGridLdsCells];
     uint32_t tie_prev;
@@ -156,6 +156,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     };
     const int d = a.dist;
     const bool use_grid = d >= 1 || (d == 0 && a.grid_at_d0);
+    const bool par = use_grid && a.par_greedy;  // workgroup-parallel greedy (greedy_block)
     // Occupancy grid of (d+1)-sized cells with a one-cell border (no bounds checks in the scan).
     const int gw2 = a.grid_w + 2;
     const int cells = gw2 * (a.grid_h + 2);
@@ -1057,7 +1058,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     FD_STAMP(13);  // place
                     }
                     }
-                    if (!a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
+                    if (!par && !a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
                         const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;
                         for (int i = opaque(tid); i < c64; i += nthr) {
                             const bool t = i > 0 && i < c && L.pk32[i] == L.pk32[i - 1];
@@ -1065,14 +1066,24 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                             if (lane == 0) L.tmask[i >> 6] = m;
                         }
                     }
-                    // conflict masks: earlier candidates of the same 64-batch within distance d
-                    if (use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
+                    // wave scan: conflict masks (earlier candidates of the same 64-batch within distance d)
+                    if (!par && use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
                 }
                 __syncthreads();
                 FD_STAMP(14);  // conflict masks
-                // greedy scan in order by wave 0 (SelectGoodFeatures :62-72); ties checked unless the
-                // order of equal responses is defined (SuperPoint's multimap)
-                if (tid < kWave) {
+                // greedy scan in order (SelectGoodFeatures :62-72); ties checked unless the order of equal
+                // responses is defined (SuperPoint's multimap)
+                if (par) {  // by the workgroup (buf, tmp: free once the chunk is placed)
+                    const uint32_t *tk = a.tie_idx_desc ? nullptr : L.pk32;
+                    GreedyLds &G = *reinterpret_cast<GreedyLds *>(buf);
+                    uint16_t *gp = reinterpret_cast<uint16_t *>(tmp);
+                    if (grid_in_lds)
+                        greedy_block<1>(a, f, c_sort, pxy, pcell, grid_lds, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                                        L.tie_has_prev, G, gp, a.stamps ? L.st : nullptr);
+                    else
+                        greedy_block<2>(a, f, c_sort, pxy, pcell, grid_g, gw2, prior, s_acc, s_done, tk, L.tie_prev,
+                                        L.tie_has_prev, G, gp, a.stamps ? L.st : nullptr);
+                } else if (tid < kWave) {  // by wave 0
                     const bool ties = !a.tie_idx_desc;
                     const uint64_t *tm = L.tmask;
                     if (!use_grid)
@@ -1153,7 +1164,8 @@ __global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
 struct alignas(16) OrderedLds {
     uint32_t pxy[kSelectChunk];
     uint32_t pcell[kSelectChunk];
-    uint64_t cmask[kSelectChunk];
+    uint64_t cmask[kSelectChunk];  // wave scan: conflict masks; greedy_block: GreedyLds
+    uint16_t gpred[kGreedyPredBytes / 2];
     uint32_t grid_lds[kGridLdsCells];
     int s_done, s_acc;
     uint32_t tie_prev;
@@ -1204,18 +1216,28 @@ __global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs
             if (use_grid) L.pcell[i] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
         }
         __syncthreads();
-        if (use_grid) conflict_masks(L.pxy, c, d, rows, cols, L.cmask, tid, NT);
-        __syncthreads();
-        if (tid < kWave) {
-            if (!use_grid)
-                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
-                                L.tie_prev, L.tie_has_prev);
-            else if (grid_in_lds)
-                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
-                                L.tie_prev, L.tie_has_prev);
+        if (use_grid && a.par_greedy) {
+            GreedyLds &G = *reinterpret_cast<GreedyLds *>(L.cmask);
+            if (grid_in_lds)
+                greedy_block<1>(a, f, c, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
+                                L.tie_has_prev, G, L.gpred);
             else
-                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
-                                L.tie_prev, L.tie_has_prev);
+                greedy_block<2>(a, f, c, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
+                                L.tie_has_prev, G, L.gpred);
+        } else {
+            if (use_grid) conflict_masks(L.pxy, c, d, rows, cols, L.cmask, tid, NT);
+            __syncthreads();
+            if (tid < kWave) {
+                if (!use_grid)
+                    greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u,
+                                    0u, L.tie_prev, L.tie_has_prev);
+                else if (grid_in_lds)
+                    greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u,
+                                    0u, L.tie_prev, L.tie_has_prev);
+                else
+                    greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u,
+                                    0u, L.tie_prev, L.tie_has_prev);
+            }
         }
         __syncthreads();
     }

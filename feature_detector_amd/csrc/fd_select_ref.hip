@@ -87,6 +87,7 @@ struct alignas(16) RefLds {
     uint32_t wstk[kRefWaves][kRefStack];
     uint32_t wsum[kRefWaves];
     uint16_t rid[kRefRidCap];  // levels with T <= kRefRidCap: each element's active range (set by pass 1)
+    uint16_t gpred[kGreedyPredBytes / 2];  // greedy_block's neighbour lists
     int cur, m_all, m_act, n_leaf, fail, n_wl;
     uint32_t T, fin;
     int s_done, s_acc;
@@ -1046,18 +1047,28 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 if (use_grid) L.pcell[i] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
             }
             __syncthreads();
-            if (use_grid) conflict_masks(L.pxy, cn, d, rows, cols, L.cmask, tid, NT);
-            __syncthreads();
-            if (tid < kWave) {
-                if (!use_grid)
-                    greedy_chunk<0>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
-                                    0u, 0u, L.tie_prev, L.tie_has_prev);
-                else if (grid_in_lds)
-                    greedy_chunk<1>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
-                                    0u, 0u, L.tie_prev, L.tie_has_prev);
+            if (use_grid && a.par_greedy) {  // the workgroup-parallel greedy (sparse NMS candidates)
+                GreedyLds &G = *reinterpret_cast<GreedyLds *>(L.cmask);
+                if (grid_in_lds)
+                    greedy_block<1>(a, f, cn, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
+                                    L.tie_has_prev, G, L.gpred);
                 else
-                    greedy_chunk<2>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
-                                    0u, 0u, L.tie_prev, L.tie_has_prev);
+                    greedy_block<2>(a, f, cn, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
+                                    L.tie_has_prev, G, L.gpred);
+            } else {
+                if (use_grid) conflict_masks(L.pxy, cn, d, rows, cols, L.cmask, tid, NT);
+                __syncthreads();
+                if (tid < kWave) {
+                    if (!use_grid)
+                        greedy_chunk<0>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
+                                        0u, 0u, L.tie_prev, L.tie_has_prev);
+                    else if (grid_in_lds)
+                        greedy_chunk<1>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
+                                        0u, 0u, L.tie_prev, L.tie_has_prev);
+                    else
+                        greedy_chunk<2>(a, f, cn, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr,
+                                        0u, 0u, L.tie_prev, L.tie_has_prev);
+                }
             }
             __syncthreads();
         }

@@ -174,6 +174,14 @@ def nn_select_list(keypoints, scores, rows: int, cols: int, counts=None, options
     return xy, cnt, dout
 
 
+def _ab_env(name: str, default=None):
+    """A/B switch of the network's layer paths (FD_SP_*): read only with FD_DEBUG_AB set, so a stray
+    variable in a user's environment does not change the code path."""
+    if os.environ.get("FD_DEBUG_AB", "0") in ("", "0"):
+        return default
+    return os.environ.get(name, default)
+
+
 def bias_relu(x, bias, pool: bool = False, out=None, ctx: Context | None = None):
     """fd_nn_bias_relu: relu(x + bias) (and the 2x2 max pool when pool) of a channels-last fp16
     activation [N, C, H, W] on the device, in one pass (torch's current stream). x is the output of a
@@ -227,7 +235,7 @@ def conv1_bias_relu(x, weight, bias, out=None, ctx: Context | None = None):
         raise ValueError(f"conv1_bias_relu: out must be a channels-last float16 {[n, c, h, w]} tensor")
     ctx = _resolve_ctx(ctx, x)
     _bind_stream(ctx, True)
-    wt = weight.detach().contiguous()
+    wt = weight.detach().to(device=x.device, dtype=torch.float16).contiguous()  # (the kernel reads it on x's device)
     b = bias.detach().to(device=x.device, dtype=torch.float16).contiguous()
     rc = _lib.load().fd_nn_conv3x3_c1(ctx.ptr, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wt.data_ptr()),
                                        ctypes.c_void_p(b.data_ptr()), c, ctypes.c_void_p(out.data_ptr()), n, h, w)
@@ -265,7 +273,10 @@ def conv64_bias_relu(x, weight, bias, pool: bool = False, out=None, ctx: Context
               and out.is_contiguous(memory_format=torch.channels_last)):
         raise ValueError(f"conv64_bias_relu: out must be a channels-last float16 {list(shape)} tensor")
     if packed is None:
-        packed = [pack_conv3x3_weight(weight[k:k + 64].to(torch.float16)) for k in range(0, co, 64)]
+        packed = [pack_conv3x3_weight(weight[k:k + 64].to(device=x.device, dtype=torch.float16)) for k in range(0, co, 64)]
+    elif any(wp.device != x.device or wp.dtype != torch.float16 or tuple(wp.shape) != (9, 64, 64) for wp in packed) \
+            or len(packed) != co // 64:
+        raise ValueError(f"conv64_bias_relu: packed must be {co // 64} float16 [9, 64, 64] blocks on {x.device}")
     b = bias.detach().to(device=x.device, dtype=torch.float16).contiguous()
     ctx = _resolve_ctx(ctx, x)
     _bind_stream(ctx, True)
@@ -387,26 +398,28 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             three or four elementwise passes over the activation); other inputs take the torch modules."""
             if x.dtype == torch.float16 and x.is_cuda and conv.in_channels == 1 and conv.kernel_size == (3, 3) \
                     and conv.stride == (1, 1) and conv.padding == (1, 1) and conv.out_channels in (8, 16, 32, 64, 128, 256) \
-                    and x.dim() == 4 and x.shape[1] == 1 and not pool and not os.environ.get("FD_SP_UNFUSED") \
-                    and not os.environ.get("FD_SP_NO_CONV1"):  # (A/B switches)
+                    and x.dim() == 4 and x.shape[1] == 1 and not pool and not _ab_env("FD_SP_UNFUSED") \
+                    and not _ab_env("FD_SP_NO_CONV1"):  # (A/B switches)
                 # first layer: write-bound (9 MACs per output), one pass instead of convolution + bias pass
                 return conv1_bias_relu(x.contiguous(), conv.weight, conv.bias)
             if x.dtype == torch.float16 and x.is_cuda and conv.in_channels == 64 and conv.out_channels % 64 == 0 \
                     and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1) \
                     and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) \
                     and (not pool or (x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)) \
-                    and not os.environ.get("FD_SP_UNFUSED") and not os.environ.get("FD_SP_NO_C64") \
-                    and (conv.out_channels == 64 or not os.environ.get("FD_SP_C64_ONLY64")):  # (A/B switches)
+                    and not _ab_env("FD_SP_UNFUSED") and not _ab_env("FD_SP_NO_C64") \
+                    and (conv.out_channels == 64 or not _ab_env("FD_SP_C64_ONLY64")):  # (A/B switches)
                 # 64 -> 64 k layers on the matrix cores with bias, ReLU and pooling in the epilogue
-                key = f"_fd_packed_{conv.weight.data_ptr()}_{conv.weight._version}"  # (in-place updates repack)
-                wp = getattr(self, key, None)
-                if wp is None:
-                    wp = [pack_conv3x3_weight(conv.weight[k:k + 64].to(torch.float16))
-                          for k in range(0, conv.out_channels, 64)]
-                    setattr(self, key, wp)
-                return conv64_bias_relu(x, conv.weight, conv.bias, pool, packed=wp)
+                # one packed copy per layer, replaced when the weight changes (in-place update, reload, device)
+                tag = (conv.weight.data_ptr(), conv.weight._version, x.device)
+                cache = self.__dict__.setdefault("_fd_packed", {})
+                hit = cache.get(id(conv))
+                if hit is None or hit[0] != tag:
+                    hit = (tag, [pack_conv3x3_weight(conv.weight[k:k + 64].to(device=x.device, dtype=torch.float16))
+                                 for k in range(0, conv.out_channels, 64)])
+                    cache[id(conv)] = hit
+                return conv64_bias_relu(x, conv.weight, conv.bias, pool, packed=hit[1])
             if x.dtype == torch.float16 and x.is_cuda and x.is_contiguous(memory_format=torch.channels_last) \
-                    and conv.out_channels % 8 == 0 and not os.environ.get("FD_SP_UNFUSED"):  # (A/B switch)
+                    and conv.out_channels % 8 == 0 and not _ab_env("FD_SP_UNFUSED"):  # (A/B switch)
                 y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding)
                 if y.is_contiguous(memory_format=torch.channels_last):
                     return bias_relu(y, conv.bias, pool, out=None if pool else y)
@@ -553,7 +566,7 @@ class NNFeaturePointDetector:
         # conv shape (~30 s). That solver never wins, so it is left out of the search unless the caller
         # set the variable: first find ~10 s, ~0.6 s once MIOpen's user find-db holds the shapes.
         os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
-        torch.backends.cudnn.benchmark = os.environ.get("FD_SP_FIND_EXHAUSTIVE", "1") == "1"
+        torch.backends.cudnn.benchmark = _ab_env("FD_SP_FIND_EXHAUSTIVE", "1") == "1"
         ones = torch.ones((1, self._options.kMaxImageRows, self._options.kMaxImageCols), dtype=torch.uint8, device=dev)
         self.InferenceSession(ones)
         return True

@@ -392,6 +392,14 @@ int fd_nn_conv3x3_c64(fd_ctx *ctx, const void *x, const void *weight_packed, con
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);
 
+/*
+ * ABI version of this header: bumped whenever an entry point's parameter list changes (5: int64_t
+ * bias_len in fd_nn_bias_relu). Bindings compare fd_abi_version() with the FD_ABI_VERSION they were
+ * written for and refuse a mismatched library, instead of passing misread arguments.
+ */
+#define FD_ABI_VERSION 5
+int fd_abi_version(void);
+
 /* ---- ingest: pinned, pipelined host frames -> features ------------------------ */
 /*
  * A streaming front end for DetectGoodFeatures on host frames (what the reference's callers do per

@@ -313,6 +313,7 @@ def test_lane_widths_bit_exact(fd, oracle, image_png, monkeypatch, px):
     library picks one by launch size) gives the oracle's unordered candidate set and, through detect
     (sorted-segment and list modes, with and without priors), the oracle's features."""
     torch = pytest.importorskip("torch")
+    monkeypatch.setenv("FD_DEBUG_AB", "1")  # (the library reads A/B switches only with it)
     monkeypatch.setenv("FD_PX", px)
     frames = [image_png, oracle.make_frame("noise", 31, 480, 640), oracle.make_frame("checker", 32, 250, 13),
               oracle.make_frame("noise", 33, 37, 1001)]

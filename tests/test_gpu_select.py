@@ -62,6 +62,7 @@ def test_repeated_calls_reset_state(fd, oracle):
 @pytest.mark.parametrize("groups", ["1", "3", "64"])
 def test_gather_kernel_groups(fd, oracle, groups, monkeypatch):
     # FD_GATHER_GROUPS=1: k_select gathers its first chunk itself; >1: k_gather (own kernel) does
+    monkeypatch.setenv("FD_DEBUG_AB", "1")  # (the library reads A/B switches only with it)
     monkeypatch.setenv("FD_GATHER_GROUPS", groups)
     frames = np.stack([oracle.make_frame("noise", 90 + i, 240, 320) for i in range(2)])
     for name in ("harris", "fast"):
@@ -73,6 +74,7 @@ def test_sorted_segment_lists_toggle(fd, oracle, seg, monkeypatch):
     # FD_SEG_LISTS=1 (default below a megapixel): each candidate-kernel workgroup writes its list
     # segment sorted by level-0 bin and k_select reads only the segments' prefixes for its first
     # chunk; tiles that overflow their staging (dense FAST) mark the frame and k_select scans it
+    monkeypatch.setenv("FD_DEBUG_AB", "1")  # (the library reads A/B switches only with it)
     monkeypatch.setenv("FD_SEG_LISTS", seg)
     for shape, bsz in (((480, 640), 1), ((240, 320), 3), ((61, 77), 2), ((700, 1000), 1)):
         frames = np.stack([oracle.make_frame("noise" if i % 2 == 0 else "checker", 700 + i, *shape) for i in range(bsz)])

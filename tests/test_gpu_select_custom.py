@@ -89,6 +89,7 @@ def test_reference_order_emulation_stress(fd, oracle, seed, wide, monkeypatch):
     result stands alone; against the oracle's std::sort (sort_mode 0). wide: the multi-workgroup
     prelude forced on (FD_REF_WIDE=1; by default it runs for frames of >= 1 Mpx only): the 60k list
     goes through three prelude levels before k_select_reference."""
+    monkeypatch.setenv("FD_DEBUG_AB", "1")  # (the library reads A/B switches only with it)
     monkeypatch.setenv("FD_REF_WIDE", "1" if wide else "0")
     rng = np.random.default_rng(seed)
     rows, cols = 480, 640

@@ -31,6 +31,7 @@ def ref_wide(request, monkeypatch):
     """k_select_reference's multi-workgroup prelude (push order and the first partition levels of large
     frames): by frame size (>= 1 Mpx, "auto"), forced on or forced off (FD_REF_WIDE)."""
     if request.param != "auto":
+        monkeypatch.setenv("FD_DEBUG_AB", "1")  # (the library reads A/B switches only with it)
         monkeypatch.setenv("FD_REF_WIDE", "1" if request.param == "wide" else "0")
     return request.param
 

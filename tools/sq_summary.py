@@ -1,4 +1,4 @@
-"""Summary of tools/gpu_sq_ab.sh counter passes: usage: sq_summary.py <dir> <label> [<dir> <label> ...]"""
+"""Summary of SQ counter passes (tools/gpu_round_pmc.sh): usage: sq_summary.py <dir> <label> [<dir> <label> ...]"""
 import csv, glob, sys, collections
 for d, envs in zip(sys.argv[1::2], sys.argv[2::2]):
     acc = collections.defaultdict(lambda: collections.defaultdict(float)); disp = collections.defaultdict(set)
