@@ -35,14 +35,65 @@ MFMA_PEAK_TFLOPS_FP16 = 2500.0  # dense BF16/FP16 MFMA (MI355X_MICROARCH.md: ~2.
 # HBM traffic per launch measured with rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) and
 # corrected by the calibrated gfx950 factor (tools/gpu_traffic.sh, tools/calib/fetch_calib.hip).
 # (tools/gpu_round_pmc.sh + tools/make_round_profiles.py write both files)
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "r04_traffic.json")
-SQ_FILE = os.path.join(ROOT, "profiles", "r04_sq.json")
+
+
+def latest_profile(suffix):
+    """profiles/rNN_<suffix> of the latest round that committed one (None if none)."""
+    d = os.path.join(ROOT, "profiles")
+    try:
+        c = sorted(f for f in os.listdir(d) if f.startswith("r") and f.endswith("_" + suffix))
+    except OSError:
+        return None
+    return os.path.join(d, c[-1]) if c else None
+
+
+TRAFFIC_FILE = latest_profile("traffic.json")
+SQ_FILE = latest_profile("sq.json")
+KSTATS_FILE = latest_profile("bench_kernel_stats.csv")  # rocprofv3 --kernel-trace of bench.py, by bench leg
+STAMPS_FILE = latest_profile("select_stamps.txt")  # k_select phase clocks (FD_SELECT_STAMPS) at the headline
+
+
+def rocprof_kernel(phase_name, name_part):
+    """(avg us, calls, source) of a kernel in a bench leg of the committed rocprofv3 summary, or None."""
+    import csv
+
+    if not KSTATS_FILE:
+        return None
+    try:
+        with open(KSTATS_FILE) as fh:
+            rows = [r for r in csv.reader(l for l in fh if not l.startswith("#"))]
+    except OSError:
+        return None
+    for r in rows[1:]:
+        if len(r) >= 4 and r[0] == "fdbench:" + phase_name and name_part in r[1]:
+            return float(r[3]), int(r[2]), os.path.relpath(KSTATS_FILE, ROOT)
+    return None
+
+
+def select_phase_cycles():
+    """k_select's phase clocks of the first headline frame in the committed stamps file (FD_SELECT_STAMPS;
+    tools/select_stamps.py), or None: {phase: cycles} and the greedy scan's share of the total."""
+    if not STAMPS_FILE:
+        return None
+    try:
+        with open(STAMPS_FILE) as fh:
+            line = next(l for l in fh if l.startswith("k_select cycles:"))
+    except (OSError, StopIteration):
+        return None
+    toks = line.replace("|", " ").split()[2:]
+    ph = {}
+    for k, v in zip(toks[0::2], toks[1::2]):
+        if v.isdigit() and k not in ("subkeys", "chunks", "descents", "subchunks"):
+            ph[k] = int(v)
+    tot = sum(ph.values())
+    return {"source": os.path.relpath(STAMPS_FILE, ROOT), "cycles": ph,
+            "greedy_share": round(ph.get("greedy", 0) / tot, 3) if tot else None}
 
 
 def north_star_issue():
     """What bounds the north-star kernel, from the committed SQ counter pass (None if absent)."""
     try:
-        with open(SQ_FILE) as fh:
+        with open(SQ_FILE or "") as fh:
             q = json.load(fh)["ns_sq"]
     except (OSError, KeyError, ValueError):
         return None
@@ -81,7 +132,7 @@ def valu_floor(issue, pixels, kernel_ms):
 
 def measured_traffic(key):
     try:
-        with open(TRAFFIC_FILE) as fh:
+        with open(TRAFFIC_FILE or "") as fh:
             t = json.load(fh)
         return int(t[key]["read_bytes_corrected"]), os.path.relpath(TRAFFIC_FILE, ROOT)
     except (OSError, KeyError, ValueError):
@@ -160,8 +211,10 @@ def timed_graph(torch, fn, steps, warmup, use_graph, per_graph, barrier=None):
     for i in range(max(warmup, 1)):  # eager warmup also sizes the library workspace
         fn(i)
     torch.cuda.synchronize()
-    # Exactly `steps` steps: reps replays of a graph of per_graph steps + one graph of the remainder.
-    per_graph = max(1, min(per_graph, steps))
+    # Exactly `steps` steps: reps replays of a graph of per_graph steps + one graph of the remainder
+    # (per_graph 0: all steps in one graph, cycling the pool inside it -- one graph launch in the timed
+    # region, up to 1024 steps).
+    per_graph = max(1, min(per_graph if per_graph > 0 else 1024, steps))
     reps, rem = divmod(steps, per_graph)
     graphs = []
     for n in (per_graph, rem):
@@ -173,6 +226,7 @@ def timed_graph(torch, fn, steps, warmup, use_graph, per_graph, barrier=None):
             for i in range(n):
                 fn(i)
         g.replay()  # untimed: first replay uploads the graph
+        torch.cuda.synchronize()
         graphs.append(g)
     fence()
     t0 = time.perf_counter()
@@ -249,7 +303,7 @@ def run_config(torch, fd, dev, detector, rows, cols, batch, pool, need, dist, pa
     def step(i):
         fd.detect_points(detector, frames_pool[i % pool], need, dist, thr, out=(xy, cnt), ctx=ctx, ties=ties)
 
-    secs, done = timed_graph(torch, step, steps, warmup, use_graph, per_graph=pool, barrier=barrier)
+    secs, done = timed_graph(torch, step, steps, warmup, use_graph, per_graph=0, barrier=barrier)
     return secs, done, frames_pool, (xy, cnt)
 
 
@@ -840,6 +894,25 @@ def main():
     if traffic_src:
         roofline["traffic_source"] = (traffic_src + ": FETCH_SIZE x calibrated 2.0; at batch 1 short tiles re-read "
                                       "their halo rows and the level-0 histogram atomics are memory-side")
+    # The same kernel in the committed rocprofv3 summary of this bench command: its roofline_kernel leg
+    # (the launches timed above: agrees with avg_launch_ms), and its duration inside the headline step
+    # (shorter: there it follows k_select instead of another K1 append).
+    kname = "k_corner<" if args.detector != "fast" else "k_fast<"
+    rp = rocprof_kernel("roofline_kernel", kname)
+    rs = rocprof_kernel("headline", kname)
+    if rp:
+        roofline["rocprof"] = {"source": rp[2], "phase": "fdbench:roofline_kernel", "avg_us": rp[0], "calls": rp[1],
+                               "frac": round(k_bytes / (rp[0] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
+    if rs:
+        roofline["in_step"] = {"source": rs[2], "phase": "fdbench:headline", "avg_us": rs[0],
+                               "frac": round(k_bytes / (rs[0] * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)}
+    # the step's dominant kernel is latency-bound (one workgroup per frame): its time, in core clocks, and
+    # where those go (phase clocks of the headline frame)
+    sel = rocprof_kernel("headline", "k_select<")
+    latency = {"kernel": "k_select", "bound": "latency (one 1024-thread workgroup per frame)",
+               "avg_us": sel[0] if sel else None, "source": sel[2] if sel else None,
+               "cycles_at_peak_clock": round(sel[0] * CLOCK_GHZ * 1e3) if sel else None,
+               "phases": select_phase_cycles()}
     del pool
 
     out = {
@@ -853,6 +926,7 @@ def main():
                    "need": args.need, "min_feature_distance": args.dist, "min_valid_response": THR[args.detector],
                    "parallelism": f"frame-sharded x{world} (no collective)", "graph": not args.no_graph},
         "roofline": roofline,
+        "latency": latency,
         "kernels": kernels,
         "ties": ties_headline,
     }

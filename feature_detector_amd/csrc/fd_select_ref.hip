@@ -30,8 +30,12 @@
 //      each in LDS (ref_wave_resolve), which saves the last levels' barriers;
 //   3. the greedy scan of k_select_ordered over the new positions (one wave, occupancy grid); stop at
 //      `need`, else the next window (ranges right of the window wait in the range list).
-// A range that would reach the depth limit (std::__partial_sort, heapsort) is not emulated: the frame
-// gets FD_FRAME_UNRESOLVED and keeps k_select's features (the host resolves it when it synchronises).
+// A range that reaches the depth limit takes libstdc++'s fallback, std::__partial_sort(first, last, last)
+// = __make_heap + __sort_heap, emulated exactly by one wave (ref_heapsort: the heap built level by level,
+// the subtrees of one level being disjoint, then the pops by one lane), in LDS when the range fits there;
+// its visiting order is then final. FD_FRAME_UNRESOLVED is left only for a broken internal invariant
+// (range guards), in which case the frame keeps k_select's raster-order features (the host resolves it
+// when it synchronises).
 #include "fd_greedy.h"
 
 #include <algorithm>
@@ -88,7 +92,8 @@ struct alignas(16) RefLds {
     uint32_t wsum[kRefWaves];
     uint16_t rid[kRefRidCap];  // levels with T <= kRefRidCap: each element's active range (set by pass 1)
     uint16_t gpred[kGreedyPredBytes / 2];  // greedy_block's neighbour lists
-    int cur, m_all, m_act, n_leaf, fail, n_wl;
+    int cur, m_all, m_act, n_leaf, fail, n_wl, n_heap;
+    uint32_t heap_j[kRefMaxRanges];  // active ranges at depth 0 (heapsort fallback)
     uint32_t T, fin;
     int s_done, s_acc;
     uint32_t tie_prev;
@@ -203,19 +208,94 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t k) {
     return pos;
 }
 
+// ---- std::__partial_sort(first, last, last): the introsort's depth-limit fallback ---------------------
+// bits/stl_heap.h with comp = response greater (feature_point_detector.cpp:58-60): __adjust_heap sifts the
+// hole down to a leaf along the child that comp does not order first, then __push_heap moves the value up
+// while comp(parent, value). f is LDS or global memory (generic pointer).
+__device__ __forceinline__ bool ref_gt(uint2 a, uint2 b) { return __uint_as_float(a.x) > __uint_as_float(b.x); }
+
+__device__ void ref_adjust_heap(uint2 *f, int hole, int len, uint2 v) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (ref_gt(f[second], f[second - 1])) --second;
+        f[hole] = f[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        f[hole] = f[second - 1];
+        hole = second - 1;
+    }
+    while (hole > top) {  // __push_heap(f, hole, top, v)
+        const int parent = (hole - 1) / 2;
+        const uint2 pv = f[parent];
+        if (!ref_gt(pv, v)) break;
+        f[hole] = pv;
+        hole = parent;
+    }
+    f[hole] = v;
+}
+
+// One wave: __make_heap then __sort_heap on f[0, len). __make_heap adjusts parents (len - 2) / 2 down to 0;
+// the parents of one tree level own disjoint subtrees and the deeper levels come first, so the lanes
+// adjust a level's parents at once. __sort_heap's pops depend on each other: lane 0.
+__device__ __attribute__((noinline)) void ref_heapsort(uint2 *f, int len) {
+    if (len < 2) return;
+    const int lane = lane_id();
+    const int last_parent = (len - 2) / 2;
+    for (int k = 31 - __clz(last_parent + 1); k >= 0; --k) {
+        const int lo = (1 << k) - 1, hi = min((1 << (k + 1)) - 2, last_parent);
+        for (int p = lo + lane; p <= hi; p += kWave) ref_adjust_heap(f, p, len, f[p]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0)
+        for (int l = len - 1; l >= 1; --l) {
+            const uint2 v = f[l];
+            f[l] = f[0];
+            ref_adjust_heap(f, 0, l, v);
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One wave, one element per lane: libstdc++'s introsort on a range of 17..64 elements (E[0, len), in
 // LDS) to the end, every subrange of a level partitioned at once. Lane p keeps its subrange [sa, sb);
 // stopper ranks are popcounts of the subrange's ballot, the k-th stopper's position a bit select, the
 // exchanges and the pivot move shuffles. Leaves: stable rank by response, descending, into ordp.
-// Returns false if a subrange would reach the depth limit.
-__device__ bool ref_wave_small(const uint2 *E, uint32_t len, uint32_t dep, uint32_t *ordp) {
+// A subrange at the depth limit is heapsorted (ref_heapsort by its first lane, in E) and final.
+__device__ bool ref_wave_small(uint2 *E, uint32_t len, uint32_t dep, uint32_t *ordp) {
     const uint32_t p = static_cast<uint32_t>(lane_id());
     uint2 v = p < len ? E[p] : make_uint2(0u, 0u);
     uint32_t sa = 0, sb = len, dp = dep;
     for (int it = 0; it < 64; ++it) {
-        const bool big = p < len && sb - sa > static_cast<uint32_t>(kRefLeaf);
+        bool big = p < len && sb - sa > static_cast<uint32_t>(kRefLeaf);
         if (ballot(big) == 0ull) break;
-        if (ballot(big && dp == 0u) != 0ull) return false;  // std::__partial_sort
+        if (ballot(big && dp == 0u) != 0ull) {  // std::__partial_sort of those subranges
+            if (p < len) E[p] = v;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const bool hp = big && dp == 0u;
+            // (one subrange at a time: ref_heapsort is a whole-wave routine)
+            for (uint64_t leaders = ballot(hp && p == sa); leaders; leaders &= leaders - 1ull) {
+                const uint32_t q = static_cast<uint32_t>(__builtin_ctzll(leaders));
+                const uint32_t qa = static_cast<uint32_t>(__shfl(static_cast<int>(sa), static_cast<int>(q)));
+                const uint32_t qb = static_cast<uint32_t>(__shfl(static_cast<int>(sb), static_cast<int>(q)));
+                ref_heapsort(E + qa, static_cast<int>(qb - qa));
+            }
+            if (hp) {  // final positions: a one-element leaf each
+                v = E[p];
+                sa = p;
+                sb = p + 1u;
+            }
+            big = p < len && sb - sa > static_cast<uint32_t>(kRefLeaf);
+            if (ballot(big) == 0ull) break;
+        }
         // pivot: __move_median_to_first(sa, sa + 1, mid, sb - 1)
         const uint32_t mid = sa + (sb - sa) / 2u;
         const uint32_t i1 = min(sa + 1u, 63u), i2 = min(mid, 63u), i3 = sb >= 1u ? min(sb - 1u, 63u) : 0u;
@@ -280,7 +360,7 @@ __device__ bool ref_wave_small(const uint2 *E, uint32_t len, uint32_t dep, uint3
 // stoppers resp <= pivot from the left paired with right stoppers resp >= pivot from the right while
 // l_k < r_k, cut = min(l_K, r_{K-1})), then the final insertion sort of every leaf (stable, response
 // descending) -- with the elements in the wave's LDS. Writes the range's visiting order into ord[lo, hi).
-// Returns false if a partition would reach the depth limit (heapsort: not emulated).
+// A subrange at the depth limit is heapsorted (std::__partial_sort). Returns false on a broken invariant.
 __device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t hi, uint32_t dep, uint2 *E,
                                  uint16_t *Lp, uint16_t *Rp, uint32_t *stk) {
     const int lane = lane_id();
@@ -320,9 +400,10 @@ __device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t 
             if (lane < kRefLeaf && q < len) ord[lo + a + rk] = v.y;
             continue;
         }
-        if (dp == 0u) {  // std::__partial_sort
-            ok = false;
-            break;
+        if (dp == 0u) {  // std::__partial_sort(a, b, b): heapsorted in E, final
+            ref_heapsort(E + a, static_cast<int>(b - a));
+            for (uint32_t i = lane; i < b - a; i += kWave) ord[lo + a + i] = E[a + i].y;
+            continue;
         }
         // pivot: __move_median_to_first(a, a + 1, mid, b - 1)
         const uint32_t mid = a + (b - a) / 2u;
@@ -595,6 +676,68 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
     for (int guard = 0; guard < 1 << 16; ++guard) {  // windows x levels (bounded: each level halves)
         const int m = L.m_act;
         if (m > 0) {
+            // ---- active ranges at the depth limit: std::__partial_sort(first, last, last) -----------------
+            // Heapsorted one at a time by wave 0 (in LDS when the range fits the free space: the greedy
+            // span before the grid exists, pxy .. cmask after), their visiting order written to ord (final),
+            // and dropped from the range list; then the level runs on the rest.
+            if (tid == 0) L.n_heap = 0;
+            __syncthreads();
+            if (tid < m && L.r_dep[L.cur][tid] == 0u) L.heap_j[atomicAdd(&L.n_heap, 1)] = static_cast<uint32_t>(tid);
+            __syncthreads();
+            if (L.n_heap > 0) {
+                if (wv == 0) {
+                    const int c = L.cur, nh = L.n_heap;
+                    const uint32_t cap_lds = static_cast<uint32_t>(
+                        (grid_ready ? sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask)
+                                    : sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask) + sizeof(L.grid_lds)) / sizeof(uint2));
+                    for (int h = 0; h < nh; ++h) {
+                        const uint32_t j = L.heap_j[h];
+                        const uint32_t lo = L.r_lo[c][j], hi = min(L.r_hi[c][j], n);
+                        const uint32_t len = hi > lo ? hi - lo : 0u;
+                        uint2 *hbuf = X + lo;
+                        if (len <= cap_lds) {
+                            hbuf = reinterpret_cast<uint2 *>(L.pxy);
+                            for (uint32_t i = lane; i < len; i += kWave) hbuf[i] = X[lo + i];
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        ref_heapsort(hbuf, static_cast<int>(len));
+                        for (uint32_t i = lane; i < len; i += kWave) {
+                            const uint2 e = hbuf[i];
+                            X[lo + i] = e;
+                            ord[lo + i] = e.y;
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
+                    // the list without them (order kept), into the other buffer
+                    const int nc = c ^ 1;
+                    uint32_t at = 0;
+                    for (int b = 0; b < L.m_all; b += kWave) {
+                        const int j = b + lane;
+                        const bool keep = j < L.m_all && !(j < m && L.r_dep[c][j] == 0u);
+                        const uint64_t bk = ballot(keep);
+                        if (keep) {
+                            const uint32_t q = at + static_cast<uint32_t>(mbcnt64(bk, 0));
+                            L.r_lo[nc][q] = L.r_lo[c][j];
+                            L.r_hi[nc][q] = L.r_hi[c][j];
+                            L.r_dep[nc][q] = L.r_dep[c][j];
+                        }
+                        at += static_cast<uint32_t>(popc64(bk));
+                    }
+                    if (lane == 0) {
+                        L.m_all = static_cast<int>(at);
+                        L.cur = nc;
+                    }
+                    __builtin_amdgcn_s_waitcnt(0);
+                    set_active(L, L.fin + kSelectChunk);
+                }
+                __syncthreads();
+                FD_REF_COUNT(31, 1u);
+                continue;
+            }
             // ---- one partition level over the active ranges ----------------------------------------------
             const int c = L.cur;
             const uint64_t t_level = a.stamps && tid == 0 ? __builtin_readcyclecounter() : 0ull;

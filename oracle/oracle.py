@@ -14,7 +14,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "liborc.so")
-SRCS = [os.path.join(HERE, f) for f in ("fd_oracle.cpp", "fd_oracle_refflow.cpp", "fd_oracle_lines.cpp", "Makefile")]
+SRCS = [os.path.join(HERE, f) for f in ("fd_oracle.cpp", "fd_oracle_refflow.cpp", "fd_oracle_lines.cpp",
+                                        "fd_oracle_introsort.cpp", "Makefile")]
 
 HARRIS, SHI_TOMASI, FAST = 0, 1, 2
 _P = ctypes.c_void_p
@@ -58,6 +59,9 @@ def lib():
             "orc_ref_state_new": (_P, []),
             "orc_ref_state_free": (None, [_P]),
             "orc_detect_refflow": (i32, [_P, i32, _P, i32, i32, i32, f32, u32, _P, i32]),
+            "orc_std_sort_perm": (None, [_P, i64, _P]),
+            "orc_std_sort_restated": (None, [_P, i64, _P, _P]),
+            "orc_introsort_killer": (None, [i64, i32, _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -180,6 +184,34 @@ class RefFlowDetector:
         if getattr(self, "_s", None) and _lib is not None:
             _lib.orc_ref_state_free(self._s)
             self._s = None
+
+
+def std_sort_perm(resp):
+    """The visiting order std::sort gives (resp, push index) pairs with the reference comparator
+    (feature_point_detector.cpp:58-60): indices into resp."""
+    resp = np.ascontiguousarray(resp, np.float32)
+    perm = np.zeros(len(resp), np.uint32)
+    lib().orc_std_sort_perm(_ptr(resp), len(resp), _ptr(perm))
+    return perm
+
+
+def std_sort_restated(resp):
+    """libstdc++ 11's std::sort restated (oracle/fd_oracle_introsort.cpp) -> (perm, stats): stats =
+    (heapsorted ranges, frontmost heapsorted range lo, hi (-1: none), smallest depth left)."""
+    resp = np.ascontiguousarray(resp, np.float32)
+    perm = np.zeros(len(resp), np.uint32)
+    stats = np.zeros(4, np.int64)
+    lib().orc_std_sort_restated(_ptr(resp), len(resp), _ptr(perm), _ptr(stats))
+    return perm, stats
+
+
+def introsort_killer(n, front=True):
+    """Responses (push order) built by McIlroy's adversary against std::sort with the reference
+    comparator: the introsort reaches its depth limit (heapsort); front: in the range the greedy visits
+    first, which then starts with a run of equal responses."""
+    out = np.zeros(n, np.float32)
+    lib().orc_introsort_killer(n, 1 if front else 0, _ptr(out))
+    return out
 
 
 def prefix_has_ties(sorted_resp, n_scanned):

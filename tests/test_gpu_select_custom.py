@@ -158,3 +158,46 @@ def test_invalid_candidates_refused(fd):
     # the context keeps working after a refused call
     res = fd.select_points([(r, np.array([1, 9], np.int32), np.array([1, 1], np.int32))], 480, 640, 10, 3)
     assert np.array_equal(res.features(0), np.array([[1, 1], [9, 1]], np.float32))
+
+
+@pytest.mark.parametrize("n", [40, 200, 1000, 5000, 20000])
+def test_reference_order_depth_limit(fd, oracle, n):
+    """Candidate lists on which std::sort's introsort reaches its depth limit inside the visited prefix
+    (McIlroy's adversary, oracle.introsort_killer: every pivot an extreme, a run of equal responses left
+    in the long front range), so the reference's order of those ties is std::__partial_sort's
+    (heapsort). k_select flags the frame, k_select_reference emulates the heapsort on the GPU
+    (ref_heapsort: in the workgroup levels for the long ranges, in a wave's LDS for <= 256 / <= 64
+    elements): device lists, host lists and a graph replay all equal oracle.select(sort_mode=0) -- the
+    real std::sort -- and no frame is left unresolved."""
+    torch = pytest.importorskip("torch")
+    rows, cols = 480, 640
+    rng = np.random.default_rng(n)
+    r = oracle.introsort_killer(n, True)
+    idx = rng.permutation(rows * cols)[:n]
+    lst = (r, (idx % cols).astype(np.int32), (idx // cols).astype(np.int32))
+    for dist, need in ((3, 200), (0, n), (40, 60)):
+        exp = oracle.select(*lst, rows, cols, dist, need, None, sort_mode=0)
+        host = fd.select_points([lst], rows, cols, need, dist, ties="reference")
+        assert np.array_equal(host.features(0), exp), ("host", dist, need)
+        dev = fd.select_points(_dev_lists([lst]), rows, cols, need, dist, ties="reference")
+        st = dev.frame_flags()
+        assert st[0] & fd.points.FRAME_TIES and st[0] & fd.points.FRAME_RESOLVED, hex(int(st[0]))
+        assert not st[0] & fd.points.FRAME_UNRESOLVED
+        assert np.array_equal(dev.check().features(0), exp), ("device", dist, need)
+    # graph replay (the emulation is capturable: no host round trip)
+    dl = _dev_lists([lst])
+    xy = torch.empty((1, 201, 2), dtype=torch.float32, device="cuda")
+    cnt = torch.empty((1,), dtype=torch.int32, device="cuda")
+    fd.select_points(dl, rows, cols, 200, 3, ties="reference", out=(xy, cnt))  # sizes the workspace
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        fd.select_points(dl, rows, cols, 200, 3, ties="reference", out=(xy, cnt))
+    exp = oracle.select(*lst, rows, cols, 3, 200, None, sort_mode=0)
+    for _ in range(2):
+        xy.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(xy[0, :int(cnt[0])].cpu().numpy(), exp)

@@ -31,3 +31,30 @@ def test_select_duplicates_and_negative_distance(oracle):
     assert oracle.select(r, x, y, 10, 10, 0, 10).tolist() == [[1, 0], [4, 2], [6, 2]]
     assert oracle.select(r, x, y, 10, 10, -1, 10).tolist() == [[1, 0], [1, 0], [4, 2], [4, 2], [6, 2]]
     assert oracle.select(r, x, y, 10, 10, 2, 10).tolist() == [[1, 0], [4, 2]]
+
+
+@pytest.mark.parametrize("n", [17, 100, 1000, 5000, 20000])
+@pytest.mark.parametrize("front", [True, False])
+def test_introsort_restatement_on_killer_inputs(oracle, n, front):
+    """libstdc++ 11's std::sort restated (oracle/fd_oracle_introsort.cpp: introsort loop, median of three,
+    unguarded partition, depth limit 2 floor(log2 n) -> __make_heap + __sort_heap, final insertion sort)
+    gives std::sort's own permutation on McIlroy-adversary inputs, which reach the heapsort fallback and
+    carry a run of equal responses into the heapsorted range: the fallback's order of ties is pinned to
+    the real library here, and the GPU emulation (fd_select_ref.hip ref_heapsort) is checked against it."""
+    r = oracle.introsort_killer(n, front)
+    perm, stats = oracle.std_sort_restated(r)
+    assert np.array_equal(perm, oracle.std_sort_perm(r))
+    if n >= 40:
+        assert stats[0] >= 1  # the depth limit was reached
+        if front:
+            assert stats[1] == 0 and stats[2] > n // 2  # ... in the range the greedy visits first
+        srt = r[perm]
+        assert (srt[1:] == srt[:-1]).sum() > n // 4  # with ties inside it
+
+
+def test_introsort_restatement_random(oracle):
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 16, 17, 300, 4097):
+        for k in (2, 7, 1000):
+            r = rng.integers(0, k, n).astype(np.float32)
+            assert np.array_equal(oracle.std_sort_restated(r)[0], oracle.std_sort_perm(r))
