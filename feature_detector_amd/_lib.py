@@ -20,7 +20,7 @@ EXPORTS = (
     "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_ctx_set_tie_order", "fd_ctx_frame_status", "fd_points_detect", "fd_points_candidates", "fd_points_response",
     "fd_points_response_append", "fd_points_select",
     "fd_lsd_map", "fd_lsd_map_pitched", "fd_lsd_lines", "fd_lsd_lines_state", "fd_brief_compute", "fd_nn_select", "fd_nn_select_list", "fd_nn_descriptors",
-    "fd_nn_bias_relu", "fd_nn_conv3x3_c1", "fd_nn_conv3x3_c64",
+    "fd_nn_bias_relu", "fd_nn_conv3x3_c1", "fd_nn_conv3x3_c64", "fd_nn_conv3x3_c1c64",
     "fd_build_info", "fd_abi_version", "fd_png_info", "fd_png_decode", "fd_png_frames",
     "fd_ingest_create", "fd_ingest_destroy", "fd_ingest_frames", "fd_ingest_submit", "fd_ingest_wait",
 )
@@ -109,6 +109,7 @@ def load() -> ctypes.CDLL:
         "fd_nn_bias_relu": (i32, [P, P, P, i64, P, i32, i32, i32, i32, i32]),
         "fd_nn_conv3x3_c1": (i32, [P, P, P, P, i64, P, i32, i32, i32]),
         "fd_nn_conv3x3_c64": (i32, [P, P, P, P, P, i32, i32, i32, i32, i32, i32]),
+        "fd_nn_conv3x3_c1c64": (i32, [P, P, P, P, P, P, P, i32, i32, i32, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
         "fd_abi_version": (i32, []),
         "fd_png_info": (i32, [P, ctypes.c_size_t, P, P, P]),
@@ -121,7 +122,12 @@ def load() -> ctypes.CDLL:
         "fd_ingest_wait": (i32, [P, i32, ctypes.POINTER(P), ctypes.POINTER(P)]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if os.environ.get("FD_LIB_PATH"):  # an older build under A/B: its missing entry points stay unbound
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     abi = L.fd_abi_version()

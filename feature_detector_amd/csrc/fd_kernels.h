@@ -123,6 +123,7 @@ struct SelectArgs {
     int dup_keys;      // equal selection keys possible (caller lists): the orderings rank them stably
     int par_greedy;    // workgroup-parallel greedy (greedy_block: sparse NMS candidates) instead of the wave scan
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
+    int repeat;        // diagnostic only (FD_SELECT_REPEAT): run the selection this many extra times (warm caches)
 };
 
 // Greedy selection over candidates given in an explicit order (FD_TIES_REFERENCE: the reference's
@@ -304,8 +305,10 @@ hipError_t launch_brief(const BriefArgs &a, hipStream_t s);
 hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s);
 int heat_blocks_per_frame(int64_t npx);
 hipError_t launch_nn_desc(const NnDescArgs &a, hipStream_t s);
+// (w1, b1 non-null: x is the one-channel frame and conv1a -- 1 -> 64, 3x3, bias, ReLU -- is fused in)
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
-                              int y_channels, int y_offset, hipStream_t s);
+                              int y_channels, int y_offset, hipStream_t s, const void *w1 = nullptr,
+                              const void *b1 = nullptr);
 hipError_t launch_conv3x3_c1_bias_relu(const void *x, const void *wt, const void *bias, void *y, int n, int h, int w,
                                        int c, hipStream_t s);
 hipError_t launch_bias_relu(const void *x, const void *bias, void *y, int n, int h, int w, int c, int pool,

@@ -163,11 +163,22 @@ __device__ __forceinline__ float cv_epilogue(float acc, float b) {
     return v > static_cast<_Float16>(0.0f) ? static_cast<float>(v) : 0.0f;
 }
 
-template <bool POOL>
+// FUSED (SuperPoint conv1a + conv1b, fd_nn_conv3x3_c1c64): the tile's 64-channel input is conv1a itself
+// (1 -> 64 channels, 3x3, bias, ReLU) recomputed from the one-channel frame rows the tile reaches (a
+// 2-pixel halo), so the full-resolution 64-channel activation never goes to HBM (~2.5 GB written and
+// read back, 1.55x with the halo, per 64 640x480 frames). Each thread keeps one 8-channel group's 72
+// conv1a weights in registers and produces that group for 1/32 of the tile's 6 x 66 input pixels: the
+// same float FMA chain in tap order, rounding to half, bias in float, rounding and ReLU as
+// k_conv3x3_c1_bias_relu, so the staged values equal that kernel's output bit for bit (zero outside the
+// frame: conv1b's own zero padding). x is then the [n][h][w] fp16 frame, w1 [64][9], b1 [64].
+template <bool POOL, bool FUSED>
 __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 *wpk, const _Float16 *bias, u4 *y,
-                                                          int n, int h, int w, int ystride, int yoff) {
+                                                          int n, int h, int w, int ystride, int yoff,
+                                                          const _Float16 *w1 = nullptr, const _Float16 *b1 = nullptr) {
     __shared__ u4 Wl[9 * 64 * 8];
     __shared__ u4 In[kCvInRows * kCvInCols * 8];  // (also the output staging after the K loop)
+    constexpr int kRawRows = kCvInRows + 2, kRawCols = kCvInCols + 2;
+    __shared__ _Float16 raw[FUSED ? kRawRows : 1][FUSED ? kRawCols : 1];  // conv1a's input rows (FUSED)
     const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
     for (int i = tid; i < 9 * 64 * 8; i += 256) {
         const int ch = i & 7, row = i >> 3, co = row & 63;
@@ -178,21 +189,47 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
     for (int nb = 0; nb < 4; ++nb) bv[nb] = static_cast<float>(bias[nb * 16 + (lane & 15)]);
     const int th = (h + kCvRows - 1) / kCvRows, tw = (w + kCvCols - 1) / kCvCols;
     const int total = n * th * tw;  // (< 2^31: checked on the host)
+    // FUSED: this thread's conv1a channel group (8 channels) and its weights
+    const int cg = tid & 7;
+    f2 w1f[4][9], b1f[4];
+    if constexpr (FUSED) {
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+                w1f[k2][t] = f2{static_cast<float>(w1[(cg * 8 + 2 * k2) * 9 + t]), static_cast<float>(w1[(cg * 8 + 2 * k2 + 1) * 9 + t])};
+            b1f[k2] = f2{static_cast<float>(b1[cg * 8 + 2 * k2]), static_cast<float>(b1[cg * 8 + 2 * k2 + 1])};
+        }
+    }
     // the input tile goes through registers: the next tile's loads are issued before this tile's K loop
-    // and stored to LDS after it, so their latency hides behind the matrix work
-    constexpr int kChunks = kCvInRows * kCvInCols * 8, kPer = (kChunks + 255) / 256;
+    // and stored to LDS after it, so their latency hides behind the matrix work (FUSED: the raw rows)
+    constexpr int kChunks = kCvInRows * kCvInCols * 8, kPer = FUSED ? 1 : (kChunks + 255) / 256;
+    constexpr int kRawN = kRawRows * kRawCols, kRawPer = (kRawN + 255) / 256;
     u4 pre[kPer];
+    _Float16 praw[kRawPer];
     auto fetch = [&](int tile) {
         const int tx = tile % tw, t2 = tile / tw, ty = t2 % th, f = t2 / th;
         const int r0 = ty * kCvRows, c0 = tx * kCvCols;
+        if constexpr (FUSED) {
+            const _Float16 *xf = reinterpret_cast<const _Float16 *>(x);
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int i = tid + k * 256;
-            const int ch = i & 7, px = i >> 3, pc = px % kCvInCols, pr = px / kCvInCols;
-            const int gy = r0 - 1 + pr, gx = c0 - 1 + pc;
-            pre[k] = u4{0u, 0u, 0u, 0u};
-            if (i < kChunks && tile < total && gy >= 0 && gy < h && gx >= 0 && gx < w)
-                pre[k] = x[((static_cast<int64_t>(f) * h + gy) * w + gx) * 8 + ch];
+            for (int k = 0; k < kRawPer; ++k) {
+                const int i = tid + k * 256, rr = i / kRawCols, rc = i - rr * kRawCols;
+                const int gy = r0 - 2 + rr, gx = c0 - 2 + rc;
+                praw[k] = static_cast<_Float16>(0.0f);
+                if (i < kRawN && tile < total && gy >= 0 && gy < h && gx >= 0 && gx < w)
+                    praw[k] = xf[(static_cast<int64_t>(f) * h + gy) * w + gx];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                const int i = tid + k * 256;
+                const int ch = i & 7, px = i >> 3, pc = px % kCvInCols, pr = px / kCvInCols;
+                const int gy = r0 - 1 + pr, gx = c0 - 1 + pc;
+                pre[k] = u4{0u, 0u, 0u, 0u};
+                if (i < kChunks && tile < total && gy >= 0 && gy < h && gx >= 0 && gx < w)
+                    pre[k] = x[((static_cast<int64_t>(f) * h + gy) * w + gx) * 8 + ch];
+            }
         }
     };
     fetch(static_cast<int>(blockIdx.x));
@@ -200,14 +237,53 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
         const int tx = tile % tw, t2 = tile / tw, ty = t2 % th, f = t2 / th;
         const int r0 = ty * kCvRows, c0 = tx * kCvCols;
         __syncthreads();  // (the previous tile's staging is read out; the filter is in place)
+        if constexpr (FUSED) {
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int i = tid + k * 256;
-            const int px = i >> 3, pc = px % kCvInCols;
-            if (i < kChunks) In[px * 8 + ((i & 7) ^ (pc & 7))] = pre[k];
+            for (int k = 0; k < kRawPer; ++k) {
+                const int i = tid + k * 256, rr = i / kRawCols;
+                if (i < kRawN) raw[rr][i - rr * kRawCols] = praw[k];
+            }
+            __syncthreads();
+            fetch(tile + static_cast<int>(gridDim.x));
+            // conv1a over the tile's input pixels (6 x 66), 8 channels per item
+            for (int px = tid >> 3; px < kCvInRows * kCvInCols; px += 32) {
+                const int pr = px / kCvInCols, pc = px - pr * kCvInCols;
+                const int gy = r0 - 1 + pr, gx = c0 - 1 + pc;
+                u4 o = u4{0u, 0u, 0u, 0u};
+                if (gy >= 0 && gy < h && gx >= 0 && gx < w) {
+                    float in[9];
+#pragma unroll
+                    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                        for (int dx = 0; dx < 3; ++dx) in[dy * 3 + dx] = static_cast<float>(raw[pr + dy][pc + dx]);
+#pragma unroll
+                    for (int k2 = 0; k2 < 4; ++k2) {
+                        f2 acc2 = f2{0.0f, 0.0f};
+#pragma unroll
+                        for (int t = 0; t < 9; ++t) acc2 = __builtin_elementwise_fma(w1f[k2][t], f2{in[t], in[t]}, acc2);
+                        uint32_t packed = 0;
+#pragma unroll
+                        for (int hlf = 0; hlf < 2; ++hlf) {
+                            _Float16 v = static_cast<_Float16>(static_cast<float>(static_cast<_Float16>(acc2[hlf])) + b1f[k2][hlf]);
+                            v = v > static_cast<_Float16>(0.0f) ? v : static_cast<_Float16>(0.0f);
+                            packed |= static_cast<uint32_t>(__builtin_bit_cast(uint16_t, v)) << (16 * hlf);
+                        }
+                        o[k2] = packed;
+                    }
+                }
+                In[px * 8 + (cg ^ (pc & 7))] = o;
+            }
+            __syncthreads();
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                const int i = tid + k * 256;
+                const int px = i >> 3, pc = px % kCvInCols;
+                if (i < kChunks) In[px * 8 + ((i & 7) ^ (pc & 7))] = pre[k];
+            }
+            __syncthreads();
+            fetch(tile + static_cast<int>(gridDim.x));
         }
-        __syncthreads();
-        fetch(tile + static_cast<int>(gridDim.x));
         f4 acc[kCvRows][4];
 #pragma unroll
         for (int m = 0; m < kCvRows; ++m)
@@ -297,17 +373,29 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
 }  // namespace
 
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
-                              int y_channels, int y_offset, hipStream_t s) {
+                              int y_channels, int y_offset, hipStream_t s, const void *w1, const void *b1) {
     const int ystride = y_channels / 8, yoff = y_offset / 8;
     const int64_t tiles = static_cast<int64_t>(n) * ((h + kCvRows - 1) / kCvRows) * ((w + kCvCols - 1) / kCvCols);
     if (tiles == 0) return hipSuccess;
     const unsigned grid = static_cast<unsigned>(std::min<int64_t>(tiles, 1024));
-    if (pool)
-        hipLaunchKernelGGL(k_conv3x3_c64_mfma<true>, dim3(grid), dim3(256), 0, s, static_cast<const u4 *>(x),
-                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w, ystride, yoff);
-    else
-        hipLaunchKernelGGL(k_conv3x3_c64_mfma<false>, dim3(grid), dim3(256), 0, s, static_cast<const u4 *>(x),
-                           static_cast<const u4 *>(wpk), static_cast<const _Float16 *>(bias), static_cast<u4 *>(y), n, h, w, ystride, yoff);
+    const u4 *xv = static_cast<const u4 *>(x), *wv = static_cast<const u4 *>(wpk);
+    const _Float16 *bv = static_cast<const _Float16 *>(bias), *w1h = static_cast<const _Float16 *>(w1),
+                   *b1h = static_cast<const _Float16 *>(b1);
+    u4 *yv = static_cast<u4 *>(y);
+    if (w1) {  // conv1a fused into the staging (fd_nn_conv3x3_c1c64)
+        if (pool)
+            hipLaunchKernelGGL((k_conv3x3_c64_mfma<true, true>), dim3(grid), dim3(256), 0, s, xv, wv, bv, yv, n, h, w, ystride,
+                               yoff, w1h, b1h);
+        else
+            hipLaunchKernelGGL((k_conv3x3_c64_mfma<false, true>), dim3(grid), dim3(256), 0, s, xv, wv, bv, yv, n, h, w, ystride,
+                               yoff, w1h, b1h);
+    } else if (pool) {
+        hipLaunchKernelGGL((k_conv3x3_c64_mfma<true, false>), dim3(grid), dim3(256), 0, s, xv, wv, bv, yv, n, h, w, ystride,
+                           yoff, nullptr, nullptr);
+    } else {
+        hipLaunchKernelGGL((k_conv3x3_c64_mfma<false, false>), dim3(grid), dim3(256), 0, s, xv, wv, bv, yv, n, h, w, ystride,
+                           yoff, nullptr, nullptr);
+    }
     return hipGetLastError();
 }
 

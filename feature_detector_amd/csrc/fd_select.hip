@@ -1154,6 +1154,10 @@ __global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
     __shared__ SelectLds L;
     const int f = blockIdx.x;
     select_frame<NT, WIDE>(a, f, L);
+    for (int r = 0; r < a.repeat; ++r) {  // (diagnostic: the same selection with warm caches; stamps of the last)
+        __syncthreads();
+        select_frame<NT, WIDE>(a, f, L);
+    }
     finish_frame(a, f);
 }
 

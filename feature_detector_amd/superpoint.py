@@ -289,6 +289,45 @@ def conv64_bias_relu(x, weight, bias, pool: bool = False, out=None, ctx: Context
     return out
 
 
+def conv1ab_bias_relu(x, weight1, bias1, weight, bias, pool: bool = True, out=None, ctx: Context | None = None,
+                      packed=None):
+    """fd_nn_conv3x3_c1c64: the encoder's first two layers in one pass -- conv1a (1 -> 64, 3x3, bias, ReLU)
+    recomputed inside conv1b's tiles (64 -> 64, 3x3, bias, ReLU, and the 2x2 max pool when pool), so the
+    full-resolution 64-channel activation never goes to memory. x [N, 1, H, W] fp16 on the device ->
+    [N, 64, H(/2), W(/2)] fp16 channels-last; equal bit for bit to conv64_bias_relu(conv1_bias_relu(x))."""
+    import torch
+
+    if not (x.is_cuda and x.dtype == torch.float16 and x.dim() == 4 and x.shape[1] == 1
+            and (x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last))):
+        raise ValueError("conv1ab_bias_relu: x must be a [N, 1, H, W] float16 device tensor")
+    n, _, h, w = x.shape
+    if tuple(weight1.shape) != (64, 1, 3, 3) or bias1.numel() != 64 or tuple(weight.shape) != (64, 64, 3, 3) \
+            or bias.numel() != 64:
+        raise ValueError("conv1ab_bias_relu: weight1 [64, 1, 3, 3], weight [64, 64, 3, 3], 64-value biases")
+    if pool and (h % 2 or w % 2):
+        raise ValueError("conv1ab_bias_relu: pooling needs even H and W")
+    shape = (n, 64, h // 2, w // 2) if pool else (n, 64, h, w)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
+    elif not (out.dtype == torch.float16 and tuple(out.shape) == shape and out.device == x.device
+              and out.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError(f"conv1ab_bias_relu: out must be a channels-last float16 {list(shape)} tensor on {x.device}")
+    if packed is None:
+        packed = pack_conv3x3_weight(weight.to(device=x.device, dtype=torch.float16))
+    w1 = weight1.detach().to(device=x.device, dtype=torch.float16).contiguous()
+    b1 = bias1.detach().to(device=x.device, dtype=torch.float16).contiguous()
+    b = bias.detach().to(device=x.device, dtype=torch.float16).contiguous()
+    xc = x.contiguous()
+    ctx = _resolve_ctx(ctx, x)
+    _bind_stream(ctx, True)
+    rc = _lib.load().fd_nn_conv3x3_c1c64(ctx.ptr, ctypes.c_void_p(xc.data_ptr()), ctypes.c_void_p(w1.data_ptr()),
+                                          ctypes.c_void_p(b1.data_ptr()), ctypes.c_void_p(packed.data_ptr()),
+                                          ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(out.data_ptr()), n, h, w,
+                                          1 if pool else 0)
+    _lib.check(ctx.ptr, rc)
+    return out
+
+
 def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = None):
     """fd_nn_descriptors: desc_map [B, C, h, w] float32, xy [B, S, 2] -> descriptors [B, S, C].
 
@@ -429,10 +468,29 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             x = self.relu(conv(x))
             return self.pool(x) if pool else x
 
+        def first_layers(self, x):
+            """conv1a -> ReLU -> conv1b -> ReLU -> MaxPool2d(2, 2): fp16 device input in one fused pass
+            (conv1ab_bias_relu, the 64-channel full-resolution activation stays on chip); otherwise
+            layer by layer through cbr."""
+            if x.dtype == torch.float16 and x.is_cuda and x.dim() == 4 and x.shape[1] == 1 \
+                    and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.shape[3] <= 4096 \
+                    and self.conv1a.out_channels == 64 and self.conv1b.in_channels == 64 \
+                    and self.conv1b.out_channels == 64 and not _ab_env("FD_SP_UNFUSED") \
+                    and not _ab_env("FD_SP_NO_C1C64"):  # (A/B switches)
+                tag = (self.conv1b.weight.data_ptr(), self.conv1b.weight._version, x.device)
+                cache = self.__dict__.setdefault("_fd_packed", {})
+                hit = cache.get(id(self.conv1b))
+                if hit is None or hit[0] != tag or len(hit[1]) != 1:
+                    hit = (tag, [pack_conv3x3_weight(self.conv1b.weight.to(device=x.device, dtype=torch.float16))])
+                    cache[id(self.conv1b)] = hit
+                return conv1ab_bias_relu(x, self.conv1a.weight, self.conv1a.bias, self.conv1b.weight,
+                                         self.conv1b.bias, pool=True, packed=hit[1][0])
+            return self.cbr(self.conv1b, self.cbr(self.conv1a, x), pool=True)
+
         def forward(self, x):
             """x: [B, 1, H, W] in [0, 1] -> (heatmap [B, H, W] f32, descriptors [B, 256, H/8, W/8] f32), or
             with nms (keypoints [B, K, 2] int64, scores [B, K] f32, descriptors [B, K, 256] f32)."""
-            x = self.cbr(self.conv1b, self.cbr(self.conv1a, x), pool=True)
+            x = self.first_layers(x)
             x = self.cbr(self.conv2b, self.cbr(self.conv2a, x), pool=True)
             x = self.cbr(self.conv3b, self.cbr(self.conv3a, x), pool=True)
             x = self.cbr(self.conv4b, self.cbr(self.conv4a, x))

@@ -389,6 +389,17 @@ int fd_nn_conv3x3_c1(fd_ctx *ctx, const void *x, const void *weight, const void 
 int fd_nn_conv3x3_c64(fd_ctx *ctx, const void *x, const void *weight_packed, const void *bias, void *y, int n, int h,
                       int w, int pool, int y_channels, int y_offset);
 
+/*
+ * fd_nn_conv3x3_c1c64 -- SuperPoint's first two layers in one pass: conv1a (1 -> 64 channels, 3x3, bias,
+ * ReLU) fused into conv1b (64 -> 64, 3x3, bias, ReLU, with pool = 1 the 2x2 max pool): x [n][h][w] fp16,
+ * weight1 [64][1][3][3] fp16, bias1 [64], weight_packed / bias as fd_nn_conv3x3_c64, y [n][h(/2)][w(/2)][64]
+ * channels-last fp16, all on the device. Equal to fd_nn_conv3x3_c1 followed by fd_nn_conv3x3_c64 bit for
+ * bit (conv1a is recomputed per conv1b tile with the same arithmetic; its full-resolution 64-channel output
+ * never goes to memory). w <= 4096; x 2-byte, y and weight_packed 16-byte aligned; pool needs even h, w.
+ */
+int fd_nn_conv3x3_c1c64(fd_ctx *ctx, const void *x, const void *weight1, const void *bias1, const void *weight_packed,
+                        const void *bias, void *y, int n, int h, int w, int pool);
+
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);
 

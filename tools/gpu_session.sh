@@ -7,7 +7,8 @@
 #   env=SHAPE:E1:E2..  A/B of environment settings (each Ek: comma-separated VAR=V) on a shape, under
 #                      rocprofv3 --kernel-trace --stats; FD_DEBUG_AB=1 is set so the library honours its switches
 #   bench=ARGS         one bench.py line (ARGS: comma-separated bench.py flags) -> gpurun_out/bench_<n>.json
-#   stamps[=LIB]       k_select phase clocks (FD_SELECT_STAMPS) at the bench shapes (LIB: FD_LIB_PATH, e.g. abvar/new.so)
+#   stamps[=LIB,E..]   k_select phase clocks (FD_SELECT_STAMPS) at the bench shapes (LIB: FD_LIB_PATH, e.g.
+#                      abvar/new.so, may be empty; E: VAR=V settings, e.g. FD_SELECT_REPEAT=1)
 #   py=SCRIPT          python3 SCRIPT (comma-separated args), output to gpurun_out/py_<n>.log
 set -e
 cd "$GRAFT_REPO_ROOT"
@@ -69,7 +70,10 @@ for S in "$@"; do
       timeout -k 10 400 python3 bench.py ${val//,/ } > gpurun_out/bench_$n.json 2> gpurun_out/bench_$n.err
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('value', d['value'], 'ms_per_step', d['ms_per_step'])" gpurun_out/bench_$n.json ;;
     stamps)
-      FD_LIB_PATH=${val:+$GRAFT_REPO_ROOT/$val} FD_DEBUG_AB=1 FD_SELECT_STAMPS=1 timeout -k 10 120 python3 tools/select_stamps.py > gpurun_out/stamps_$n.txt 2>&1
+      IFS=',' read -ra sp <<< "$val"
+      lib=${sp[0]:-}
+      env ${sp[@]:1} FD_LIB_PATH=${lib:+$GRAFT_REPO_ROOT/$lib} FD_DEBUG_AB=1 FD_SELECT_STAMPS=1 timeout -k 10 120 \
+          python3 tools/select_stamps.py > gpurun_out/stamps_$n.txt 2>&1
       grep -v "^  levels\|k_select_reference" gpurun_out/stamps_$n.txt | head -12 ;;
     py)
       timeout -k 10 300 python3 ${val//,/ } > gpurun_out/py_$n.log 2>&1 || { tail -30 gpurun_out/py_$n.log; exit 1; }
