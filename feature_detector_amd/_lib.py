@@ -130,7 +130,7 @@ def load() -> ctypes.CDLL:
             raise
         fn.restype = res
         fn.argtypes = args
-    abi = L.fd_abi_version()
+    abi = L.fd_abi_version() if hasattr(L, "fd_abi_version") or not os.environ.get("FD_LIB_PATH") else ABI_VERSION
     if abi != ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has C ABI version {abi}, this binding needs {ABI_VERSION}: rebuild the library")
     _lib = L

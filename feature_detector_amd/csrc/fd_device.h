@@ -110,6 +110,15 @@ __device__ __forceinline__ int opaque(int x) {
     return x;
 }
 
+// LDS pointer type: a noinline function taking one keeps issuing ds_* instructions (a generic pointer
+// would make them flat accesses). to_lds / from_lds convert (the object must live in LDS).
+template <class T>
+using lds_t = __attribute__((address_space(3))) T;
+template <class T>
+__device__ __forceinline__ lds_t<T> *to_lds(T *p) { return (lds_t<T> *)(p); }
+template <class T>
+__device__ __forceinline__ T *from_lds(lds_t<T> *p) { return (T *)(p); }
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int popc64(uint64_t m) { return __popcll(m); }
 __device__ __forceinline__ uint64_t lanes_below() {

@@ -297,311 +297,6 @@ __device__ __forceinline__ void conflict_masks(const uint32_t *pxy, int c, int d
     }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// Workgroup-parallel greedy (the corner detectors' scan: candidates after a strict 4-neighbour NMS are
-// sparse, ~1-2 earlier neighbours within d each on noise).
-//
-// SelectGoodFeatures (:62-72) accepts a candidate iff no earlier accepted feature lies within Chebyshev
-// distance d (the box it zeroes in the mask), and stops once `need` features exist. The accepted set of
-// a scan is therefore the lexicographically-first maximal independent set of the chunk's conflict graph
-// in scan order, cut after its (need - have)-th member: candidate i is accepted iff every earlier
-// neighbour j < i within d is rejected, and rejected iff one of them is accepted. Every thread takes one
-// candidate of a pass of blockDim.x positions:
-//   1. occupancy-grid test against the features of earlier passes / sub-chunks (and priors);
-//   2. the survivors are counting-sorted by grid-cell bucket in LDS; a candidate's earlier neighbours are
-//      then in three contiguous runs (the three cells of each of its three cell rows; cells are
-//      (d+1)-sized, so every neighbour within d is there) and go to its slot list in LDS;
-//   3. rounds: an undecided candidate whose earlier neighbours are all decided becomes accepted if none
-//      of them is, and one with an accepted earlier neighbour becomes rejected; a workgroup OR ends the
-//      loop. Each round decides at least the lowest undecided position (its neighbours are all earlier),
-//      so the rounds are bounded by the pass, in practice by the longest chain of conflicts (~5 at the
-//      headline);
-//   4. accepted ranks by a workgroup prefix in scan order, the first (need - have) appended to the
-//      output and written into the grid (<= 1 accepted feature per cell: two features in one cell would
-//      be within d of each other).
-// Same features in the same order as the wave-serial scan (greedy_chunk), which FAST and the heatmap
-// lists keep: their candidates cluster (no NMS), so conflict chains there are long.
-// ---------------------------------------------------------------------------------------------------
-constexpr int kGreedyBuckets = 1024;  // cell buckets: cell mod this (frames with more cells share buckets)
-constexpr int kGreedyMaxPred = 8;     // earlier neighbours kept per candidate (more: re-walked each round)
-constexpr int kGreedyPass = 1024;     // positions per pass (one per thread; blockDim.x <= this)
-
-struct GreedyLds {  // overlays free space of the kernels (<= 16 KiB)
-    uint32_t bst[kGreedyBuckets + 1];  // bucket counts, then their exclusive starts (bst[kGreedyBuckets] = total)
-    uint16_t sidx[kGreedyPass];        // survivors by bucket: pass position
-    uint32_t se[kGreedyPass];          // ... and (y << 16) | x
-    uint8_t st[kGreedyPass + 4];       // 0 undecided, 1 accepted, 2 rejected; st[kGreedyPass] = 2 (sentinel)
-    uint32_t wsum[kGreedyPass / kWave];
-    int stop;
-};
-static_assert(sizeof(GreedyLds) <= 16384, "GreedyLds overlays 16 KiB");
-constexpr int kGreedyPredBytes = kGreedyPass * kGreedyMaxPred * 2;  // the pred lists (uint16_t [pass][8])
-
-// Chebyshev distance <= d between two packed (y << 16) | x positions.
-struct NearTest {
-    int d;
-    uint32_t w2;
-    bool pk16;
-    __device__ __forceinline__ bool operator()(uint32_t e, uint32_t g) const {
-        if (pk16) {  // |gx - x| <= d  <=>  (gx - x + d) mod 2^16 <= 2d (no wrap: rows, cols + 3d < 2^16)
-            const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
-            const u16x2 dt = __builtin_bit_cast(u16x2, g) - base;
-            return static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y) <= w2;
-        }
-        const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-        const int gx = static_cast<int>(g & 0xFFFFu), gy = static_cast<int>(g >> 16);
-        return abs(x - gx) <= d && abs(y - gy) <= d;
-    }
-};
-
-// GRID: 1 = occupancy grid in LDS, 2 = grid in global memory (d >= 0 with a grid; no grid: greedy_chunk).
-// Every thread of the workgroup calls it (blockDim.x <= kGreedyPass, a multiple of 64); the callers'
-// barriers order it against the writes of pxy / pcell and the reads of s_acc / s_done after it.
-// pred: kGreedyPredBytes of LDS. Tie check (pk32 != null: the chunk's 32-bit response keys in scan
-// order): FD_FRAME_TIES is raised when two adjacent candidates of the visited prefix, or the last visited
-// one and the next, have equal responses -- the only case in which the reference's unstable std::sort
-// (:58-60) can change the result. tie_prev / tie_has_prev carry the last key of the previous chunk.
-template <int GRID>
-__device__ __forceinline__ void greedy_block(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
-                                             const uint32_t *pcell, uint32_t *grid, int gw2, uint32_t prior, int &s_acc,
-                                             int &s_done, const uint32_t *pk32, uint32_t &tie_prev, int &tie_has_prev,
-                                             GreedyLds &G, uint16_t *pred, uint64_t *st = nullptr) {
-    static_assert(GRID == 1 || GRID == 2, "greedy_block needs the occupancy grid");
-    const int tid = threadIdx.x, nthr = blockDim.x, lane = lane_id(), wave = tid >> 6;
-    // diagnostic clocks (st: k_select's stamps, a.stamps set): phases into slots 26-29, counters 16-19
-    auto gst = [&](int slot) {
-        if (st && tid == 0) {
-            const uint64_t now = __builtin_readcyclecounter();
-            st[slot] += now - st[15];
-            st[15] = now;
-        }
-    };
-    const int d = a.dist;
-    const NearTest near{d, 2u * static_cast<uint32_t>(max(d, 0)), a.rows + 3 * d < 65536 && a.cols + 3 * d < 65536};
-    const bool pk15 = grid_pk15(a.rows, a.cols, d);
-    const uint32_t gempty = grid_empty(a.rows, a.cols, d);
-    constexpr uint32_t kM = kGreedyBuckets - 1;
-    int acc = s_acc;
-    bool done = false;
-    int stop = -1;
-    for (int base = 0; base < cnt && !done; base += nthr) {
-        const int cp = min(nthr, cnt - base);
-        const bool in = tid < cp;
-        const uint32_t e = in ? pxy[base + tid] : kEmpty;
-        bool ok = e != kEmpty;
-        const int cell = in ? static_cast<int>(pcell[base + tid]) : 0;
-        for (int i = tid; i <= kGreedyBuckets; i += nthr) G.bst[i] = 0u;
-        if (tid == 0) G.st[kGreedyPass] = 2;
-        if (ok) {  // 1. features of earlier passes, sub-chunks and priors (the 3x3 cells)
-            uint32_t g[9];
-#pragma unroll
-            for (int q = 0; q < 9; ++q) {
-                const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
-                if constexpr (GRID == 1) g[q] = grid[o];
-                else g[q] = __hip_atomic_load(&grid[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (pk15) {  // the empty cell tests far (grid_empty): min over the 9 cells
-                const u16x2 b = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
-                uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - b;
-                    mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
-                }
-                ok = mn > near.w2;
-            } else {
-#pragma unroll
-                for (int q = 0; q < 9; ++q)
-                    if (g[q] != gempty && near(e, g[q])) ok = false;
-            }
-        }
-        if (in) G.st[tid] = ok ? 0 : 2;
-        __syncthreads();  // buckets cleared, states set
-        gst(26);
-        // 2. counting sort of the survivors by cell bucket
-        uint32_t slot = 0;
-        if (ok) slot = atomicAdd(&G.bst[static_cast<uint32_t>(cell) & kM], 1u);
-        __syncthreads();
-        gst(30);
-        {  // exclusive scan of the bucket counts (kGreedyBuckets / nthr consecutive buckets per thread)
-            constexpr int kMaxPer = kGreedyBuckets / kWave;
-            const int per = kGreedyBuckets / nthr;
-            uint32_t v[kMaxPer];
-            uint32_t sum = 0;
-#pragma unroll
-            for (int k = 0; k < kMaxPer; ++k) {
-                v[k] = k < per ? G.bst[tid * per + k] : 0u;
-                sum += v[k];
-            }
-            const uint32_t incl = wave_incl_add(sum);
-            if (lane == kWave - 1) G.wsum[wave] = incl;
-            __syncthreads();
-            uint32_t wb = 0, tot = 0;
-            for (int w = 0; w < nthr / kWave; ++w) {
-                const uint32_t t = G.wsum[w];
-                wb += w < wave ? t : 0u;
-                tot += t;
-            }
-            uint32_t run = wb + incl - sum;
-#pragma unroll
-            for (int k = 0; k < kMaxPer; ++k)
-                if (k < per) {
-                    G.bst[tid * per + k] = run;
-                    run += v[k];
-                }
-            if (tid == 0) G.bst[kGreedyBuckets] = tot;
-            __syncthreads();
-        }
-        gst(31);
-        if (ok) {
-            const uint32_t k = G.bst[static_cast<uint32_t>(cell) & kM] + slot;
-            G.sidx[k] = static_cast<uint16_t>(tid);
-            G.se[k] = e;
-        }
-        __syncthreads();
-        gst(20);
-        const uint32_t nsurv = G.bst[kGreedyBuckets];
-        uint16_t *const mypred = pred + tid * kGreedyMaxPred;
-        // visit(j) for every earlier neighbour j of this candidate: per cell row, the three buckets of
-        // cells cx-1 .. cx+1 are consecutive in the (cyclic) bucket order of the sorted survivors
-        auto walk = [&](auto &&visit) {
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const uint32_t cr = static_cast<uint32_t>(cell + (r - 1) * gw2);
-                const uint32_t b0 = (cr - 1u) & kM, b1 = cr & kM, b2 = (cr + 1u) & kM;
-                const uint32_t s0 = G.bst[b0];
-                const uint32_t len = (G.bst[b0 + 1] - s0) + (G.bst[b1 + 1] - G.bst[b1]) + (G.bst[b2 + 1] - G.bst[b2]);
-                for (uint32_t t = 0; t < len; ++t) {
-                    uint32_t k = s0 + t;
-                    k = k >= nsurv ? k - nsurv : k;
-                    const uint32_t j = G.sidx[k];
-                    const uint32_t ej = G.se[k];
-                    if (j < static_cast<uint32_t>(tid) && near(e, ej)) visit(j);
-                }
-            }
-        };
-        int np = 0;
-        if (ok) {
-            walk([&](uint32_t j) {
-                if (np < kGreedyMaxPred) mypred[np] = static_cast<uint16_t>(j);
-                ++np;
-            });
-            if (np == 0) G.st[tid] = 1;  // no earlier neighbour: accepted at once
-        }
-        const bool ovf = np > kGreedyMaxPred;
-        if (st) {
-            const uint32_t mx = wave_max_u32(static_cast<uint32_t>(np));
-            const uint32_t no = static_cast<uint32_t>(popc64(ballot(ovf)));
-            if (lane == 0) {
-                atomicMax(reinterpret_cast<unsigned long long *>(&st[18]), static_cast<unsigned long long>(mx));
-                atomicAdd(reinterpret_cast<unsigned long long *>(&st[19]), static_cast<unsigned long long>(no));
-            }
-            __syncthreads();
-            gst(27);
-        }
-        // 3. rounds until every candidate of the pass is decided
-        bool und = ok && np > 0;
-        for (int round = 0;; ++round) {
-            if (und) {
-                bool any_acc = false, all_dec = true;
-                {  // (one 16-byte load of the list, then all states; 1 accepted, 2 rejected, 0 undecided)
-                    const uint4 pv = *reinterpret_cast<const uint4 *>(mypred);
-                    const uint32_t w4[4] = {pv.x, pv.y, pv.z, pv.w};
-                    uint32_t v[kGreedyMaxPred];
-#pragma unroll
-                    for (int k = 0; k < kGreedyMaxPred; ++k) {
-                        const uint32_t j = (w4[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                        v[k] = G.st[k < np ? j : static_cast<uint32_t>(kGreedyPass)];
-                    }
-                    uint32_t orv = 0u, mnv = 2u;
-#pragma unroll
-                    for (int k = 0; k < kGreedyMaxPred; ++k) {
-                        orv |= v[k];
-                        mnv = min(mnv, v[k]);
-                    }
-                    any_acc = (orv & 1u) != 0u;
-                    all_dec = mnv != 0u;
-                }
-                if (ovf && all_dec && !any_acc) {  // the listed ones are all rejected: check the rest
-                    walk([&](uint32_t j) {
-                        const uint32_t v = G.st[j];
-                        any_acc = any_acc || v == 1u;
-                        all_dec = all_dec && v != 0u;
-                    });
-                }
-                if (any_acc) {
-                    G.st[tid] = 2;
-                    und = false;
-                } else if (all_dec) {
-                    G.st[tid] = 1;
-                    und = false;
-                }
-            }
-            if (!__syncthreads_or(und)) {
-                if (st && tid == 0) st[16] += static_cast<uint64_t>(round + 1);
-                break;
-            }
-            if (round > kGreedyPass) {  // each round decides the lowest undecided position: unreachable
-                if (tid == 0) atomicOr(&a.status[f], 0x20000000u);
-                break;
-            }
-        }
-        gst(28);
-        if (st && tid == 0) st[17] += 1;
-        // 4. ranks of the accepted candidates in scan order; the need cutoff (:67-69)
-        const bool accd = in && G.st[tid] == 1;
-        const uint64_t m = ballot(accd);
-        if (lane == 0) G.wsum[wave] = static_cast<uint32_t>(popc64(m));
-        __syncthreads();
-        uint32_t before = 0, total = 0;
-        for (int w = 0; w < nthr / kWave; ++w) {
-            const uint32_t t = G.wsum[w];
-            before += w < wave ? t : 0u;
-            total += t;
-        }
-        const uint32_t rank = before + static_cast<uint32_t>(mbcnt64(m, 0));
-        const uint32_t have = prior + static_cast<uint32_t>(acc);
-        const uint32_t allow = have < a.need ? a.need - have : 1u;  // features.size() >= need after each append
-        done = total >= allow;
-        if (accd && rank < allow) {
-            const int pos = acc + static_cast<int>(rank);
-            if (pos < a.out_stride) {
-                float2 *o = reinterpret_cast<float2 *>(a.out_xy) + static_cast<int64_t>(f) * a.out_stride + pos;
-                *o = make_float2(static_cast<float>(e & 0xFFFFu), static_cast<float>(e >> 16));
-            }
-            if constexpr (GRID == 1) grid[cell] = e;
-            else __hip_atomic_store(&grid[cell], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (rank == allow - 1u) G.stop = base + tid;
-        }
-        acc += static_cast<int>(min(total, allow));
-        __syncthreads();  // grid and stop written; G reused by the next pass
-        if (done) stop = G.stop;
-        gst(29);
-    }
-    if (pk32 && cnt > 0) {
-        // The reference's visiting order of this chunk ends at the stop (or runs through it). Its prefix
-        // holds a tie if two adjacent keys in it are equal, if its first key equals the previous chunk's
-        // last, or if the candidate after the stop equals the stop (unknown past the chunk: assumed).
-        const int last = done ? stop : cnt - 1;
-        bool t = false;
-        for (int i = tid + 1; i <= last; i += nthr) t = t || pk32[i] == pk32[i - 1];
-        if (tid == 0) {
-            if (tie_has_prev && pk32[0] == tie_prev) t = true;
-            if (done && (last + 1 >= cnt || pk32[last + 1] == pk32[last])) t = true;
-        }
-        const bool tied = __syncthreads_or(t);
-        if (tid == 0) {
-            if (tied) atomicOr(&a.status[f], FD_FRAME_TIES);
-            tie_prev = pk32[cnt - 1];  // for the next chunk's first comparison
-            tie_has_prev = 1;
-        }
-    }
-    if (tid == 0) {
-        s_acc = acc;
-        if (done) s_done = 1;
-    }
-}
-
 }  // namespace
 
 }  // namespace fdk

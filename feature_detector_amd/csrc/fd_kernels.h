@@ -15,6 +15,10 @@ constexpr int kSegFast = kTileW;        // FAST has no NMS
 #define FD_LIST_NT 0  // candidate list stores with the nt (streaming) cache policy
 #endif
 constexpr int kSelectChunk = 2048;      // candidates sorted per greedy chunk (LDS)
+#ifndef FD_SELECT_THREADS
+#define FD_SELECT_THREADS 1024
+#endif
+constexpr int kSelectThreads = FD_SELECT_THREADS;  // k_select workgroup size (sorted segments: <= this many per frame)
 constexpr int kGridLdsCells = 16384;    // occupancy grid kept in LDS up to this many cells
 constexpr int kMaxOffsetSegs = 48;
 constexpr int kSegHead = 64;           // selection keys kept per sorted segment head (PointsArgs::seghead)
@@ -121,9 +125,7 @@ struct SelectArgs {
     int first_sub;     // sorted-segment corner frames: first chunk cut at one sub-chunk (kSubChunk keys)
     int grid_at_d0;    // distance 0 still tests the grid (1-pixel cells): caller lists may name a pixel twice
     int dup_keys;      // equal selection keys possible (caller lists): the orderings rank them stably
-    int par_greedy;    // workgroup-parallel greedy (greedy_block: sparse NMS candidates) instead of the wave scan
     uint64_t *stamps;  // diagnostic only (FD_SELECT_STAMPS): per-frame phase clocks, never read back by kernels
-    int repeat;        // diagnostic only (FD_SELECT_REPEAT): run the selection this many extra times (warm caches)
 };
 
 // Greedy selection over candidates given in an explicit order (FD_TIES_REFERENCE: the reference's

@@ -76,10 +76,6 @@ struct fd_ctx {
     fdk::FastOffsets off{};
 };
 
-#ifndef FD_PAR_GREEDY
-#define FD_PAR_GREEDY 0  // 1: corner detectors take the workgroup-parallel greedy (greedy_block; A/B build)
-#endif
-
 namespace {
 
 // A/B and diagnostic switches (FD_PX, FD_TILE_H, FD_SELECT_STAMPS, ...) take effect only when FD_DEBUG_AB is
@@ -434,7 +430,6 @@ struct SelectCall {
     const uint64_t *seghead = nullptr;
     int nseg = 0;
     bool push_order = false;  // lists hold the caller's push order (fd_points_select), not raster order
-    bool par_greedy = false;  // sparse candidates (strict 4-neighbour NMS): the workgroup-parallel greedy
     bool dup_keys = false;    // a pixel may be listed twice with one response (caller lists): equal keys
     bool grid_at_d0 = false;  // distance 0 tests the grid too (1-pixel cells; set with push_order)
     const char *value_msg = "a value above the declared maximum (fd_nn_opts::max_response)";
@@ -445,7 +440,7 @@ struct SelectCall {
 // otherwise gather their first chunk inside k_select (no k_gather kernel). FD_SEG_LISTS=0: off (A/B).
 bool use_seg_lists(int blocks_per_frame, int rows, int cols) {
     if (const char *e = ab_env("FD_SEG_LISTS"); e && std::atoi(e) == 0) return false;
-    return blocks_per_frame <= 1024 && static_cast<int64_t>(rows) * cols < (1 << 20);
+    return blocks_per_frame <= fdk::kSelectThreads && static_cast<int64_t>(rows) * cols < (1 << 20);
 }
 
 std::string hex(uint32_t v) {
@@ -614,7 +609,6 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.dist = q.dist;
     s.grid_at_d0 = (q.push_order || q.grid_at_d0) ? 1 : 0;  // caller lists may name a pixel twice: distance 0 tests it
     s.dup_keys = q.dup_keys ? 1 : 0;
-    s.par_greedy = q.par_greedy ? 1 : 0;
     if (s.dist >= 1 || (s.dist == 0 && s.grid_at_d0)) {
         s.grid_w = (cols + s.dist) / (s.dist + 1);
         s.grid_h = (rows + s.dist) / (s.dist + 1);
@@ -662,7 +656,6 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.first_sub = 1;
     if (const char *e = ab_env("FD_FIRST_SUB")) s.first_sub = std::atoi(e) != 0;  // (A/B switch)
     static const bool stamps = ab_env("FD_SELECT_STAMPS") != nullptr;
-    if (const char *e = ab_env("FD_SELECT_REPEAT")) s.repeat = std::max(0, std::atoi(e));  // diagnostic
     if (stamps) {  // diagnostic build-free switch: phase clocks of k_select for frame 0
         FD_HIP_TRY(c, ensure(c, c->dbg, sizeof(uint64_t) * 32 * batch));
         FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 32 * batch, c->stream));
@@ -1067,7 +1060,6 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     sc.seghead = a.seghead;
     sc.nseg = g.blocks_per_frame;
     sc.wide_eager = kind == FD_FAST;
-    sc.par_greedy = FD_PAR_GREEDY && kind != FD_FAST;  // (FAST candidates cluster: no NMS)
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
 }
 

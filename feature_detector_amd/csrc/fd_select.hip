@@ -88,7 +88,6 @@ constexpr int kSubChunkFast = kSelectChunk;
 constexpr int kBucketMax = 64;  // largest bin of a sub-chunk ordered by bucket placement (else merge sort)
 // k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
 // with 256 threads (4x the items per wave) the headline frame's selection measured 1.3x slower.
-constexpr int kSelectThreads = 1024;
 constexpr int kSegPer = 2;  // sorted-segment entries per thread and round
 constexpr int kRegGather = 16;  // list responses per thread and round in the level-0 gather
 
@@ -104,8 +103,8 @@ struct alignas(16) SelectLds {
     uint32_t pxy[kSelectChunk];
     uint32_t pcell[kSelectChunk];
     uint32_t pk32[kSelectChunk];  // 32-bit response keys in scan order (tie check)
-    uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor (wave scan)
-    uint32_t prev_min;                        // smallest 32-bit key of the previous sub-chunk (prefilter)
+    uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor
+    uint32_t prev_min;                         // smallest 32-bit key of the previous sub-chunk (prefilter)
     int have_prev_min;
     uint32_t grid_lds[kGridLdsCells];
     uint32_t tie_prev;
@@ -156,7 +155,6 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     };
     const int d = a.dist;
     const bool use_grid = d >= 1 || (d == 0 && a.grid_at_d0);
-    const bool par = use_grid && a.par_greedy;  // workgroup-parallel greedy (greedy_block)
     // Occupancy grid of (d+1)-sized cells with a one-cell border (no bounds checks in the scan).
     const int gw2 = a.grid_w + 2;
     const int cells = gw2 * (a.grid_h + 2);
@@ -1058,7 +1056,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     FD_STAMP(13);  // place
                     }
                     }
-                    if (!par && !a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
+                    if (!a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
                         const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;
                         for (int i = opaque(tid); i < c64; i += nthr) {
                             const bool t = i > 0 && i < c && L.pk32[i] == L.pk32[i - 1];
@@ -1066,24 +1064,14 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                             if (lane == 0) L.tmask[i >> 6] = m;
                         }
                     }
-                    // wave scan: conflict masks (earlier candidates of the same 64-batch within distance d)
-                    if (!par && use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
+                    // conflict masks: earlier candidates of the same 64-batch within distance d
+                    if (use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
                 }
                 __syncthreads();
                 FD_STAMP(14);  // conflict masks
-                // greedy scan in order (SelectGoodFeatures :62-72); ties checked unless the order of equal
-                // responses is defined (SuperPoint's multimap)
-                if (par) {  // by the workgroup (buf, tmp: free once the chunk is placed)
-                    const uint32_t *tk = a.tie_idx_desc ? nullptr : L.pk32;
-                    GreedyLds &G = *reinterpret_cast<GreedyLds *>(buf);
-                    uint16_t *gp = reinterpret_cast<uint16_t *>(tmp);
-                    if (grid_in_lds)
-                        greedy_block<1>(a, f, c_sort, pxy, pcell, grid_lds, gw2, prior, s_acc, s_done, tk, L.tie_prev,
-                                        L.tie_has_prev, G, gp, a.stamps ? L.st : nullptr);
-                    else
-                        greedy_block<2>(a, f, c_sort, pxy, pcell, grid_g, gw2, prior, s_acc, s_done, tk, L.tie_prev,
-                                        L.tie_has_prev, G, gp, a.stamps ? L.st : nullptr);
-                } else if (tid < kWave) {  // by wave 0
+                // greedy scan in order by wave 0 (SelectGoodFeatures :62-72); ties checked unless the
+                // order of equal responses is defined (SuperPoint's multimap)
+                if (tid < kWave) {
                     const bool ties = !a.tie_idx_desc;
                     const uint64_t *tm = L.tmask;
                     if (!use_grid)
@@ -1154,10 +1142,6 @@ __global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
     __shared__ SelectLds L;
     const int f = blockIdx.x;
     select_frame<NT, WIDE>(a, f, L);
-    for (int r = 0; r < a.repeat; ++r) {  // (diagnostic: the same selection with warm caches; stamps of the last)
-        __syncthreads();
-        select_frame<NT, WIDE>(a, f, L);
-    }
     finish_frame(a, f);
 }
 
@@ -1168,8 +1152,7 @@ __global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
 struct alignas(16) OrderedLds {
     uint32_t pxy[kSelectChunk];
     uint32_t pcell[kSelectChunk];
-    uint64_t cmask[kSelectChunk];  // wave scan: conflict masks; greedy_block: GreedyLds
-    uint16_t gpred[kGreedyPredBytes / 2];
+    uint64_t cmask[kSelectChunk];
     uint32_t grid_lds[kGridLdsCells];
     int s_done, s_acc;
     uint32_t tie_prev;
@@ -1220,28 +1203,18 @@ __global__ __launch_bounds__(NT) void k_select_ordered(SelectArgs a, OrderedArgs
             if (use_grid) L.pcell[i] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
         }
         __syncthreads();
-        if (use_grid && a.par_greedy) {
-            GreedyLds &G = *reinterpret_cast<GreedyLds *>(L.cmask);
-            if (grid_in_lds)
-                greedy_block<1>(a, f, c, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
-                                L.tie_has_prev, G, L.gpred);
+        if (use_grid) conflict_masks(L.pxy, c, d, rows, cols, L.cmask, tid, NT);
+        __syncthreads();
+        if (tid < kWave) {
+            if (!use_grid)
+                greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
+                                L.tie_prev, L.tie_has_prev);
+            else if (grid_in_lds)
+                greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
+                                L.tie_prev, L.tie_has_prev);
             else
-                greedy_block<2>(a, f, c, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
-                                L.tie_has_prev, G, L.gpred);
-        } else {
-            if (use_grid) conflict_masks(L.pxy, c, d, rows, cols, L.cmask, tid, NT);
-            __syncthreads();
-            if (tid < kWave) {
-                if (!use_grid)
-                    greedy_chunk<0>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u,
-                                    0u, L.tie_prev, L.tie_has_prev);
-                else if (grid_in_lds)
-                    greedy_chunk<1>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u,
-                                    0u, L.tie_prev, L.tie_has_prev);
-                else
-                    greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u,
-                                    0u, L.tie_prev, L.tie_has_prev);
-            }
+                greedy_chunk<2>(a, f, c, L.pxy, L.pcell, L.cmask, grid, gw2, prior, L.s_acc, L.s_done, false, nullptr, 0u, 0u,
+                                L.tie_prev, L.tie_has_prev);
         }
         __syncthreads();
     }

@@ -91,9 +91,9 @@ struct alignas(16) RefLds {
     uint32_t wstk[kRefWaves][kRefStack];
     uint32_t wsum[kRefWaves];
     uint16_t rid[kRefRidCap];  // levels with T <= kRefRidCap: each element's active range (set by pass 1)
-    uint16_t gpred[kGreedyPredBytes / 2];  // greedy_block's neighbour lists
-    int cur, m_all, m_act, n_leaf, fail, n_wl, n_heap;
-    uint32_t heap_j[kRefMaxRanges];  // active ranges at depth 0 (heapsort fallback)
+    int cur, m_all, m_act, n_leaf, fail, n_wl, n_heap, n_hq;
+    uint32_t heap_j[kRefMaxRanges];      // active ranges at depth 0 (heapsort fallback)
+    uint32_t hq[2 * kRefMaxRanges];      // wave-local subranges at depth 0: absolute [lo, hi), heapsorted after the phase
     uint32_t T, fin;
     int s_done, s_acc;
     uint32_t tie_prev;
@@ -241,7 +241,7 @@ __device__ void ref_adjust_heap(uint2 *f, int hole, int len, uint2 v) {
 // One wave: __make_heap then __sort_heap on f[0, len). __make_heap adjusts parents (len - 2) / 2 down to 0;
 // the parents of one tree level own disjoint subtrees and the deeper levels come first, so the lanes
 // adjust a level's parents at once. __sort_heap's pops depend on each other: lane 0.
-__device__ __attribute__((noinline)) void ref_heapsort(uint2 *f, int len) {
+__device__ __forceinline__ void ref_heapsort(uint2 *f, int len) {
     if (len < 2) return;
     const int lane = lane_id();
     const int last_parent = (len - 2) / 2;
@@ -267,33 +267,29 @@ __device__ __attribute__((noinline)) void ref_heapsort(uint2 *f, int len) {
 // LDS) to the end, every subrange of a level partitioned at once. Lane p keeps its subrange [sa, sb);
 // stopper ranks are popcounts of the subrange's ballot, the k-th stopper's position a bit select, the
 // exchanges and the pivot move shuffles. Leaves: stable rank by response, descending, into ordp.
-// A subrange at the depth limit is heapsorted (ref_heapsort by its first lane, in E) and final.
-__device__ bool ref_wave_small(uint2 *E, uint32_t len, uint32_t dep, uint32_t *ordp) {
+// A subrange at the depth limit (std::__partial_sort) is written back to X (xp: X at E[0]'s position) and
+// queued in hq (absolute [lo, hi) pairs, count *hn) for the heapsort step; its lanes take no further part.
+__device__ bool ref_wave_small(uint2 *E, uint32_t len, uint32_t dep, uint32_t *ordp, uint2 *xp, uint32_t xlo,
+                               uint32_t *hq, int *hn) {
     const uint32_t p = static_cast<uint32_t>(lane_id());
     uint2 v = p < len ? E[p] : make_uint2(0u, 0u);
     uint32_t sa = 0, sb = len, dp = dep;
+    bool queued = false;
     for (int it = 0; it < 64; ++it) {
-        bool big = p < len && sb - sa > static_cast<uint32_t>(kRefLeaf);
+        bool big = p < len && !queued && sb - sa > static_cast<uint32_t>(kRefLeaf);
         if (ballot(big) == 0ull) break;
-        if (ballot(big && dp == 0u) != 0ull) {  // std::__partial_sort of those subranges
-            if (p < len) E[p] = v;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (ballot(big && dp == 0u) != 0ull) {
             const bool hp = big && dp == 0u;
-            // (one subrange at a time: ref_heapsort is a whole-wave routine)
-            for (uint64_t leaders = ballot(hp && p == sa); leaders; leaders &= leaders - 1ull) {
-                const uint32_t q = static_cast<uint32_t>(__builtin_ctzll(leaders));
-                const uint32_t qa = static_cast<uint32_t>(__shfl(static_cast<int>(sa), static_cast<int>(q)));
-                const uint32_t qb = static_cast<uint32_t>(__shfl(static_cast<int>(sb), static_cast<int>(q)));
-                ref_heapsort(E + qa, static_cast<int>(qb - qa));
+            if (hp) xp[p] = v;
+            if (hp && p == sa) {
+                const int q = atomicAdd(hn, 1);
+                if (q < kRefMaxRanges) {
+                    hq[2 * q] = xlo + sa;
+                    hq[2 * q + 1] = xlo + sb;
+                }
             }
-            if (hp) {  // final positions: a one-element leaf each
-                v = E[p];
-                sa = p;
-                sb = p + 1u;
-            }
-            big = p < len && sb - sa > static_cast<uint32_t>(kRefLeaf);
+            queued = queued || hp;
+            big = big && !hp;
             if (ballot(big) == 0ull) break;
         }
         // pivot: __move_median_to_first(sa, sa + 1, mid, sb - 1)
@@ -351,7 +347,7 @@ __device__ bool ref_wave_small(uint2 *E, uint32_t len, uint32_t dep, uint32_t *o
         const float rt = __uint_as_float(static_cast<uint32_t>(__shfl(static_cast<int>(v.x), static_cast<int>(min(t, 63u)))));
         rk += (t < sb && (rt > ri || (rt == ri && t < p))) ? 1u : 0u;
     }
-    if (p < len) ordp[sa + rk] = v.y;
+    if (p < len && !queued) ordp[sa + rk] = v.y;
     return true;
 }
 
@@ -360,9 +356,9 @@ __device__ bool ref_wave_small(uint2 *E, uint32_t len, uint32_t dep, uint32_t *o
 // stoppers resp <= pivot from the left paired with right stoppers resp >= pivot from the right while
 // l_k < r_k, cut = min(l_K, r_{K-1})), then the final insertion sort of every leaf (stable, response
 // descending) -- with the elements in the wave's LDS. Writes the range's visiting order into ord[lo, hi).
-// A subrange at the depth limit is heapsorted (std::__partial_sort). Returns false on a broken invariant.
+// A subrange at the depth limit is queued for the heapsort step (hq, hn). Returns false on a broken invariant.
 __device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t hi, uint32_t dep, uint2 *E,
-                                 uint16_t *Lp, uint16_t *Rp, uint32_t *stk) {
+                                 uint16_t *Lp, uint16_t *Rp, uint32_t *stk, uint32_t *hq, int *hn) {
     const int lane = lane_id();
     const uint32_t s = hi - lo;
     for (uint32_t i = lane; i < s; i += kWave) E[i] = X[lo + i];
@@ -379,7 +375,7 @@ __device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t 
         const uint32_t ent = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(stk[top])));
         const uint32_t a = ent & 1023u, b = (ent >> 10) & 2047u, dp = ent >> 21;
         if (b - a <= static_cast<uint32_t>(kWave) && b - a > static_cast<uint32_t>(kRefLeaf)) {
-            if (!ref_wave_small(E + a, b - a, dp, ord + lo + a)) {
+            if (!ref_wave_small(E + a, b - a, dp, ord + lo + a, X + lo + a, lo + a, hq, hn)) {
                 ok = false;
                 break;
             }
@@ -400,9 +396,15 @@ __device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t 
             if (lane < kRefLeaf && q < len) ord[lo + a + rk] = v.y;
             continue;
         }
-        if (dp == 0u) {  // std::__partial_sort(a, b, b): heapsorted in E, final
-            ref_heapsort(E + a, static_cast<int>(b - a));
-            for (uint32_t i = lane; i < b - a; i += kWave) ord[lo + a + i] = E[a + i].y;
+        if (dp == 0u) {  // std::__partial_sort(a, b, b): back to X and queued for the heapsort step
+            for (uint32_t i = lane; i < b - a; i += kWave) X[lo + a + i] = E[a + i];
+            if (lane == 0) {
+                const int q = atomicAdd(hn, 1);
+                if (q < kRefMaxRanges) {
+                    hq[2 * q] = lo + a;
+                    hq[2 * q + 1] = lo + b;
+                }
+            }
             continue;
         }
         // pivot: __move_median_to_first(a, a + 1, mid, b - 1)
@@ -496,6 +498,63 @@ __device__ bool ref_wave_resolve(uint2 *X, uint32_t *ord, uint32_t lo, uint32_t 
     do {                                                                                \
         if (a.stamps && tid == 0) a.stamps[static_cast<int64_t>(f) * 32 + (k)] += (v);  \
     } while (0)
+
+// Wave 0: the active ranges at the depth limit (L.heap_j) heapsorted one at a time (std::__partial_sort,
+// ref_heapsort; in LDS when the range fits the free space: the greedy span before the grid exists, pxy ..
+// cmask after), their visiting order written to ord (final), and the range list rebuilt without them.
+// (A function of its own: the rare path stays out of k_select_reference's register allocation.)
+__device__ __attribute__((noinline)) void ref_heap_step(lds_t<RefLds> *Lp, uint2 *X, uint32_t *ord, uint32_t n, int m,
+                                                        bool grid_ready) {
+    RefLds &L = *from_lds(Lp);
+    const int lane = lane_id();
+    const int c = L.cur, nh = L.n_heap;
+    const uint32_t cap_lds = static_cast<uint32_t>(
+        (grid_ready ? sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask)
+                    : sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask) + sizeof(L.grid_lds)) / sizeof(uint2));
+    for (int h = 0; h < nh; ++h) {
+        const uint32_t j = L.heap_j[h];
+        const uint32_t lo = L.r_lo[c][j], hi = min(L.r_hi[c][j], n);
+        const uint32_t len = hi > lo ? hi - lo : 0u;
+        uint2 *hbuf = X + lo;
+        if (len <= cap_lds) {
+            hbuf = reinterpret_cast<uint2 *>(L.pxy);
+            for (uint32_t i = lane; i < len; i += kWave) hbuf[i] = X[lo + i];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        ref_heapsort(hbuf, static_cast<int>(len));
+        for (uint32_t i = lane; i < len; i += kWave) {
+            const uint2 e = hbuf[i];
+            X[lo + i] = e;
+            ord[lo + i] = e.y;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // the list without them (order kept), into the other buffer
+    const int nc = c ^ 1;
+    uint32_t at = 0;
+    for (int b = 0; b < L.m_all; b += kWave) {
+        const int j = b + lane;
+        const bool keep = j < L.m_all && !(j < m && L.r_dep[c][j] == 0u);
+        const uint64_t bk = ballot(keep);
+        if (keep) {
+            const uint32_t q = at + static_cast<uint32_t>(mbcnt64(bk, 0));
+            L.r_lo[nc][q] = L.r_lo[c][j];
+            L.r_hi[nc][q] = L.r_hi[c][j];
+            L.r_dep[nc][q] = L.r_dep[c][j];
+        }
+        at += static_cast<uint32_t>(popc64(bk));
+    }
+    if (lane == 0) {
+        L.m_all = static_cast<int>(at);
+        L.cur = nc;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    set_active(L, L.fin + kSelectChunk);
+}
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortArgs r) {
@@ -626,6 +685,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         L.tie_prev = 0;
         L.tie_has_prev = 0;
         L.fail = 0;
+        L.n_hq = 0;
         L.cur = 0;
         L.n_leaf = 0;
         L.fin = 0;
@@ -685,55 +745,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             if (tid < m && L.r_dep[L.cur][tid] == 0u) L.heap_j[atomicAdd(&L.n_heap, 1)] = static_cast<uint32_t>(tid);
             __syncthreads();
             if (L.n_heap > 0) {
-                if (wv == 0) {
-                    const int c = L.cur, nh = L.n_heap;
-                    const uint32_t cap_lds = static_cast<uint32_t>(
-                        (grid_ready ? sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask)
-                                    : sizeof(L.pxy) + sizeof(L.pcell) + sizeof(L.cmask) + sizeof(L.grid_lds)) / sizeof(uint2));
-                    for (int h = 0; h < nh; ++h) {
-                        const uint32_t j = L.heap_j[h];
-                        const uint32_t lo = L.r_lo[c][j], hi = min(L.r_hi[c][j], n);
-                        const uint32_t len = hi > lo ? hi - lo : 0u;
-                        uint2 *hbuf = X + lo;
-                        if (len <= cap_lds) {
-                            hbuf = reinterpret_cast<uint2 *>(L.pxy);
-                            for (uint32_t i = lane; i < len; i += kWave) hbuf[i] = X[lo + i];
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        ref_heapsort(hbuf, static_cast<int>(len));
-                        for (uint32_t i = lane; i < len; i += kWave) {
-                            const uint2 e = hbuf[i];
-                            X[lo + i] = e;
-                            ord[lo + i] = e.y;
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    }
-                    // the list without them (order kept), into the other buffer
-                    const int nc = c ^ 1;
-                    uint32_t at = 0;
-                    for (int b = 0; b < L.m_all; b += kWave) {
-                        const int j = b + lane;
-                        const bool keep = j < L.m_all && !(j < m && L.r_dep[c][j] == 0u);
-                        const uint64_t bk = ballot(keep);
-                        if (keep) {
-                            const uint32_t q = at + static_cast<uint32_t>(mbcnt64(bk, 0));
-                            L.r_lo[nc][q] = L.r_lo[c][j];
-                            L.r_hi[nc][q] = L.r_hi[c][j];
-                            L.r_dep[nc][q] = L.r_dep[c][j];
-                        }
-                        at += static_cast<uint32_t>(popc64(bk));
-                    }
-                    if (lane == 0) {
-                        L.m_all = static_cast<int>(at);
-                        L.cur = nc;
-                    }
-                    __builtin_amdgcn_s_waitcnt(0);
-                    set_active(L, L.fin + kSelectChunk);
-                }
+                if (wv == 0) ref_heap_step(to_lds(&L), X, ord, n, m, grid_ready);
                 __syncthreads();
                 FD_REF_COUNT(31, 1u);
                 continue;
@@ -1153,13 +1165,28 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             bool ok = true;
             for (int j = wv; j < nw && ok;) {
                 const uint32_t q = L.wl_ord[j];
-                ok = ref_wave_resolve(X, ord, L.wl_lo[q], L.wl_hi[q], L.wl_dep[q], E, Lp, Rp, L.wstk[wv]);
+                ok = ref_wave_resolve(X, ord, L.wl_lo[q], L.wl_hi[q], L.wl_dep[q], E, Lp, Rp, L.wstk[wv], L.hq, &L.n_hq);
                 int nj = 0;
                 if (lane == 0) nj = atomicAdd(&L.wl_next, 1);
                 j = __builtin_amdgcn_readfirstlane(__shfl(nj, 0));
             }
             if (!ok && lane == 0) L.fail = 5;
             __syncthreads();
+            if (L.n_hq > 0) {  // queued depth-limit subranges (<= kRefWaveLocal each): one wave each, in its buffer
+                const int nq = min(L.n_hq, kRefMaxRanges);
+                for (int q = wv; q < nq; q += kRefWaves) {
+                    const uint32_t qlo = L.hq[2 * q], len = min(L.hq[2 * q + 1] - qlo, kRefWaveLocal);
+                    for (uint32_t i = lane; i < len; i += kWave) E[i] = X[FD_REF_IDX(qlo + i, n, 19)];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    ref_heapsort(E, static_cast<int>(len));
+                    for (uint32_t i = lane; i < len; i += kWave) ord[FD_REF_IDX(qlo + i, n, 19)] = E[i].y;
+                }
+                if (tid == 0 && L.n_hq > kRefMaxRanges) L.fail = 7;
+                __syncthreads();
+                if (tid == 0) L.n_hq = 0;
+            }
             if (tid == 0) L.n_wl = 0;
             FD_REF_MARK(23);  // wave-local ranges
             if (L.fail) break;
@@ -1190,15 +1217,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
                 if (use_grid) L.pcell[i] = (y / s1 + 1) * static_cast<uint32_t>(gw2) + (x / s1 + 1);
             }
             __syncthreads();
-            if (use_grid && a.par_greedy) {  // the workgroup-parallel greedy (sparse NMS candidates)
-                GreedyLds &G = *reinterpret_cast<GreedyLds *>(L.cmask);
-                if (grid_in_lds)
-                    greedy_block<1>(a, f, cn, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
-                                    L.tie_has_prev, G, L.gpred);
-                else
-                    greedy_block<2>(a, f, cn, L.pxy, L.pcell, grid, gw2, prior, L.s_acc, L.s_done, nullptr, L.tie_prev,
-                                    L.tie_has_prev, G, L.gpred);
-            } else {
+            {
                 if (use_grid) conflict_masks(L.pxy, cn, d, rows, cols, L.cmask, tid, NT);
                 __syncthreads();
                 if (tid < kWave) {
