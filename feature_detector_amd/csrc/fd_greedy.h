@@ -31,6 +31,26 @@ typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));  // packed (x, y) of
 // than one ordered step per conflicted lane.
 constexpr int kSeqConflicts = FD_SEQ_CONFLICTS;
 
+// A batch's conflicted lanes (conf) decided by a fixed point on wave-uniform masks: each pass decides
+// every undecided lane whose earlier ok neighbours (C, already restricted to ok lanes) are all decided
+// -- accepted iff none of them was. Passes = the longest conflict chain; each decides at least the
+// lowest undecided lane. acc_m holds the unconflicted ok lanes on entry.
+__device__ __forceinline__ uint64_t resolve_batch(const SelectArgs &a, int f, uint64_t C, uint64_t conf,
+                                                  uint64_t acc_m) {
+    uint64_t dec_m = ~conf;  // decided: unconflicted lanes (accepted if ok) and the not-ok ones
+    for (int pass = 0; dec_m != ~0ull; ++pass) {
+        if (pass >= kWave) {  // unreachable
+            if (lane_id() == 0) atomicOr(&a.status[f], 0x20000000u);
+            break;
+        }
+        const uint64_t can_m = ballot((C & ~dec_m) == 0ull) & ~dec_m;
+        const uint64_t free_m = ballot((C & acc_m) == 0ull);
+        dec_m |= can_m;
+        acc_m |= can_m & free_m;
+    }
+    return acc_m;
+}
+
 // One wave scans a sorted chunk in order (SelectGoodFeatures, feature_point_detector.cpp:62-72), a
 // batch of 64 candidates at a time: occupancy-grid test against earlier batches, then the batch is
 // resolved at once from cmask (per candidate: earlier candidates of its batch within distance d,
@@ -40,12 +60,20 @@ constexpr int kSeqConflicts = FD_SEQ_CONFLICTS;
 // when two adjacent candidates of the visited prefix, or the last visited one and the next, have
 // equal responses -- the only case in which the reference's unstable std::sort (:58-60) can change the
 // result. tie_prev / tie_has_prev carry the last key of the previous chunk (wave 0's LDS state).
-template <int GRID>
+//
+// XM (cross masks, xmask[p]: bit j = candidate (p & ~63) - 64 + j of the previous batch lies within d):
+// the grid test runs one batch ahead. Batch b+1's nine cells are read before batch b's grid writes (LDS
+// operations of a wave complete in order), so it sees batches <= b-1; batch b's accepted candidates are
+// excluded by xmask & (b's accepted lanes) once they are known. The grid reads' latency then overlaps
+// a batch's resolution instead of starting the next one.
+template <int GRID, bool XM = false>
 __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
                                              const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
                                              uint32_t prior, int &s_acc, int &s_done, bool ties, const uint64_t *tmask,
                                              uint32_t key0, uint32_t keylast,
-                                             uint32_t &tie_prev, int &tie_has_prev, uint64_t *st = nullptr) {
+                                             uint32_t &tie_prev, int &tie_has_prev, uint64_t *st = nullptr,
+                                             const uint64_t *xmask = nullptr) {
+    static_assert(!XM || GRID != 0, "cross masks need a grid");
     const int lane = lane_id();
     // diagnostic clocks (a.stamps): per-batch phases into slots 26-28 (st[15]: the running clock)
     auto gst = [&](int slot) {
@@ -67,7 +95,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     bool tied = false;
     // Software pipeline: a batch's position, cell and conflict mask are loaded during the previous
     // batch's resolution (they are read-only here; only the grid is written).
-    auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C) {
+    auto fetch = [&](int b, uint32_t &e, int &cell, uint64_t &C, uint64_t &X) {
         // unconditional LDS reads at a clamped index (in the array: cnt <= kSelectChunk), masked after:
         // no exec-masked branch per array
         const int i = b + lane;
@@ -76,61 +104,90 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         e = pxy[ic];
         cell = gw2 + 1;
         C = 0;
+        X = 0;
         if constexpr (GRID != 0) {
             cell = static_cast<int>(pcell[ic]);
             C = cmask[ic];
         }
+        if constexpr (XM) X = xmask[ic];
         if (!in) {
             e = kEmpty;
             cell = gw2 + 1;
             C = 0;
+            X = 0;
         }
+    };
+    auto gload = [&](int cell, uint32_t (&g)[9]) {
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
+            if constexpr (GRID == 1) g[q] = grid[o];
+            else g[q] = __hip_atomic_load(&grid[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    // no grid entry within distance d of e (e != kEmpty)
+    auto gfree = [&](uint32_t e, const uint32_t (&g)[9]) {
+        bool ok = true;
+        if (pk15) {  // packed halves; the empty cell tests far (grid_empty): min over the 9 cells
+            const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+            uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
+                mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
+            }
+            ok = mn > w2;
+        } else if (pk16) {  // packed halves, as in the conflict masks (select_frame)
+            const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
+                const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
+                if (g[q] != gempty && m <= w2) ok = false;
+            }
+        } else {
+            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const int gx = static_cast<int>(g[q] & 0xFFFFu), gy = static_cast<int>(g[q] >> 16);
+                if (g[q] != gempty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
+            }
+        }
+        return ok;
     };
     uint32_t e_n;
     int cell_n;
-    uint64_t C_n;
+    uint64_t C_n, X_n;
     int stop = -1;  // position of the append that reached `need` (scan order of pxy)
-    fetch(0, e_n, cell_n, C_n);
+    uint64_t acc_prev = 0;  // XM: the previous batch's accepted lanes
+    bool gok_n = true;      // XM: the next batch's grid test
+    uint32_t g_n[9];        // XM: the batch after next's grid cells (in flight)
+    fetch(0, e_n, cell_n, C_n, X_n);
+    if constexpr (XM) {
+        uint32_t g0[9];
+        gload(cell_n, g0);
+        gok_n = gfree(e_n, g0);
+    }
     for (int b0 = 0; b0 < cnt && !done; b0 += kWave) {
         const uint32_t e = e_n;
         const int cell = cell_n;
         uint64_t C = C_n;
         bool ok = e != kEmpty;
         const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-        if constexpr (GRID != 0) {
-            uint32_t g[9];
-#pragma unroll
-            for (int q = 0; q < 9; ++q) {
-                const int o = cell + (q / 3 - 1) * gw2 + (q % 3 - 1);
-                if constexpr (GRID == 1) g[q] = grid[o];
-                else g[q] = __hip_atomic_load(&grid[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (XM) {
+            ok = ok && gok_n && (X_n & acc_prev) == 0ull;
+            if (b0 + kWave < cnt) {  // the next batch: its grid cells before this batch's writes
+                fetch(b0 + kWave, e_n, cell_n, C_n, X_n);
+                gload(cell_n, g_n);
             }
-            if (pk15) {  // packed halves; the empty cell tests far (grid_empty): min over the 9 cells
-                const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
-                uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
-                    mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
-                }
-                ok = ok && mn > w2;
-            } else if (pk16) {  // packed halves, as in the conflict masks (select_frame)
-                const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
-#pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
-                    const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
-                    if (g[q] != gempty && m <= w2) ok = false;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 9; ++q) {
-                    const int gx = static_cast<int>(g[q] & 0xFFFFu), gy = static_cast<int>(g[q] >> 16);
-                    if (g[q] != gempty && abs(x - gx) <= d && abs(y - gy) <= d) ok = false;
-                }
+        } else {
+            if constexpr (GRID != 0) {
+                uint32_t g[9];
+                gload(cell, g);
+                ok = ok && gfree(e, g);
             }
+            if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n, X_n);
         }
-        if (b0 + kWave < cnt) fetch(b0 + kWave, e_n, cell_n, C_n);
         const uint64_t m = ballot(ok);
         gst(26);  // grid test
         C &= m;
@@ -148,19 +205,7 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
                 acc_m |= free_m & (1ull << i);
             }
         } else {
-            uint64_t dec_m = ~conf;  // decided: unconflicted lanes (accepted if ok) and the not-ok ones
-            bool mine = ((conf >> lane) & 1ull) == 0ull;
-            for (int pass = 0; dec_m != ~0ull; ++pass) {
-                if (pass >= kWave) {  // each pass decides the lowest undecided lane: unreachable
-                    if (lane == 0) atomicOr(&a.status[f], 0x20000000u);
-                    break;
-                }
-                const bool can = !mine && (C & ~dec_m) == 0ull;
-                const bool take = can && (C & acc_m) == 0ull;
-                dec_m |= ballot(can);
-                acc_m |= ballot(take);
-                mine = mine || can;
-            }
+            acc_m = resolve_batch(a, f, C, conf, acc_m);
         }
         gst(27);  // resolution
         // need cutoff (:67-69): features.size() >= need is checked after every append
@@ -190,6 +235,10 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
         }
         acc += popc64(acc_m);
         if constexpr (GRID == 2) __builtin_amdgcn_s_waitcnt(0);
+        if constexpr (XM) {
+            acc_prev = acc_m;
+            if (b0 + kWave < cnt) gok_n = e_n != kEmpty && gfree(e_n, g_n);
+        }
         gst(28);  // output + grid update
     }
     if (ties && cnt > 0) {
@@ -223,21 +272,164 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     }
 }
 
+// k_select's scan for its common frame -- occupancy grid in LDS, coordinates with grid_pk15 -- with
+// greedy_chunk<1>'s semantics and less work per batch (tools/calib/greedy_probe.hip: 9.2k -> 5.5k core
+// clocks for 8 batches): the chunk is padded to whole batches (pxy kEmpty, pcell gw2 + 1, cmask 0 for
+// positions [cnt, cnt rounded up to 64)), so the next batch's loads need no masking; one grid-test form;
+// no diagnostic clocks; the tie check (greedy_chunk's tail) folded into the loop on each batch's tmask
+// word, prefetched with the batch.
+__device__ __forceinline__ void greedy_scan(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
+                                            const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
+                                            uint32_t prior, int &s_acc, int &s_done, bool ties, const uint64_t *tmask,
+                                            uint32_t key0, uint32_t keylast, uint32_t &tie_prev, int &tie_has_prev) {
+    const int lane = lane_id();
+    const int d = a.dist;
+    const uint32_t w2 = 2u * static_cast<uint32_t>(d);
+    const u16x2 dd = {static_cast<uint16_t>(d), static_cast<uint16_t>(d)};
+    int acc = s_acc;
+    const int nb = (cnt + kWave - 1) / kWave;
+    bool done = false;
+    bool tied = ties && tie_has_prev != 0 && cnt > 0 && key0 == tie_prev;
+    uint32_t e_n = pxy[lane], cell_n = pcell[lane];
+    uint64_t C_n = cmask[lane];
+    uint64_t tw_n = ties ? tmask[0] : 0ull;
+    for (int b = 0; b < nb && !done; ++b) {
+        const uint32_t e = e_n, cell = cell_n;
+        uint64_t C = C_n;
+        const uint64_t tw = tw_n;
+        uint32_t g[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) g[q] = grid[cell + (q / 3 - 1) * gw2 + (q % 3 - 1)];
+        if (b + 1 < nb) {
+            const int i = (b + 1) * kWave + lane;
+            e_n = pxy[i];
+            cell_n = pcell[i];
+            C_n = cmask[i];
+            if (ties) tw_n = tmask[b + 1];
+        }
+        // packed halves; the empty cell tests far (grid_empty): min over the 9 cells
+        const u16x2 base = __builtin_bit_cast(u16x2, e) - dd;
+        uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
+            mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
+        }
+        const uint64_t m = ballot(e != kEmpty && mn > w2);
+        C &= m;
+        const uint64_t conf = ballot(C != 0ull) & m;
+        uint64_t acc_m = m & ~conf;
+        if (conf) acc_m = resolve_batch(a, f, C, conf, acc_m);
+        // need cutoff (:67-69): features.size() >= need is checked after every append
+        const uint32_t have = prior + static_cast<uint32_t>(acc);
+        const int allow = have < a.need ? static_cast<int>(a.need - have) : 1;
+        uint64_t visited = ~0ull;  // scan positions of this batch the reference visits
+        if (popc64(acc_m) >= allow) {
+            uint64_t keep = 0, t = acc_m;
+            for (int k = 0; k < allow; ++k) {
+                keep |= t & (~t + 1ull);
+                t &= t - 1ull;
+            }
+            acc_m = keep;
+            done = true;
+            const int sl = 63 - __builtin_clzll(acc_m);  // the stop's lane
+            visited = (2ull << sl) - 1ull;
+            if (ties) {  // the candidate after the stop equals it (unknown past the chunk: assumed)
+                const int nx = b * kWave + sl + 1;
+                if (nx >= cnt || (sl < kWave - 1 ? (tw >> (sl + 1)) & 1ull : tw_n & 1ull)) tied = true;
+            }
+        }
+        if (ties && (tw & visited) != 0ull) tied = true;
+        if ((acc_m >> lane) & 1ull) {
+            const int pos = mbcnt64(acc_m, acc);
+            if (pos < a.out_stride) {
+                float2 *o = reinterpret_cast<float2 *>(a.out_xy) + static_cast<int64_t>(f) * a.out_stride + pos;
+                *o = make_float2(static_cast<float>(e & 0xFFFFu), static_cast<float>(e >> 16));
+            }
+            grid[cell] = e;
+        }
+        acc += popc64(acc_m);
+    }
+    if (lane == 0) {
+        s_acc = acc;
+        if (done) s_done = 1;
+        if (ties && cnt > 0) {
+            tie_prev = keylast;  // the chunk's last key, for the next chunk's first comparison
+            tie_has_prev = 1;
+        }
+        if (tied) atomicOr(&a.status[f], FD_FRAME_TIES);
+    }
+}
+
+// Near-bits of 16 candidates q16[0..15] (16-aligned LDS, broadcast reads) around position e: bit j set
+// iff entry j lies within Chebyshev distance d (and j < lim). pk16: packed (x, y) halves,
+// |ex - x| <= d  <=>  (ex - x + d) mod 2^16 <= 2d (no wrap-around: rows, cols + 3d < 2^16); empty
+// entries then need no test (the greedy clears their bits: C &= ballot(ok), and an empty candidate is
+// never accepted, so its cross bit never meets an accepted lane).
+__device__ __forceinline__ uint32_t near16(uint32_t e, const uint32_t *q16, int lim, int d, bool pk16, uint32_t w2) {
+    const uint4 *q4 = reinterpret_cast<const uint4 *>(q16);
+    uint32_t bits = 0;
+    if (pk16) {
+        const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+            const uint4 e4 = q4[j4];
+            const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const u16x2 dt = __builtin_bit_cast(u16x2, ev[t]) - base;
+                const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
+                bits |= (m <= w2 ? 1u : 0u) << (j4 * 4 + t);
+            }
+        }
+        if (lim < 16) bits &= (1u << lim) - 1u;
+    } else {
+        const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+            const uint4 e4 = q4[j4];
+            const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
+                const bool nb = j4 * 4 + t < lim && ev[t] != kEmpty && abs(x - ex) <= d && abs(y - ey) <= d;
+                bits |= static_cast<uint32_t>(nb) << (j4 * 4 + t);
+            }
+        }
+    }
+    return bits;
+}
+
 // Conflict masks of a chunk in scan order: bit j of cmask[p] = candidate (p & ~63) + j, earlier in p's
 // batch of 64, lies within Chebyshev distance d. One work item per (candidate, quarter of its batch)
 // that holds earlier candidates: 16 entries each, no divergent trip counts; each item writes its 16
 // bits of the 64-bit mask. Only those items are enumerated (157 per batch of 64 instead of 4 x 64, the
 // rest were idle lanes): quarter 0 for every position me (me = 0 tests nothing) -- that item also
 // zeroes the quarters past its own -- and quarter q >= 1 for me > 16q, q-major within the batch.
+// xmask (optional, greedy_chunk's XM): bit j of xmask[p] = candidate (p & ~63) - 64 + j (the previous
+// batch) within distance d; 4 x 64 more items per batch (zero for the first batch).
 constexpr int kCmItems = 64 + 47 + 31 + 15;
 __device__ __forceinline__ void conflict_masks(const uint32_t *pxy, int c, int d, int rows, int cols, uint64_t *cmask,
-                                               int tid, int nthr) {
+                                               int tid, int nthr, uint64_t *xmask = nullptr) {
     uint16_t *cm16 = reinterpret_cast<uint16_t *>(cmask);
+    uint16_t *xm16 = reinterpret_cast<uint16_t *>(xmask);
     const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
     const uint32_t w2 = 2u * static_cast<uint32_t>(d);
-    const int n_items = ((c + kWave - 1) / kWave) * kCmItems;
+    const int per = xmask ? kCmItems + 4 * kWave : kCmItems;
+    const int n_items = ((c + kWave - 1) / kWave) * per;
     for (int item = tid; item < n_items; item += nthr) {
-        const int bi = item / kCmItems, t = item - bi * kCmItems;
+        const int bi = item / per, t = item - bi * per;
+        const int bb = bi * kWave;
+        if (t >= kCmItems) {  // cross item: quarter q of the previous batch
+            const int me = (t - kCmItems) & (kWave - 1), q = (t - kCmItems) >> 6;
+            const int p = bb + me;
+            if (p >= c) continue;
+            const uint32_t e = pxy[p];
+            uint32_t bits = 0;
+            if (bi > 0 && e != kEmpty) bits = near16(e, pxy + bb - kWave + 16 * q, 16, d, pk16, w2);
+            xm16[4 * p + q] = static_cast<uint16_t>(bits);
+            continue;
+        }
         int q, me;
         if (t < 64) {
             q = 0;
@@ -252,47 +444,13 @@ __device__ __forceinline__ void conflict_masks(const uint32_t *pxy, int c, int d
             q = 3;
             me = t - (64 + 47 + 31) + 49;
         }
-        const int bb = bi * kWave, p = bb + me;
+        const int p = bb + me;
         if (p >= c) continue;
         if (q == 0)  // quarters without an item of their own (16q >= me): no earlier candidates there
             for (int qz = max(1, (me + 15) >> 4); qz < 4; ++qz) cm16[4 * p + qz] = 0;
         const uint32_t e = pxy[p];
         uint32_t bits = 0;
-        if (e != kEmpty && 16 * q < me) {
-            const int x = static_cast<int>(e & 0xFFFFu), y = static_cast<int>(e >> 16);
-            const uint4 *q4 = reinterpret_cast<const uint4 *>(pxy + bb + 16 * q);  // broadcast
-            const int lim = me - 16 * q;  // entries j < lim of this quarter are earlier
-            if (pk16) {
-                // packed (x, y) halves: |ex - x| <= d  <=>  (ex - x + d) mod 2^16 <= 2d
-                // (no wrap-around: rows, cols + 3d < 2^16). Empty entries need no test:
-                // the greedy clears their bits (C &= ballot(ok)).
-                const u16x2 base = __builtin_bit_cast(u16x2, e) - static_cast<uint16_t>(d);
-#pragma unroll
-                for (int j4 = 0; j4 < 4; ++j4) {
-                    const uint4 e4 = q4[j4];
-                    const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const u16x2 dt = __builtin_bit_cast(u16x2, ev[t]) - base;
-                        const uint32_t m = dt.x > dt.y ? dt.x : dt.y;
-                        bits |= (m <= w2 ? 1u : 0u) << (j4 * 4 + t);
-                    }
-                }
-                if (lim < 16) bits &= (1u << lim) - 1u;
-            } else {
-#pragma unroll
-                for (int j4 = 0; j4 < 4; ++j4) {
-                    const uint4 e4 = q4[j4];
-                    const uint32_t ev[4] = {e4.x, e4.y, e4.z, e4.w};
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const int ex = static_cast<int>(ev[t] & 0xFFFFu), ey = static_cast<int>(ev[t] >> 16);
-                        const bool nb = j4 * 4 + t < lim && ev[t] != kEmpty && abs(x - ex) <= d && abs(y - ey) <= d;
-                        bits |= static_cast<uint32_t>(nb) << (j4 * 4 + t);
-                    }
-                }
-            }
-        }
+        if (e != kEmpty && 16 * q < me) bits = near16(e, pxy + bb + 16 * q, me - 16 * q, d, pk16, w2);
         cm16[4 * p + q] = static_cast<uint16_t>(bits);
     }
 }

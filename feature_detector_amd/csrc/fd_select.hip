@@ -85,6 +85,12 @@ constexpr int kPassUnroll = 8;  // independent list loads in flight per thread
 // corner selection prefers 512: 768 -> 78 us vs ~74).
 constexpr int kSubChunk = 512;
 constexpr int kSubChunkFast = kSelectChunk;
+#ifndef FD_KO
+#define FD_KO 0
+#endif
+// Phase-cost diagnostic builds only (-DFD_KO=mask; results are wrong): 1 = no greedy (the frame stops
+// after its first sub-chunk), 2 = no conflict masks, 4 = no tie bits.
+constexpr int kKnockOut = FD_KO;
 constexpr int kBucketMax = 64;  // largest bin of a sub-chunk ordered by bucket placement (else merge sort)
 // k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
 // with 256 threads (4x the items per wave) the headline frame's selection measured 1.3x slower.
@@ -116,6 +122,10 @@ struct alignas(16) SelectLds {
     uint32_t seg_more[2];
     uint32_t lb_rng[2];  // local-digit bucket sort: the sub-chunk's smallest / largest 32-bit key
     int ff_res[2];  // first_le results (alternating slots)
+    // placement votes (bucket / local-digit placement impossible), zero between sub-chunks: a store by
+    // the voting threads and one barrier instead of __syncthreads_or (measured 858 vs 213 clocks at
+    // 1024 threads, tools/calib/wg_probe.hip)
+    uint32_t vote[2];
     int s_done, s_acc;
     uint64_t st[32];  // diagnostic phase clocks (a.stamps only); 16..31 free for ad-hoc probes
 };
@@ -159,6 +169,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     const int gw2 = a.grid_w + 2;
     const int cells = gw2 * (a.grid_h + 2);
     const bool grid_in_lds = cells <= kGridLdsCells;
+    // the greedy's common case: LDS grid and packed coordinates without an empty-cell test (greedy_scan)
+    const bool scan_fast = use_grid && grid_in_lds && grid_pk15(rows, cols, d);
     uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
     const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
     const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
@@ -223,6 +235,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     if (tid == 0) {
         s_done = 0;
         s_acc = 0;
+        L.vote[0] = 0;
+        L.vote[1] = 0;
         prefix[0] = 0;
         L.tie_prev = 0;
         L.tie_has_prev = 0;
@@ -896,7 +910,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         s_b1 = S[bin + 1];
                         big = s_b - s_b1 > static_cast<uint32_t>(kBucketMax);
                     }
-                    if (!__syncthreads_or(big)) {
+                    if (ballot(big) != 0ull && lane == 0) L.vote[0] = 1u;
+                    __syncthreads();
+                    if (L.vote[0] == 0u) {
                         uint32_t slot = 0;
                         if (tid < c) {
                             slot = atomicAdd(const_cast<uint32_t *>(&S[bin + 1]), 1u) - sbase;
@@ -974,7 +990,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
 #pragma unroll
                     for (int j = 0; j < kPer; ++j)
                         if (tid + j * nthr < c) lbig = lbig || lcnt[dg[j]] - lcnt[dg[j] + 1] > static_cast<uint32_t>(kBucketMax);
-                    if (!__syncthreads_or(lbig)) {
+                    if (ballot(lbig) != 0ull && lane == 0) L.vote[1] = 1u;
+                    __syncthreads();
+                    if (L.vote[1] == 0u) {
 #pragma unroll
                         for (int j = 0; j < kPer; ++j)
                             if (tid + j * nthr < c) tmp[min(lcnt[dg[j] + 1] + sl[j], static_cast<uint32_t>(kSelectChunk - 1))] = kk[j];
@@ -1056,7 +1074,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     FD_STAMP(13);  // place
                     }
                     }
-                    if (!a.tie_idx_desc) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
+                    if (!a.tie_idx_desc && !(kKnockOut & 4)) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
                         const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;
                         for (int i = opaque(tid); i < c64; i += nthr) {
                             const bool t = i > 0 && i < c && L.pk32[i] == L.pk32[i - 1];
@@ -1065,19 +1083,34 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         }
                     }
                     // conflict masks: earlier candidates of the same 64-batch within distance d
-                    if (use_grid) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
+                    if (use_grid && !(kKnockOut & 2)) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
+                    if (scan_fast)  // greedy_scan's padding to whole batches
+                        for (int i = c + tid; i < ((c + kWave - 1) & ~(kWave - 1)); i += nthr) {
+                            pxy[i] = kEmpty;
+                            pcell[i] = static_cast<uint32_t>(gw2 + 1);
+                            buf[i] = 0ull;
+                        }
                 }
                 __syncthreads();
+                if (tid == 0) {  // (read before the barrier above; the next placement is barriers away)
+                    L.vote[0] = 0u;
+                    L.vote[1] = 0u;
+                }
                 FD_STAMP(14);  // conflict masks
                 // greedy scan in order by wave 0 (SelectGoodFeatures :62-72); ties checked unless the
                 // order of equal responses is defined (SuperPoint's multimap)
-                if (tid < kWave) {
+                if (kKnockOut & 1) {  // (phase-cost diagnostic build: no greedy, the frame ends here)
+                    if (tid == 0) s_done = 1;
+                } else if (tid < kWave) {
                     const bool ties = !a.tie_idx_desc;
                     const uint64_t *tm = L.tmask;
                     if (!use_grid)
                         greedy_chunk<0>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
                                         L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev,
                                         a.stamps ? L.st : nullptr);
+                    else if (scan_fast)
+                        greedy_scan(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
+                                    L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
                     else if (grid_in_lds)
                         greedy_chunk<1>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
                                         L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev,

@@ -469,14 +469,16 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             return self.pool(x) if pool else x
 
         def first_layers(self, x):
-            """conv1a -> ReLU -> conv1b -> ReLU -> MaxPool2d(2, 2): fp16 device input in one fused pass
-            (conv1ab_bias_relu, the 64-channel full-resolution activation stays on chip); otherwise
-            layer by layer through cbr."""
+            """conv1a -> ReLU -> conv1b -> ReLU -> MaxPool2d(2, 2), layer by layer through cbr (conv1a's
+            write-bound pass, then conv1b on the matrix cores). The fused pass (conv1ab_bias_relu: conv1a
+            recomputed inside conv1b's tiles, the full-resolution activation never written) is bit-exact
+            but measured slower -- 5.87 vs 5.57-5.60 ms per 64-frame forward (conv1b is bound by its LDS
+            reads, which the recompute adds to) -- so it runs only under the FD_SP_C1C64 A/B switch."""
             if x.dtype == torch.float16 and x.is_cuda and x.dim() == 4 and x.shape[1] == 1 \
                     and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.shape[3] <= 4096 \
                     and self.conv1a.out_channels == 64 and self.conv1b.in_channels == 64 \
                     and self.conv1b.out_channels == 64 and not _ab_env("FD_SP_UNFUSED") \
-                    and not _ab_env("FD_SP_NO_C1C64"):  # (A/B switches)
+                    and _ab_env("FD_SP_C1C64"):  # (A/B switches)
                 tag = (self.conv1b.weight.data_ptr(), self.conv1b.weight._version, x.device)
                 cache = self.__dict__.setdefault("_fd_packed", {})
                 hit = cache.get(id(self.conv1b))

@@ -4,6 +4,7 @@
 #   tests=PATHS        a subset (comma-separated pytest paths / node ids), no smoke()
 #   ab=SHAPE           A/B of abvar/base.so vs abvar/new.so (FD_LIB_PATH) on a tools/profile_kernels.py
 #                      shape (comma-separated args), alternating twice, each under rocprofv3 --kernel-trace --stats
+#   abx=SHAPE:L1:L2..  the same over libraries L1, L2, ... (paths under the repo), each once, in order
 #   env=SHAPE:E1:E2..  A/B of environment settings (each Ek: comma-separated VAR=V) on a shape, under
 #                      rocprofv3 --kernel-trace --stats; FD_DEBUG_AB=1 is set so the library honours its switches
 #   bench=ARGS         one bench.py line (ARGS: comma-separated bench.py flags) -> gpurun_out/bench_<n>.json
@@ -55,6 +56,14 @@ for S in "$@"; do
       for L in abvar/base.so abvar/new.so abvar/base.so abvar/new.so; do
         d=gpurun_out/abl/$(basename $L .so)_${n}_$RANDOM
         prof $d "${val//,/ }" FD_LIB_PATH=$GRAFT_REPO_ROOT/$L
+        kstats $d $L
+        rm -rf $d
+      done ;;
+    abx)
+      IFS=':' read -ra parts <<< "$val"
+      for L in "${parts[@]:1}"; do
+        d=gpurun_out/abl/$(basename $L .so)_${n}_$RANDOM
+        prof $d "${parts[0]//,/ }" FD_LIB_PATH=$GRAFT_REPO_ROOT/$L
         kstats $d $L
         rm -rf $d
       done ;;
