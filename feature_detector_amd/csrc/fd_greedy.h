@@ -272,95 +272,6 @@ __device__ __forceinline__ void greedy_chunk(const SelectArgs &a, int f, int cnt
     }
 }
 
-// k_select's scan for its common frame -- occupancy grid in LDS, coordinates with grid_pk15 -- with
-// greedy_chunk<1>'s semantics and less work per batch (tools/calib/greedy_probe.hip: 9.2k -> 5.5k core
-// clocks for 8 batches): the chunk is padded to whole batches (pxy kEmpty, pcell gw2 + 1, cmask 0 for
-// positions [cnt, cnt rounded up to 64)), so the next batch's loads need no masking; one grid-test form;
-// no diagnostic clocks; the tie check (greedy_chunk's tail) folded into the loop on each batch's tmask
-// word, prefetched with the batch.
-__device__ __forceinline__ void greedy_scan(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
-                                            const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
-                                            uint32_t prior, int &s_acc, int &s_done, bool ties, const uint64_t *tmask,
-                                            uint32_t key0, uint32_t keylast, uint32_t &tie_prev, int &tie_has_prev) {
-    const int lane = lane_id();
-    const int d = a.dist;
-    const uint32_t w2 = 2u * static_cast<uint32_t>(d);
-    const u16x2 dd = {static_cast<uint16_t>(d), static_cast<uint16_t>(d)};
-    int acc = s_acc;
-    const int nb = (cnt + kWave - 1) / kWave;
-    bool done = false;
-    bool tied = ties && tie_has_prev != 0 && cnt > 0 && key0 == tie_prev;
-    uint32_t e_n = pxy[lane], cell_n = pcell[lane];
-    uint64_t C_n = cmask[lane];
-    uint64_t tw_n = ties ? tmask[0] : 0ull;
-    for (int b = 0; b < nb && !done; ++b) {
-        const uint32_t e = e_n, cell = cell_n;
-        uint64_t C = C_n;
-        const uint64_t tw = tw_n;
-        uint32_t g[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) g[q] = grid[cell + (q / 3 - 1) * gw2 + (q % 3 - 1)];
-        if (b + 1 < nb) {
-            const int i = (b + 1) * kWave + lane;
-            e_n = pxy[i];
-            cell_n = pcell[i];
-            C_n = cmask[i];
-            if (ties) tw_n = tmask[b + 1];
-        }
-        // packed halves; the empty cell tests far (grid_empty): min over the 9 cells
-        const u16x2 base = __builtin_bit_cast(u16x2, e) - dd;
-        uint32_t mn = 0xFFFFFFFFu;
-#pragma unroll
-        for (int q = 0; q < 9; ++q) {
-            const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
-            mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
-        }
-        const uint64_t m = ballot(e != kEmpty && mn > w2);
-        C &= m;
-        const uint64_t conf = ballot(C != 0ull) & m;
-        uint64_t acc_m = m & ~conf;
-        if (conf) acc_m = resolve_batch(a, f, C, conf, acc_m);
-        // need cutoff (:67-69): features.size() >= need is checked after every append
-        const uint32_t have = prior + static_cast<uint32_t>(acc);
-        const int allow = have < a.need ? static_cast<int>(a.need - have) : 1;
-        uint64_t visited = ~0ull;  // scan positions of this batch the reference visits
-        if (popc64(acc_m) >= allow) {
-            uint64_t keep = 0, t = acc_m;
-            for (int k = 0; k < allow; ++k) {
-                keep |= t & (~t + 1ull);
-                t &= t - 1ull;
-            }
-            acc_m = keep;
-            done = true;
-            const int sl = 63 - __builtin_clzll(acc_m);  // the stop's lane
-            visited = (2ull << sl) - 1ull;
-            if (ties) {  // the candidate after the stop equals it (unknown past the chunk: assumed)
-                const int nx = b * kWave + sl + 1;
-                if (nx >= cnt || (sl < kWave - 1 ? (tw >> (sl + 1)) & 1ull : tw_n & 1ull)) tied = true;
-            }
-        }
-        if (ties && (tw & visited) != 0ull) tied = true;
-        if ((acc_m >> lane) & 1ull) {
-            const int pos = mbcnt64(acc_m, acc);
-            if (pos < a.out_stride) {
-                float2 *o = reinterpret_cast<float2 *>(a.out_xy) + static_cast<int64_t>(f) * a.out_stride + pos;
-                *o = make_float2(static_cast<float>(e & 0xFFFFu), static_cast<float>(e >> 16));
-            }
-            grid[cell] = e;
-        }
-        acc += popc64(acc_m);
-    }
-    if (lane == 0) {
-        s_acc = acc;
-        if (done) s_done = 1;
-        if (ties && cnt > 0) {
-            tie_prev = keylast;  // the chunk's last key, for the next chunk's first comparison
-            tie_has_prev = 1;
-        }
-        if (tied) atomicOr(&a.status[f], FD_FRAME_TIES);
-    }
-}
-
 // Near-bits of 16 candidates q16[0..15] (16-aligned LDS, broadcast reads) around position e: bit j set
 // iff entry j lies within Chebyshev distance d (and j < lim). pk16: packed (x, y) halves,
 // |ex - x| <= d  <=>  (ex - x + d) mod 2^16 <= 2d (no wrap-around: rows, cols + 3d < 2^16); empty
@@ -452,6 +363,205 @@ __device__ __forceinline__ void conflict_masks(const uint32_t *pxy, int c, int d
         uint32_t bits = 0;
         if (e != kEmpty && 16 * q < me) bits = near16(e, pxy + bb + 16 * q, me - 16 * q, d, pk16, w2);
         cm16[4 * p + q] = static_cast<uint16_t>(bits);
+    }
+}
+
+// ---- k_select's pipelined scan (sorted chunks, occupancy grid in LDS, coordinates with grid_pk15) ----
+//
+// The greedy is one wave's chain of dependent instructions (a lone wave issues a dependent VALU op
+// about every 8 core clocks: tools/calib/icache_probe.hip), so everything that need not be on it is
+// moved off it: the conflict masks of batch b are computed by the other waves while wave 0 scans
+// (their work items in batch order; ScanLds::cnt[b] counts the finished items of batch b), and the
+// outputs and the tie check are done after the scan by the whole workgroup from the accepted lanes of
+// each batch (ScanLds::accm / accb). tools/calib/greedy_probe.hip times the scan alone.
+constexpr int kScanBatches = kSelectChunk / kWave;
+struct ScanLds {  // (placed in the unused tail of the LDS occupancy grid)
+    uint64_t accm[kScanBatches];  // accepted lanes of each scanned batch
+    uint32_t accb[kScanBatches];  // features accepted before the batch (this frame)
+    uint32_t cnt[kScanBatches];   // finished conflict-mask items of batch b (kCmItems: ready)
+    int nbp, stop, done, pad;  // batches scanned; scan position of the stop; stopped at `need`
+};
+constexpr int kScanLdsWords = static_cast<int>(sizeof(ScanLds) / 4);
+
+// Conflict masks (as conflict_masks) by waves 1.. of the workgroup (hw = wave - 1 of nh), items in
+// batch order so that the first batches are ready first; each wave adds its finished items per batch
+// to sl.cnt after its mask writes.
+__device__ __forceinline__ void scan_masks(const uint32_t *pxy, int c, int d, int rows, int cols, uint64_t *cmask,
+                                           ScanLds &sl, int hw, int nh) {
+    const int lane = lane_id();
+    uint16_t *cm16 = reinterpret_cast<uint16_t *>(cmask);
+    const bool pk16 = rows + 3 * d < 65536 && cols + 3 * d < 65536;
+    const uint32_t w2 = 2u * static_cast<uint32_t>(d);
+    const int nb = (c + kWave - 1) / kWave;
+    const int total = nb * kCmItems;
+    for (int base = hw * kWave; base < total; base += nh * kWave) {
+        const int item = base + lane;
+        if (item < total) {
+            const int bi = item / kCmItems, t = item - bi * kCmItems;
+            int q, me;
+            if (t < 64) {
+                q = 0;
+                me = t;
+            } else if (t < 64 + 47) {
+                q = 1;
+                me = t - 64 + 17;
+            } else if (t < 64 + 47 + 31) {
+                q = 2;
+                me = t - (64 + 47) + 33;
+            } else {
+                q = 3;
+                me = t - (64 + 47 + 31) + 49;
+            }
+            const int bb = bi * kWave, p = bb + me;
+            if (p < c) {
+                if (q == 0)
+                    for (int qz = max(1, (me + 15) >> 4); qz < 4; ++qz) cm16[4 * p + qz] = 0;
+                const uint32_t e = pxy[p];
+                uint32_t bits = 0;
+                if (e != kEmpty && 16 * q < me) bits = near16(e, pxy + bb + 16 * q, me - 16 * q, d, pk16, w2);
+                cm16[4 * p + q] = static_cast<uint16_t>(bits);
+            } else if (q == 0) {
+                cmask[p] = 0ull;  // (the last batch past c)
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) {
+            const int hi = min(base + kWave, total);
+            for (int b = base / kCmItems; b * kCmItems < hi; ++b)
+                atomicAdd(&sl.cnt[b], static_cast<uint32_t>(min(hi, (b + 1) * kCmItems) - max(base, b * kCmItems)));
+        }
+    }
+}
+
+// Wave 0's scan of a sorted chunk (SelectGoodFeatures, feature_point_detector.cpp:62-72), greedy_chunk<1>'s
+// semantics: per batch, the occupancy-grid test, the in-batch resolution from the conflict masks, the
+// need cutoff (:67-69) and the grid update; the accepted lanes go to sl.accm. Waits for each batch's
+// masks (sl.cnt[b] == kCmItems). Outputs: s_acc, s_done, sl.nbp / stop / done.
+__device__ __forceinline__ void greedy_scan(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
+                                            const uint32_t *pcell, const uint64_t *cmask, uint32_t *grid, int gw2,
+                                            uint32_t prior, int &s_acc, int &s_done, ScanLds &sl,
+                                            uint64_t *st = nullptr) {
+    const int lane = lane_id();
+    // diagnostic clocks (a.stamps): slot 26 the first batch, slot 27 the others (st[15]: the running clock)
+    auto gst = [&](int slot) {
+        if (st && lane == 0) {
+            const uint64_t now = __builtin_readcyclecounter();
+            st[slot] += now - st[15];
+            st[15] = now;
+        }
+    };
+    const int d = a.dist;
+    const uint32_t w2 = 2u * static_cast<uint32_t>(d);
+    const u16x2 dd = {static_cast<uint16_t>(d), static_cast<uint16_t>(d)};
+    uint32_t acc = static_cast<uint32_t>(s_acc);
+    const int nb = (cnt + kWave - 1) / kWave;
+    bool done = false;
+    int stop = -1, b = 0;
+    // positions and cells are final before the scan starts: prefetched one batch ahead (entries past
+    // cnt are replaced when used: an empty position in a valid cell); the masks once their batch is done
+    uint32_t e_n = pxy[lane], cell_n = pcell[lane];
+    uint32_t rdy_n = __hip_atomic_load(&sl.cnt[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (; b < nb && !done; ++b) {
+        const bool in = b * kWave + lane < cnt;
+        const uint32_t e = in ? e_n : kEmpty;
+        const uint32_t cell = in ? cell_n : static_cast<uint32_t>(gw2 + 1);
+        uint32_t rdy = rdy_n;
+        for (int spin = 0; rdy != static_cast<uint32_t>(kCmItems); ++spin) {  // (the mask waves reach every batch)
+            if (spin > (1 << 20)) {  // consistency guard instead of a hang
+                if (lane == 0) atomicOr(&a.status[f], 0x20000000u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            rdy = __hip_atomic_load(&sl.cnt[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        uint32_t g[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) g[q] = grid[cell + (q / 3 - 1) * gw2 + (q % 3 - 1)];
+        uint64_t C = cmask[b * kWave + lane];
+        if (b + 1 < nb) {
+            const int i = min((b + 1) * kWave + lane, kSelectChunk - 1);
+            e_n = pxy[i];
+            cell_n = pcell[i];
+            rdy_n = __hip_atomic_load(&sl.cnt[b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // packed halves; the empty cell tests far (grid_empty): min over the 9 cells
+        const u16x2 base = __builtin_bit_cast(u16x2, e) - dd;
+        uint32_t mn = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) {
+            const u16x2 dt = __builtin_bit_cast(u16x2, g[q]) - base;
+            mn = min(mn, static_cast<uint32_t>(dt.x > dt.y ? dt.x : dt.y));
+        }
+        const uint64_t m = ballot(e != kEmpty && mn > w2);
+        C &= m;
+        const uint64_t conf = ballot(C != 0ull) & m;
+        uint64_t acc_m = m & ~conf;
+        if (conf) acc_m = resolve_batch(a, f, C, conf, acc_m);
+        // need cutoff (:67-69): features.size() >= need is checked after every append
+        const uint32_t have = prior + acc;
+        const int allow = have < a.need ? static_cast<int>(a.need - have) : 1;
+        if (popc64(acc_m) >= allow) {
+            uint64_t keep = 0, t = acc_m;
+            for (int k = 0; k < allow; ++k) {
+                keep |= t & (~t + 1ull);
+                t &= t - 1ull;
+            }
+            acc_m = keep;
+            done = true;
+            stop = b * kWave + 63 - __builtin_clzll(acc_m);
+        }
+        if ((acc_m >> lane) & 1ull) grid[cell] = e;
+        if (lane == 0) {
+            sl.accm[b] = acc_m;
+            sl.accb[b] = acc;
+        }
+        acc += static_cast<uint32_t>(popc64(acc_m));
+        gst(b == 0 ? 26 : 27);
+    }
+    if (lane == 0) {
+        s_acc = static_cast<int>(acc);
+        if (done) s_done = 1;
+        sl.nbp = b;
+        sl.stop = stop;
+        sl.done = done ? 1 : 0;
+    }
+}
+
+// After the scan (all threads, past a barrier): the accepted candidates' outputs in scan order, and
+// greedy_chunk's tie check on the visited prefix from the 32-bit keys in scan order (pk32): equal
+// adjacent keys in it, the chunk's first key equal to the previous sub-chunk's last, or (stopped) the
+// candidate after the stop equal to it (unknown past the sub-chunk: assumed).
+__device__ __forceinline__ void scan_outputs(const SelectArgs &a, int f, int cnt, const uint32_t *pxy,
+                                             const ScanLds &sl, bool ties, const uint32_t *pk32, uint32_t &tie_prev,
+                                             int &tie_has_prev, int tid, int nthr) {
+    const int lane = lane_id();
+    const int np = sl.nbp * kWave;
+    for (int p = tid; p < np; p += nthr) {
+        const uint64_t m = sl.accm[p >> 6];
+        if ((m >> (p & 63)) & 1ull) {
+            const int pos = static_cast<int>(sl.accb[p >> 6]) + popc64(m & ((1ull << (p & 63)) - 1ull));
+            if (pos < a.out_stride) {
+                const uint32_t e = pxy[p];
+                float2 *o = reinterpret_cast<float2 *>(a.out_xy) + static_cast<int64_t>(f) * a.out_stride + pos;
+                *o = make_float2(static_cast<float>(e & 0xFFFFu), static_cast<float>(e >> 16));
+            }
+        }
+    }
+    if (!ties || cnt <= 0) return;
+    const bool done = sl.done != 0;
+    const int last = done ? sl.stop : cnt - 1;
+    bool t = false;
+    for (int i = tid; i <= last; i += nthr)
+        if (i > 0 && pk32[i] == pk32[i - 1]) t = true;
+    if (tid == 0) {
+        if (tie_has_prev && pk32[0] == tie_prev) t = true;
+        if (done && (last + 1 >= cnt || pk32[last + 1] == pk32[last])) t = true;
+    }
+    if (ballot(t) != 0ull && lane == 0) atomicOr(&a.status[f], FD_FRAME_TIES);
+    if (tid == 0) {  // (tie_prev was read above by this thread only)
+        tie_prev = pk32[cnt - 1];
+        tie_has_prev = 1;
     }
 }
 

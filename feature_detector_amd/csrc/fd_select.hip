@@ -89,7 +89,8 @@ constexpr int kSubChunkFast = kSelectChunk;
 #define FD_KO 0
 #endif
 // Phase-cost diagnostic builds only (-DFD_KO=mask; results are wrong): 1 = no greedy (the frame stops
-// after its first sub-chunk), 2 = no conflict masks, 4 = no tie bits.
+// after its first sub-chunk), 2 = no conflict masks, 4 = no tie bits, 8 = bucket placement without the
+// rank scan (group slot order), 16 = place() without the position decode.
 constexpr int kKnockOut = FD_KO;
 constexpr int kBucketMax = 64;  // largest bin of a sub-chunk ordered by bucket placement (else merge sort)
 // k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
@@ -112,7 +113,7 @@ struct alignas(16) SelectLds {
     uint64_t tmask[kSelectChunk / kWave + 1];  // per 64-batch: bit l = candidate equals its predecessor
     uint32_t prev_min;                         // smallest 32-bit key of the previous sub-chunk (prefilter)
     int have_prev_min;
-    uint32_t grid_lds[kGridLdsCells];
+    alignas(16) uint32_t grid_lds[kGridLdsCells];  // (its tail holds the pipelined scan's ScanLds)
     uint32_t tie_prev;
     int tie_has_prev;
     uint64_t prefix[kLevels];
@@ -169,8 +170,12 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     const int gw2 = a.grid_w + 2;
     const int cells = gw2 * (a.grid_h + 2);
     const bool grid_in_lds = cells <= kGridLdsCells;
-    // the greedy's common case: LDS grid and packed coordinates without an empty-cell test (greedy_scan)
-    const bool scan_fast = use_grid && grid_in_lds && grid_pk15(rows, cols, d);
+    // the greedy's common case: LDS grid (with room for ScanLds in its tail) and packed coordinates
+    // without an empty-cell test: the pipelined scan (greedy_scan beside scan_masks)
+    const bool scan_fast = use_grid && grid_in_lds && cells <= kGridLdsCells - kScanLdsWords &&
+                           grid_pk15(rows, cols, d) && nthr >= 2 * kWave;
+    ScanLds &sl = *reinterpret_cast<ScanLds *>(&L.grid_lds[kGridLdsCells - kScanLdsWords]);
+    static_assert((kGridLdsCells - kScanLdsWords) % 4 == 0, "ScanLds alignment");
     uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
     const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
     const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
@@ -750,6 +755,12 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             const uint32_t s1 = static_cast<uint32_t>(d + 1);
             const float rcp_cols = 1.0f / static_cast<float>(cols), rcp_s1 = 1.0f / static_cast<float>(s1);
             auto place = [&](int pos, uint64_t sk) {  // decode position, prior mask, grid cell
+                if (kKnockOut & 16) {  // (diagnostic build: keys only)
+                    pxy[pos] = static_cast<uint32_t>(sk) & 0x00FF00FFu;
+                    L.pk32[pos] = static_cast<uint32_t>(sk >> 32);
+                    pcell[pos] = static_cast<uint32_t>(gw2 + 1);
+                    return;
+                }
                 uint32_t idx = a.tie_idx_desc ? static_cast<uint32_t>(sk) : ~static_cast<uint32_t>(sk);
                 bool ok = true;
                 if (idx >= static_cast<uint32_t>(rows) * static_cast<uint32_t>(cols)) {  // consistency guard
@@ -911,6 +922,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         big = s_b - s_b1 > static_cast<uint32_t>(kBucketMax);
                     }
                     if (ballot(big) != 0ull && lane == 0) L.vote[0] = 1u;
+                    if (scan_fast && tid < kScanBatches) sl.cnt[tid] = 0u;  // (the last scan's reads are barriers ago)
                     __syncthreads();
                     if (L.vote[0] == 0u) {
                         uint32_t slot = 0;
@@ -923,7 +935,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         if (tid < c) {
                             const uint32_t g0 = s_b1 - sbase, gn = s_b - s_b1;
                             uint32_t r = 0;
-                            if (!a.dup_keys) {
+                            if (kKnockOut & 8) {
+                                r = slot - g0;  // (diagnostic build: group slot instead of rank)
+                            } else if (!a.dup_keys) {
                                 for (uint32_t j0 = 0; j0 < gn; j0 += 8) {  // 8 loads in flight (clamped to the group)
                                     uint64_t v[8];
 #pragma unroll
@@ -1074,7 +1088,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     FD_STAMP(13);  // place
                     }
                     }
-                    if (!a.tie_idx_desc && !(kKnockOut & 4)) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
+                    if (!a.tie_idx_desc && !(kKnockOut & 4) && !scan_fast) {  // tie bits over the ordered sub-chunk (wave-aligned 64-blocks)
                         const int c64 = ((c + kWave - 1) & ~(kWave - 1)) + kWave;
                         for (int i = opaque(tid); i < c64; i += nthr) {
                             const bool t = i > 0 && i < c && L.pk32[i] == L.pk32[i - 1];
@@ -1083,16 +1097,11 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         }
                     }
                     // conflict masks: earlier candidates of the same 64-batch within distance d
-                    if (use_grid && !(kKnockOut & 2)) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
-                    if (scan_fast)  // greedy_scan's padding to whole batches
-                        for (int i = c + tid; i < ((c + kWave - 1) & ~(kWave - 1)); i += nthr) {
-                            pxy[i] = kEmpty;
-                            pcell[i] = static_cast<uint32_t>(gw2 + 1);
-                            buf[i] = 0ull;
-                        }
+                    // (the pipelined scan computes both per batch, beside the scan)
+                    if (use_grid && !(kKnockOut & 2) && !scan_fast) conflict_masks(pxy, c, d, rows, cols, buf, tid, nthr);
                 }
-                __syncthreads();
-                if (tid == 0) {  // (read before the barrier above; the next placement is barriers away)
+                if (!scan_fast) __syncthreads();
+                if (tid == 0) {  // (read before the placement's last barrier; the next placement is barriers away)
                     L.vote[0] = 0u;
                     L.vote[1] = 0u;
                 }
@@ -1101,6 +1110,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                 // order of equal responses is defined (SuperPoint's multimap)
                 if (kKnockOut & 1) {  // (phase-cost diagnostic build: no greedy, the frame ends here)
                     if (tid == 0) s_done = 1;
+                } else if (scan_fast) {
+                    // wave 0 scans batch b once waves 1.. have its conflict masks in LDS
+                    if (wave == 0)
+                        greedy_scan(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, sl,
+                                    a.stamps ? L.st : nullptr);
+                    else
+                        scan_masks(pxy, c_sort, d, rows, cols, buf, sl, wave - 1, nthr / kWave - 1);
+                    __syncthreads();
+                    scan_outputs(a, f, c_sort, pxy, sl, !a.tie_idx_desc, L.pk32, L.tie_prev, L.tie_has_prev, tid, nthr);
                 } else if (tid < kWave) {
                     const bool ties = !a.tie_idx_desc;
                     const uint64_t *tm = L.tmask;
@@ -1108,9 +1126,6 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         greedy_chunk<0>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
                                         L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev,
                                         a.stamps ? L.st : nullptr);
-                    else if (scan_fast)
-                        greedy_scan(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
-                                    L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev);
                     else if (grid_in_lds)
                         greedy_chunk<1>(a, f, c_sort, pxy, pcell, buf, grid_lds, gw2, prior, s_acc, s_done, ties, tm,
                                         L.pk32[0], L.pk32[max(c_sort - 1, 0)], L.tie_prev, L.tie_has_prev,

@@ -118,6 +118,7 @@ struct alignas(16) ProbeLds {
     uint64_t cmask[kSelectChunk];
     uint64_t tmask[kSelectChunk / kWave + 1];
     uint64_t accm[kSelectChunk / kWave];
+    ScanLds sl;
     uint32_t grid[kGridLdsCells];
     uint32_t tie_prev;
     int tie_has_prev, s_acc, s_done;
@@ -137,6 +138,7 @@ __global__ __launch_bounds__(1024) void k_probe(SelectArgs a, const uint32_t *po
                            : static_cast<uint32_t>(gw2 + 1);
     }
     for (int i = tid; i <= kSelectChunk / kWave; i += nthr) L.tmask[i] = 0;
+    for (int i = tid; i < kScanBatches; i += nthr) L.sl.cnt[i] = kCmItems;  // (masks all ready)
     if (tid == 0) {
         L.tie_prev = 0;
         L.tie_has_prev = 0;
@@ -147,8 +149,9 @@ __global__ __launch_bounds__(1024) void k_probe(SelectArgs a, const uint32_t *po
     conflict_masks(L.pxy, c, a.dist, a.rows, a.cols, L.cmask, tid, nthr);
     for (int i = c + tid; i < ((c + kWave - 1) & ~(kWave - 1)); i += nthr) L.cmask[i] = 0;
     __syncthreads();
-    uint64_t t0 = 0, t1 = 0;
+    uint64_t t0 = 0, t1 = 0, r0 = 0, r1 = 0;
     if (tid < kWave) {
+        r0 = __builtin_amdgcn_s_memrealtime();
         t0 = __builtin_readcyclecounter();
         if constexpr (VAR == 0)
             greedy_chunk<1>(a, 0, c, L.pxy, L.pcell, L.cmask, L.grid, gw2, 0u, L.s_acc, L.s_done, false, L.tmask, 0u,
@@ -156,22 +159,42 @@ __global__ __launch_bounds__(1024) void k_probe(SelectArgs a, const uint32_t *po
         else if constexpr (VAR == 1)
             greedy_chunk<1>(a, 0, c, L.pxy, L.pcell, L.cmask, L.grid, gw2, 0u, L.s_acc, L.s_done, true, L.tmask, 0u,
                             0u, L.tie_prev, L.tie_has_prev, nullptr);
+        else if constexpr (VAR == 5)
+            greedy_scan(a, 0, c, L.pxy, L.pcell, L.cmask, L.grid, gw2, 0u, L.s_acc, L.s_done, L.sl);
         else
             greedy_lean<VAR >= 3, VAR == 4>(a, 0, c, L.pxy, L.pcell, L.cmask, L.grid, gw2, 0u, L.s_acc, L.s_done, L.accm);
         t1 = __builtin_readcyclecounter();
+        if constexpr (VAR == 0) {  // core clock calibration: a ~20 us spin against the 100 MHz real-time counter
+            while (__builtin_readcyclecounter() - t1 < 50000) __builtin_amdgcn_s_sleep(1);
+            t1 = __builtin_readcyclecounter();
+        }
+        r1 = __builtin_amdgcn_s_memrealtime();
     }
     __syncthreads();
     if (tid == 0) {
         out[0] = t1 - t0;
         out[1] = static_cast<uint64_t>(L.s_acc);
+        out[2] = r1 - r0;
     }
 }
 
-int main() {
+int main(int argc, char **argv) {
+    // argv[1] (optional): a chunk's positions in scan order, uint32 (y << 16) | x (greedy_probe_pos.bin:
+    // the top 512 Harris candidates of oracle.make_frame("noise", 7, 480, 640), threshold 30), need 200
     const int c = 509;
     std::mt19937 rng(7);
-    std::vector<uint32_t> pos(c);
+    std::vector<uint32_t> pos(512);
     for (auto &p : pos) p = (static_cast<uint32_t>(rng() % kRows) << 16) | static_cast<uint32_t>(rng() % kCols);
+    uint32_t need = 500;
+    if (argc > 1) {
+        FILE *fp = std::fopen(argv[1], "rb");
+        if (!fp || std::fread(pos.data(), 4, 512, fp) != 512) {
+            std::printf("cannot read %s\n", argv[1]);
+            return 1;
+        }
+        std::fclose(fp);
+        need = 200;
+    }
     uint32_t *dpos = nullptr, *status = nullptr;
     uint64_t *out = nullptr;
     float *oxy = nullptr;
@@ -180,36 +203,43 @@ int main() {
     hipMalloc(&out, 64);
     hipMalloc(&oxy, 8 * 1024);
     hipMemcpy(dpos, pos.data(), c * 4, hipMemcpyHostToDevice);
+    std::printf("%s positions, need %u\n", argc > 1 ? argv[1] : "uniform random", need);
     SelectArgs a{};
     a.rows = kRows;
     a.cols = kCols;
     a.dist = kD;
-    a.need = 500;
+    a.need = need;
     a.grid_w = (kCols + kD) / (kD + 1);
     a.grid_h = (kRows + kD) / (kD + 1);
     a.out_xy = oxy;
     a.out_stride = 1024;
     a.status = status;
-    const char *names[] = {"greedy_chunk<1>", "greedy_chunk<1> + ties", "lean", "lean, deferred output",
-                           "lean, deferred, mask fp"};
-    for (int var = 0; var < 5; ++var)
+    const char *names[] = {"greedy_chunk<1> (+spin)", "greedy_chunk<1> + ties", "lean", "lean, deferred output",
+                           "lean, deferred, mask fp", "greedy_scan (pipelined)"};
+    for (int var = 0; var < 6; ++var)
     for (int nt : {64, 1024}) {
-        uint64_t best = ~0ull, acc = 0;
+        uint64_t best = ~0ull, acc = 0, first = 0;
         for (int r = 0; r < 7; ++r) {
             switch (var) {
                 case 0: hipLaunchKernelGGL(k_probe<0>, dim3(1), dim3(nt), 0, 0, a, dpos, c, out); break;
                 case 1: hipLaunchKernelGGL(k_probe<1>, dim3(1), dim3(nt), 0, 0, a, dpos, c, out); break;
                 case 2: hipLaunchKernelGGL(k_probe<2>, dim3(1), dim3(nt), 0, 0, a, dpos, c, out); break;
                 case 3: hipLaunchKernelGGL(k_probe<3>, dim3(1), dim3(nt), 0, 0, a, dpos, c, out); break;
-                default: hipLaunchKernelGGL(k_probe<4>, dim3(1), dim3(nt), 0, 0, a, dpos, c, out); break;
+                case 4: hipLaunchKernelGGL(k_probe<4>, dim3(1), dim3(nt), 0, 0, a, dpos, c, out); break;
+                default: hipLaunchKernelGGL(k_probe<5>, dim3(1), dim3(nt), 0, 0, a, dpos, c, out); break;
             }
-            uint64_t h[2];
-            hipMemcpy(h, out, 16, hipMemcpyDeviceToHost);
+            uint64_t h[3];
+            hipMemcpy(h, out, 24, hipMemcpyDeviceToHost);
+            if (var == 0 && r == 6)
+                std::printf("core clock: %llu clocks in %llu real-time ticks (100 MHz): %.0f MHz\n",
+                            static_cast<unsigned long long>(h[0]), static_cast<unsigned long long>(h[2]),
+                            100.0 * static_cast<double>(h[0]) / static_cast<double>(h[2]));
             if (h[0] < best) best = h[0];
+            if (r == 0) first = h[0];
             acc = h[1];
         }
-        std::printf("%-24s threads %4d: %llu clocks for %d candidates (%d batches, %llu accepted): %.0f per batch\n",
-                    names[var], nt, static_cast<unsigned long long>(best), c, (c + 63) / 64, static_cast<unsigned long long>(acc),
+        std::printf("%-24s threads %4d: first launch %llu, best %llu clocks for %d candidates (%d batches, %llu accepted): %.0f per batch\n",
+                    names[var], nt, static_cast<unsigned long long>(first), static_cast<unsigned long long>(best), c, (c + 63) / 64, static_cast<unsigned long long>(acc),
                     static_cast<double>(best) / ((c + 63) / 64));
     }
     return 0;
