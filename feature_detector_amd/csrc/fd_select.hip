@@ -89,9 +89,16 @@ constexpr int kSubChunkFast = kSelectChunk;
 #define FD_KO 0
 #endif
 // Phase-cost diagnostic builds only (-DFD_KO=mask; results are wrong): 1 = no greedy (the frame stops
-// after its first sub-chunk), 2 = no conflict masks, 4 = no tie bits, 8 = bucket placement without the
-// rank scan (group slot order), 16 = place() without the position decode.
+// after its first sub-chunk), 2 = no conflict masks, 4 = no tie bits, 16 = place() without the
+// position decode.
 constexpr int kKnockOut = FD_KO;
+#ifndef FD_EXIT
+#define FD_EXIT 0
+#endif
+// Phase-cost diagnostic builds only (-DFD_EXIT=n; no outputs): k_select returns after phase n (1 the
+// histogram scan and first cut, 2 the first gather, 3 the first sub-chunk's ordering), so that the
+// differences of the kernel times are the phases' costs without clock stamps.
+constexpr int kExitAt = FD_EXIT;
 constexpr int kBucketMax = 64;  // largest bin of a sub-chunk ordered by bucket placement (else merge sort)
 // k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
 // with 256 threads (4x the items per wave) the headline frame's selection measured 1.3x slower.
@@ -255,6 +262,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         if (tid == 0) a.out_counts[f] = 0;
         return;
     }
+    if (kExitAt == 9) return;  // (diagnostic: launch and prologue only)
 
     // In-place suffix sums of S[0..nb) by the whole block; S[nb] = 0.
     auto suffix = [&](uint32_t *S, int nb) {
@@ -610,6 +618,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             lo_b = first_le(suf0, 0, kHistBins, 0u, static_cast<uint32_t>(kSelectChunk));
         first_lo = lo_b;
         FD_STAMP(21);
+        if (kExitAt == 1) return;
         if (lo_b < kHistBins && suf0[lo_b] > 0) {
             const uint32_t want = suf0[lo_b];
             if (a.pre_keys && a.pre_count[f] == want) {  // k_gather's result (previous kernel)
@@ -637,6 +646,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         }
     }
     FD_STAMP(22);
+    if (kExitAt == 2) return;
     if (use_grid && grid_in_lds) {  // the first round's LDS-direct loads are consumed (or never used)
         // vmcnt(0): no load still landing in this space (only if they were issued: the wait would
         // also hold for this thread's outstanding global stores and atomics, a memory round trip)
@@ -646,6 +656,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         __syncthreads();
     }
     FD_STAMP(3);
+    if (kExitAt == 4) return;
     int level = 0;
     int hi = (1 << lvl_width(0)) - 1;
     for (int64_t iter = 0;; ++iter) {
@@ -921,6 +932,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         s_b1 = S[bin + 1];
                         big = s_b - s_b1 > static_cast<uint32_t>(kBucketMax);
                     }
+                    if (kExitAt == 5) return;
                     if (ballot(big) != 0ull && lane == 0) L.vote[0] = 1u;
                     if (scan_fast && tid < kScanBatches) sl.cnt[tid] = 0u;  // (the last scan's reads are barriers ago)
                     __syncthreads();
@@ -932,12 +944,11 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                         }
                         __syncthreads();
                         FD_STAMP(11);  // bucket scatter
+                        if (kExitAt == 6) return;
                         if (tid < c) {
                             const uint32_t g0 = s_b1 - sbase, gn = s_b - s_b1;
                             uint32_t r = 0;
-                            if (kKnockOut & 8) {
-                                r = slot - g0;  // (diagnostic build: group slot instead of rank)
-                            } else if (!a.dup_keys) {
+                            if (!a.dup_keys) {
                                 for (uint32_t j0 = 0; j0 < gn; j0 += 8) {  // 8 loads in flight (clamped to the group)
                                     uint64_t v[8];
 #pragma unroll
@@ -1019,9 +1030,17 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                             if (tid + j * nthr >= c) continue;
                             const uint32_t g0 = lcnt[dg[j] + 1], gn = lcnt[dg[j]] - g0;
                             uint32_t r = 0;
-                            for (uint32_t q = 0; q < gn; ++q) {
-                                const uint64_t v = tmp[g0 + q];
-                                r += (v > kk[j] || (v == kk[j] && q < sl[j])) ? 1u : 0u;
+                            // 8 loads in flight (clamped to the group; a group is usually a few keys):
+                            // not a chain of dependent LDS round trips
+                            for (uint32_t q0 = 0; q0 < gn; q0 += 8) {
+                                uint64_t v[8];
+#pragma unroll
+                                for (uint32_t u = 0; u < 8; ++u) v[u] = tmp[g0 + min(q0 + u, gn - 1)];
+#pragma unroll
+                                for (uint32_t u = 0; u < 8; ++u) {
+                                    const uint32_t q = q0 + u;
+                                    r += (q < gn && (v[u] > kk[j] || (v[u] == kk[j] && q < sl[j]))) ? 1u : 0u;
+                                }
                             }
                             pos[j] = g0 + r;
                         }
@@ -1106,6 +1125,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     L.vote[1] = 0u;
                 }
                 FD_STAMP(14);  // conflict masks
+                if (kExitAt == 3) return;
                 // greedy scan in order by wave 0 (SelectGoodFeatures :62-72); ties checked unless the
                 // order of equal responses is defined (SuperPoint's multimap)
                 if (kKnockOut & 1) {  // (phase-cost diagnostic build: no greedy, the frame ends here)
