@@ -77,17 +77,24 @@ def select_phase_cycles():
         return None
     try:
         with open(STAMPS_FILE) as fh:
-            line = next(l for l in fh if l.startswith("k_select cycles:"))
+            lines = fh.readlines()
+        i = next(k for k, l in enumerate(lines) if l.startswith("k_select cycles:"))
     except (OSError, StopIteration):
         return None
-    toks = line.replace("|", " ").split()[2:]
+    toks = lines[i].replace("|", " ").split()[2:]
     ph = {}
     for k, v in zip(toks[0::2], toks[1::2]):
         if v.isdigit() and k not in ("subkeys", "chunks", "descents", "subchunks"):
             ph[k] = int(v)
+    # the wave-serial scan (fine slots 26 / 27: its first batch and the others) when the line below has them
+    fine = lines[i + 1].split()[1:] if i + 1 < len(lines) and lines[i + 1].strip().startswith("fine:") else []
+    if len(fine) >= 12 and all(f.isdigit() for f in fine):
+        ph["scan_first_batch"] = int(fine[10])
+        ph["scan_other_batches"] = int(fine[11])
     tot = sum(ph.values())
+    serial = ph.get("greedy", 0) + ph.get("scan_first_batch", 0) + ph.get("scan_other_batches", 0)
     return {"source": os.path.relpath(STAMPS_FILE, ROOT), "cycles": ph,
-            "greedy_share": round(ph.get("greedy", 0) / tot, 3) if tot else None}
+            "greedy_share": round(serial / tot, 3) if tot else None}
 
 
 def north_star_issue():
