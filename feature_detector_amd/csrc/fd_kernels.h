@@ -166,6 +166,7 @@ struct RefSortArgs {
     uint32_t *wcnt;  // [batch][kRefWideGroups][2] per-workgroup counts of the prelude
     uint32_t *wfr;   // [1 + batch] the prelude's compact list: count, flagged frames
     int wide;        // set by the launcher: the prelude ran (push order and the first levels are done)
+    int order_only;  // the visiting order alone (ord, every window; no greedy, no outputs): LSD seed order
 };
 
 // fd_points_select: caller candidates (response, x, y at [f * stride], counts[f]) -> list format.
@@ -297,6 +298,11 @@ hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int 
 // libstdc++ std::sort order emulated on the GPU for the frames k_select flagged (FD_FRAME_TIES)
 // wide: run the multi-workgroup prelude first (r.ctl, r.wcnt set): frames of >= 1 Mpx
 hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r, int batch, bool wide, hipStream_t s);
+// fd_lsd_lines: the reference's seed order (std::sort of the scan-ordered valid list by norm, descending,
+// feature_line_detector.cpp:88-94) of every frame into r.ord: the compact lists (frame_base, idx, lnorm)
+// into the list format of `a` (push order), then k_select_reference with order_only.
+hipError_t launch_lsd_seed_order(const int64_t *frame_base, const int32_t *idx, const float *lnorm, const SelectArgs &a,
+                                 const RefSortArgs &r, int batch, bool wide, hipStream_t s);
 hipError_t launch_cand_lists(const CandInArgs &a, int64_t max_count, hipStream_t s);
 hipError_t launch_nn_pick(const NnPickArgs &a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs &a, int batch, hipStream_t s);

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <memory>
 #include <thread>
@@ -35,8 +36,13 @@ namespace {
 
 constexpr float kPi = 3.14159265358979323846f;  // kPai (slam_basic_math.h)
 constexpr float k2Pi = 2.0f * kPi;               // k2Pai
-constexpr uint8_t kUsed = 1, kOccupied = 2;
+constexpr uint8_t kUsed = 1, kOccupied = 2, kSeen = 4;  // (kSeen: order_seeds' permutation check only)
 constexpr int kRing = 1000;  // CircularBuffer<PixelParam *, 1000> (feature_line_detector.h:76-77)
+#ifdef FD_LINES_PHASES
+}  // namespace
+std::atomic<long long> g_phase_ns[3];  // load (incl. sort), sort, grow + fit
+namespace {
+#endif
 
 float wrap_diff(float a, float b) {  // Utility::AngleDiffInRad (assumed: wrap a - b into [-pi, pi])
     float d = a - b;
@@ -82,8 +88,19 @@ public:
     }
 
     // One frame: returns the number of rectangles (writes at most stride of them).
-    int32_t run(const FrameList &fl, fd_lsd_rect *out, int32_t stride, uint8_t *used_out) {
+    // order: this frame's seed order from the GPU, or null (host sort); obtained through get_order after
+    // the frame's setup.
+    template <typename GetOrder>
+    int32_t run(const FrameList &fl, fd_lsd_rect *out, int32_t stride, uint8_t *used_out, GetOrder get_order) {
+#ifdef FD_LINES_PHASES  // diagnostic build only (tools/calib/lines_host_timing.cpp)
+        const auto t0 = std::chrono::steady_clock::now();
+#endif
         load(fl);
+        order_seeds(get_order());
+#ifdef FD_LINES_PHASES
+        const auto t1 = std::chrono::steady_clock::now();
+        g_phase_ns[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+#endif
         int32_t nrect = 0;
         for (const auto &seed : seeds_) {  // :27-46
             const int32_t s = seed.second;
@@ -103,6 +120,9 @@ public:
             if (nrect < stride) out[nrect] = r;
             ++nrect;
         }
+#ifdef FD_LINES_PHASES
+        g_phase_ns[2] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
+#endif
         if (used_out)
             for (int64_t k = 0; k < fl.n; ++k) used_out[k] = (state_[k] & kUsed) ? 1 : 0;
         for (int64_t k = 0; k < fl.n; ++k) mask_[static_cast<size_t>(fl.idx[k]) >> 6] = 0ull;  // clean for the next frame
@@ -127,16 +147,46 @@ private:
             entry_of_[static_cast<size_t>(i)] = static_cast<int32_t>(k);
             row_[k] = i / pc_;
             col_[k] = i - row_[k] * pc_;
-            seeds_[k] = {fl.norm[k], static_cast<int32_t>(k)};
             // glibc cosf / sinf of the angle: GrowRegion calls them whenever a pixel seeds or joins a
             // region, which happens many times per pixel (rejected regions release their pixels);
             // the same call on the same value, made once
             cos_[k] = std::cos(fl.angle[k]);
             sin_[k] = std::sin(fl.angle[k]);
         }
-        // sorted_pixels_: the scan-ordered list under the reference's comparator (:92-94)
-        std::sort(seeds_.begin(), seeds_.end(),
-                  [](const std::pair<float, int32_t> &a, const std::pair<float, int32_t> &b) { return a.first > b.first; });
+    }
+
+    // sorted_pixels_: the scan-ordered list under the reference's comparator (:92-94). The GPU's order
+    // (the same libstdc++ introsort permutation, emulated by k_select_reference) is taken when it is a
+    // permutation of this frame's valid pixels; otherwise, and without one, std::sort here.
+    void order_seeds(const uint32_t *ord) {
+#ifdef FD_LINES_PHASES
+        const auto ts = std::chrono::steady_clock::now();
+#endif
+        const size_t n = seeds_.size();
+        bool ok = ord != nullptr;
+        for (size_t k = 0; ok && k < n; ++k) {
+            const uint32_t i = ord[k];
+            if (i >= static_cast<uint32_t>(words_ * 64) || !((mask_[i >> 6] >> (i & 63)) & 1ull)) {
+                ok = false;
+                break;
+            }
+            const int32_t e = entry_of_[i];
+            if (state_[e] & kSeen) {
+                ok = false;
+                break;
+            }
+            state_[e] |= kSeen;
+            seeds_[k].second = e;
+        }
+        for (uint8_t &v : state_) v = 0;  // (kSeen cleared; nothing else is set before the growing)
+        if (!ok) {
+            for (size_t k = 0; k < n; ++k) seeds_[k] = {norm_[k], static_cast<int32_t>(k)};
+            std::sort(seeds_.begin(), seeds_.end(),
+                      [](const std::pair<float, int32_t> &a, const std::pair<float, int32_t> &b) { return a.first > b.first; });
+        }
+#ifdef FD_LINES_PHASES
+        g_phase_ns[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - ts).count();
+#endif
     }
 
     // TryToAddPixelIntoCandidates (:156-161) for the 8 neighbours of entry e, in the reference's order
@@ -266,13 +316,25 @@ uint32_t min_region_size(int rows, int cols, float tol_rad) {
 }
 
 void detect_lines(int rows, int cols, const fd_lsd_opts &o, const FrameList *frames, int batch, fd_lsd_rect *out,
-                  int32_t stride, int32_t *counts, uint8_t *used0, int threads) {
+                  int32_t stride, int32_t *counts, uint8_t *used0, int threads, const SeedOrder *seeds) {
     threads = std::max(1, std::min(threads, batch));
     std::atomic<int> next{0};
     auto worker = [&]() {
         FrameLines fl(rows, cols, o);
-        for (int f = next.fetch_add(1); f < batch; f = next.fetch_add(1))
-            counts[f] = fl.run(frames[f], out + static_cast<int64_t>(f) * stride, stride, f == 0 ? used0 : nullptr);
+        bool waited = false;
+        for (int f = next.fetch_add(1); f < batch; f = next.fetch_add(1)) {
+            auto get_order = [&]() -> const uint32_t * {
+                if (!seeds) return nullptr;
+                if (!waited) {
+                    seeds->wait();
+                    waited = true;
+                }
+                const uint32_t st = seeds->status[f];
+                if (!(st & FD_FRAME_RESOLVED) || (st & (FD_FRAME_UNRESOLVED | FD_FRAME_GUARD))) return nullptr;
+                return seeds->ord + static_cast<int64_t>(f) * seeds->stride;
+            };
+            counts[f] = fl.run(frames[f], out + static_cast<int64_t>(f) * stride, stride, f == 0 ? used0 : nullptr, get_order);
+        }
     };
     if (threads == 1) {
         worker();

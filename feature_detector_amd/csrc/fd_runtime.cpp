@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -63,6 +64,13 @@ struct fd_ctx {
     // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
     DevBuf l_lnorm, l_langle, l_fbase;
     HostBuf h_idx, h_norm, h_angle;
+    // fd_lsd_lines' seed order on the GPU: lists in the selection's format, status + counts, the orders'
+    // and statuses' pinned host copies; a side stream (the sort overlaps the lists' copy and the host
+    // setup) and its two events (lists ready -> sort; sort copied back)
+    DevBuf l_sresp, l_sidx, l_sst;
+    HostBuf h_ord, h_sst;
+    hipStream_t aux = nullptr;
+    hipEvent_t l_ev0 = nullptr, l_ev1 = nullptr;
     HostBuf h_png;  // fd_png_frames: decoded samples of a batch (pinned)
     DevBuf d_png;
     std::vector<int32_t> st_idx;
@@ -850,11 +858,16 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
                       &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
                       &c->l_lnorm,  &c->l_langle, &c->l_fbase, &c->wide_keys, &c->r_x, &c->r_lpos,
-                      &c->r_rpos,   &c->r_ord,    &c->r_ctl,       &c->r_wcnt,      &c->r_wfr};
-    for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle, &c->h_png}) release(*b);
+                      &c->r_rpos,   &c->r_ord,    &c->r_ctl,       &c->r_wcnt,      &c->r_wfr,
+                      &c->l_sresp,  &c->l_sidx,   &c->l_sst};
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
+    for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle, &c->h_png, &c->h_ord, &c->h_sst}) release(*b);
     release(c->d_png);
     for (DevBuf *b : bufs) release(*b);
     if (c->xev) (void)hipEventDestroy(c->xev);
+    if (c->l_ev0) (void)hipEventDestroy(c->l_ev0);
+    if (c->l_ev1) (void)hipEventDestroy(c->l_ev1);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -1436,6 +1449,52 @@ int fd_lsd_map_pitched(fd_ctx *c, const uint8_t *frames, int frames_on_device, i
     return FD_OK;
 }
 
+namespace {
+
+// fd_lsd_lines' seed order (sorted_pixels_, feature_line_detector.cpp:88-94) on a side stream, once the
+// compact lists exist: k_select_reference in push order over each frame's (norm, map index) list, the
+// orders and statuses copied to c->h_ord / c->h_sst, c->l_ev1 recorded after the copies. The context
+// stream does not wait for it: fd_lsd_lines waits on l_ev1 before it returns.
+int lsd_seed_order(fd_ctx *c, int batch, int map_rows, int map_cols, const std::vector<int64_t> &base,
+                   const fdk::LsdArgs &la, int64_t &ord_stride) {
+    int64_t cap = 1;
+    for (int b = 0; b < batch; ++b) cap = std::max(cap, base[static_cast<size_t>(b) + 1] - base[static_cast<size_t>(b)]);
+    if (cap >= (int64_t(1) << 30)) return fail(c, FD_ERR_INVALID, "LSD frame with >= 2^30 valid pixels");
+    if (!c->aux) FD_HIP_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    if (!c->l_ev0) FD_HIP_TRY(c, hipEventCreateWithFlags(&c->l_ev0, hipEventDisableTiming));
+    if (!c->l_ev1) FD_HIP_TRY(c, hipEventCreateWithFlags(&c->l_ev1, hipEventDisableTiming));
+    const size_t nb = static_cast<size_t>(batch);
+    FD_HIP_TRY(c, ensure(c, c->l_sresp, sizeof(float) * static_cast<size_t>(cap) * nb));
+    FD_HIP_TRY(c, ensure(c, c->l_sidx, sizeof(uint32_t) * static_cast<size_t>(cap) * nb));
+    FD_HIP_TRY(c, ensure(c, c->l_sst, sizeof(uint32_t) * 2 * nb));
+    fdk::RefSortArgs r{};
+    const int rc = ref_buffers(c, batch, map_rows, map_cols, cap, r);
+    if (rc) return rc;
+    FD_HIP_TRY(c, ensure_host(c->h_ord, sizeof(uint32_t) * static_cast<size_t>(r.cap) * nb));
+    FD_HIP_TRY(c, ensure_host(c->h_sst, sizeof(uint32_t) * nb));
+    fdk::SelectArgs s{};
+    s.list_resp = as<float>(c->l_sresp);
+    s.list_idx = as<uint32_t>(c->l_sidx);
+    s.list_cap = cap;
+    s.rows = map_rows;
+    s.cols = map_cols;
+    s.need = 0xFFFFFFFFu;
+    s.status = as<uint32_t>(c->l_sst);
+    s.cand_n = s.status + batch;
+    const bool wide = static_cast<int64_t>(map_rows) * map_cols >= (int64_t{1} << 20);
+    FD_HIP_TRY(c, hipEventRecord(c->l_ev0, c->stream));  // after the lists (k_lsd_scatter + k_lsd_values)
+    FD_HIP_TRY(c, hipStreamWaitEvent(c->aux, c->l_ev0, 0));
+    FD_HIP_TRY(c, fdk::launch_lsd_seed_order(la.frame_base, la.idx, la.lnorm, s, r, batch, wide, c->aux));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->h_ord.p, r.ord, sizeof(uint32_t) * static_cast<size_t>(r.cap) * nb,
+                                 hipMemcpyDeviceToHost, c->aux));
+    FD_HIP_TRY(c, hipMemcpyAsync(c->h_sst.p, s.status, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost, c->aux));
+    FD_HIP_TRY(c, hipEventRecord(c->l_ev1, c->aux));
+    ord_stride = r.cap;
+    return FD_OK;
+}
+
+}  // namespace
+
 int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int batch, int rows, int cols,
                  const fd_lsd_opts *opts, uint32_t needed, fd_lsd_rect *out_rects, int32_t rect_stride,
                  int32_t *out_counts, int threads) {
@@ -1453,7 +1512,12 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     c->st_used.clear();
     for (int b = 0; b < batch; ++b) out_counts[b] = 0;
     if (needed == 0) return FD_OK;  // :15
-    static const bool timing = ab_env("FD_LINES_TIMING") != nullptr;  // diagnostic: phase times to stderr
+    if (c->aux) FD_HIP_TRY(c, hipStreamSynchronize(c->aux));  // (a failed earlier call's seed sort: drained)
+    const bool timing = ab_env("FD_LINES_TIMING") != nullptr;  // diagnostic: phase times to stderr
+    // FD_LSD_HOST_SORT=1 (A/B): the seed order by std::sort on the host workers instead of the GPU
+    const bool host_sort = ab_env("FD_LSD_HOST_SORT") && std::atoi(ab_env("FD_LSD_HOST_SORT")) != 0;
+    bool gpu_seeds = false;
+    int64_t ord_stride = 0;
     const auto t_start = std::chrono::steady_clock::now();
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const uint8_t *dframes = nullptr;
@@ -1490,6 +1554,11 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
             a.lnorm = as<float>(c->l_lnorm);
             a.langle = as<float>(c->l_langle);
             FD_HIP_TRY(c, fdk::launch_lsd_scatter(a, c->stream));
+            if (!host_sort) {
+                const int rc2 = lsd_seed_order(c, batch, rows - 1, cols - 1, base, a, ord_stride);
+                if (rc2) return rc2;
+                gpu_seeds = true;
+            }
             FD_HIP_TRY(c, ensure_host(c->h_idx, sizeof(int32_t) * total));
             FD_HIP_TRY(c, ensure_host(c->h_norm, sizeof(float) * total));
             FD_HIP_TRY(c, ensure_host(c->h_angle, sizeof(float) * total));
@@ -1513,14 +1582,35 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     }
     const int64_t n0 = fl[0].n;
     c->st_used.assign(static_cast<size_t>(n0), 0);
+    // the workers wait for the GPU's seed orders after their first frame's setup (once per call)
+    std::once_flag seeds_once;
+    hipError_t seeds_err = hipSuccess;
+    fdl::SeedOrder so{static_cast<const uint32_t *>(c->h_ord.p), ord_stride, static_cast<const uint32_t *>(c->h_sst.p),
+                      [&]() {
+                          std::call_once(seeds_once, [&]() {
+                              seeds_err = hipEventSynchronize(c->l_ev1);
+                              if (seeds_err != hipSuccess)  // (reported below; the frames sort on the host)
+                                  std::memset(c->h_sst.p, 0, sizeof(uint32_t) * static_cast<size_t>(batch));
+                          });
+                      }};
     fdl::detect_lines(rows, cols, *opts, fl.data(), batch, out_rects, rect_stride, out_counts, c->st_used.data(),
-                      threads > 0 ? threads : default_line_threads());
+                      threads > 0 ? threads : default_line_threads(), gpu_seeds ? &so : nullptr);
+    if (gpu_seeds) {
+        so.wait();  // (every worker waited unless none ran a frame) the side stream's work is done
+        FD_HIP_TRY(c, seeds_err);
+    }
     if (timing) {
         const auto t_end = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[fd_lsd_lines] batch %d: gpu+d2h %.3f ms, host %.3f ms, valid %lld\n", batch,
+        int on_gpu = 0;
+        for (int b = 0; gpu_seeds && b < batch; ++b) {
+            const uint32_t st = static_cast<const uint32_t *>(c->h_sst.p)[b];
+            on_gpu += (st & FD_FRAME_RESOLVED) && !(st & (FD_FRAME_UNRESOLVED | FD_FRAME_GUARD));
+        }
+        std::fprintf(stderr, "[fd_lsd_lines] batch %d: gpu+d2h %.3f ms, host %.3f ms, valid %lld, seed orders from the "
+                             "gpu %d\n", batch,
                      std::chrono::duration<double, std::milli>(t_gpu - t_start).count(),
                      std::chrono::duration<double, std::milli>(t_end - t_gpu).count(),
-                     static_cast<long long>(base[static_cast<size_t>(batch)]));
+                     static_cast<long long>(base[static_cast<size_t>(batch)]), on_gpu);
     }
     if (n0 > 0) {
         c->st_idx.assign(fl[0].idx, fl[0].idx + n0);

@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             grid_ready = true;
             __syncthreads();
         }
-        for (uint32_t base = fin; base < fin_new; base += kSelectChunk) {
+        for (uint32_t base = fin; base < fin_new && !r.order_only; base += kSelectChunk) {
             if (L.s_done) break;
             const int cn = static_cast<int>(min(static_cast<uint32_t>(kSelectChunk), fin_new - base));
             for (int i = tid; i < cn; i += NT) {
@@ -1248,7 +1248,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         if (L.fail) {
             atomicOr(&a.status[f], FD_FRAME_UNRESOLVED);
         } else {
-            a.out_counts[f] = L.s_acc;
+            if (!r.order_only) a.out_counts[f] = L.s_acc;
             atomicOr(&a.status[f], FD_FRAME_RESOLVED);
         }
     }
@@ -1686,6 +1686,44 @@ hipError_t launch_select_reference(const SelectArgs &a, const RefSortArgs &r0, i
     }
     hipLaunchKernelGGL(k_select_reference<kRefThreads>, dim3(static_cast<unsigned>(batch)), dim3(kRefThreads), 0, s, a, r);
     return hipGetLastError();
+}
+
+namespace {
+
+// fd_lsd_lines' seed lists: frame f's compact run [frame_base[f], frame_base[f+1]) of (map index, norm)
+// into the list format at [f * list_cap] (the scan order is the push order), the frame flagged for
+// k_select_reference with its count.
+__global__ __launch_bounds__(256) void k_lsd_seed_lists(const int64_t *frame_base, const int32_t *idx, const float *lnorm,
+                                                        float *list_resp, uint32_t *list_idx, SelectArgs a) {
+    const int f = blockIdx.y;
+    const int64_t o = frame_base[f];
+    const int64_t n = min(frame_base[f + 1] - o, a.list_cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.status[f] = FD_FRAME_TIES;
+        a.cand_n[f] = static_cast<uint32_t>(n);
+    }
+    float *lr = list_resp + static_cast<int64_t>(f) * a.list_cap;
+    uint32_t *li = list_idx + static_cast<int64_t>(f) * a.list_cap;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
+        lr[i] = lnorm[o + i];
+        li[i] = static_cast<uint32_t>(idx[o + i]);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_lsd_seed_order(const int64_t *frame_base, const int32_t *idx, const float *lnorm, const SelectArgs &a,
+                                 const RefSortArgs &r0, int batch, bool wide, hipStream_t s) {
+    if (batch <= 0) return hipSuccess;
+    // (the selection reads its lists through const pointers; these are the runtime's list buffers)
+    hipLaunchKernelGGL(k_lsd_seed_lists, dim3(32, static_cast<unsigned>(batch)), dim3(256), 0, s, frame_base, idx, lnorm,
+                       const_cast<float *>(a.list_resp), const_cast<uint32_t *>(a.list_idx), a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    RefSortArgs r = r0;
+    r.push_order = 1;
+    r.order_only = 1;
+    return launch_select_reference(a, r, batch, wide, s);
 }
 
 }  // namespace fdk

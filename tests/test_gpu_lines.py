@@ -101,3 +101,28 @@ def test_config4_batch_spot_check(oracle):
     for seg in got:
         assert len(seg) > 0 and (seg[:, 6] >= 20).all()
         assert (seg[:, [0, 2]] > -2).all() and (seg[:, [0, 2]] < cols + 2).all()
+
+
+def test_seed_order_on_gpu(oracle, monkeypatch, capfd):
+    # the seed order (sorted_pixels_, feature_line_detector.cpp:88-94) comes from the GPU
+    # (k_select_reference in push order) for every frame, including a ramp whose norms are all equal
+    # (the introsort's equal-key paths) and frames large enough for the wide prelude; the segments are
+    # the oracle's and those of the host std::sort (FD_LSD_HOST_SORT=1)
+    import feature_detector_amd as fd
+
+    r, c = np.mgrid[0:400, 0:600]
+    ramp = ((r * 3 + c * 5) % 256).astype(np.uint8)
+    small = np.stack([ramp, oracle.make_frame("checker", 11, 400, 600, 24), oracle.make_frame("noise", 12, 400, 600, 16)])
+    big = oracle.make_frame("checker", 13, 1080, 1920, 64)[None]
+    monkeypatch.setenv("FD_DEBUG_AB", "1")
+    monkeypatch.setenv("FD_LINES_TIMING", "1")
+    for frames in (small, big):
+        capfd.readouterr()
+        got = _check(fd, oracle, frames)
+        err = capfd.readouterr().err
+        assert f"seed orders from the gpu {frames.shape[0]}" in err, err
+        monkeypatch.setenv("FD_LSD_HOST_SORT", "1")
+        host = fd.lsd_lines(frames)
+        assert "seed orders from the gpu 0" in capfd.readouterr().err
+        monkeypatch.delenv("FD_LSD_HOST_SORT")
+        assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(got, host))
