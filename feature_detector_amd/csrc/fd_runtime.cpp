@@ -62,8 +62,9 @@ struct fd_ctx {
     DevBuf r_x, r_lpos, r_rpos, r_ord, r_ctl, r_wcnt, r_wfr;  // FD_TIES_REFERENCE on the GPU (k_select_reference scratch)
     DevBuf run_lut;        // FAST score per 16-bit ring mask (FastOffsets::run_lut), filled once
     // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
-    DevBuf l_lnorm, l_langle, l_fbase;
-    HostBuf h_idx, h_norm, h_angle;
+    // (l_lists: one buffer of three sections, map index | norm | angle, copied back in one transfer)
+    DevBuf l_lists, l_fbase;
+    HostBuf h_lists;
     // fd_lsd_lines' seed order on the GPU: lists in the selection's format, status + counts, the orders'
     // and statuses' pinned host copies; a side stream (the sort overlaps the lists' copy and the host
     // setup) and its two events (lists ready -> sort; sort copied back)
@@ -857,11 +858,11 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
                       &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
-                      &c->l_lnorm,  &c->l_langle, &c->l_fbase, &c->wide_keys, &c->r_x, &c->r_lpos,
+                      &c->l_lists,  &c->l_fbase, &c->wide_keys, &c->r_x, &c->r_lpos,
                       &c->r_rpos,   &c->r_ord,    &c->r_ctl,       &c->r_wcnt,      &c->r_wfr,
                       &c->l_sresp,  &c->l_sidx,   &c->l_sst};
     if (c->aux) (void)hipStreamSynchronize(c->aux);
-    for (HostBuf *b : {&c->h_idx, &c->h_norm, &c->h_angle, &c->h_png, &c->h_ord, &c->h_sst}) release(*b);
+    for (HostBuf *b : {&c->h_lists, &c->h_png, &c->h_ord, &c->h_sst}) release(*b);
     release(c->d_png);
     for (DevBuf *b : bufs) release(*b);
     if (c->xev) (void)hipEventDestroy(c->xev);
@@ -1451,18 +1452,16 @@ int fd_lsd_map_pitched(fd_ctx *c, const uint8_t *frames, int frames_on_device, i
 
 namespace {
 
-// fd_lsd_lines' seed order (sorted_pixels_, feature_line_detector.cpp:88-94) on a side stream, once the
-// compact lists exist: k_select_reference in push order over each frame's (norm, map index) list, the
-// orders and statuses copied to c->h_ord / c->h_sst, c->l_ev1 recorded after the copies. The context
-// stream does not wait for it: fd_lsd_lines waits on l_ev1 before it returns.
+// fd_lsd_lines' seed order (sorted_pixels_, feature_line_detector.cpp:88-94) on a side stream, after
+// c->l_ev0 (recorded on the context stream once the compact lists exist): k_select_reference in push
+// order over each frame's (norm, map index) list, the orders and statuses copied to c->h_ord / c->h_sst,
+// c->l_ev1 recorded after the copies. The context stream does not wait for it: fd_lsd_lines waits on
+// l_ev1 before it returns.
 int lsd_seed_order(fd_ctx *c, int batch, int map_rows, int map_cols, const std::vector<int64_t> &base,
                    const fdk::LsdArgs &la, int64_t &ord_stride) {
     int64_t cap = 1;
     for (int b = 0; b < batch; ++b) cap = std::max(cap, base[static_cast<size_t>(b) + 1] - base[static_cast<size_t>(b)]);
     if (cap >= (int64_t(1) << 30)) return fail(c, FD_ERR_INVALID, "LSD frame with >= 2^30 valid pixels");
-    if (!c->aux) FD_HIP_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
-    if (!c->l_ev0) FD_HIP_TRY(c, hipEventCreateWithFlags(&c->l_ev0, hipEventDisableTiming));
-    if (!c->l_ev1) FD_HIP_TRY(c, hipEventCreateWithFlags(&c->l_ev1, hipEventDisableTiming));
     const size_t nb = static_cast<size_t>(batch);
     FD_HIP_TRY(c, ensure(c, c->l_sresp, sizeof(float) * static_cast<size_t>(cap) * nb));
     FD_HIP_TRY(c, ensure(c, c->l_sidx, sizeof(uint32_t) * static_cast<size_t>(cap) * nb));
@@ -1482,11 +1481,20 @@ int lsd_seed_order(fd_ctx *c, int batch, int map_rows, int map_cols, const std::
     s.status = as<uint32_t>(c->l_sst);
     s.cand_n = s.status + batch;
     const bool wide = static_cast<int64_t>(map_rows) * map_cols >= (int64_t{1} << 20);
-    FD_HIP_TRY(c, hipEventRecord(c->l_ev0, c->stream));  // after the lists (k_lsd_scatter + k_lsd_values)
     FD_HIP_TRY(c, hipStreamWaitEvent(c->aux, c->l_ev0, 0));
+    // order_only never reads ord back: the kernel may write it straight into the pinned host buffer
+    // (FD_LSD_ORD_MAPPED=0: a device buffer and a copy, A/B)
+    const char *mapped_env = ab_env("FD_LSD_ORD_MAPPED");
+    const bool mapped = !mapped_env || std::atoi(mapped_env) != 0;
+    if (mapped) {
+        void *dp = nullptr;
+        FD_HIP_TRY(c, hipHostGetDevicePointer(&dp, c->h_ord.p, 0));
+        r.ord = static_cast<uint32_t *>(dp);
+    }
     FD_HIP_TRY(c, fdk::launch_lsd_seed_order(la.frame_base, la.idx, la.lnorm, s, r, batch, wide, c->aux));
-    FD_HIP_TRY(c, hipMemcpyAsync(c->h_ord.p, r.ord, sizeof(uint32_t) * static_cast<size_t>(r.cap) * nb,
-                                 hipMemcpyDeviceToHost, c->aux));
+    if (!mapped)
+        FD_HIP_TRY(c, hipMemcpyAsync(c->h_ord.p, r.ord, sizeof(uint32_t) * static_cast<size_t>(r.cap) * nb,
+                                     hipMemcpyDeviceToHost, c->aux));
     FD_HIP_TRY(c, hipMemcpyAsync(c->h_sst.p, s.status, sizeof(uint32_t) * nb, hipMemcpyDeviceToHost, c->aux));
     FD_HIP_TRY(c, hipEventRecord(c->l_ev1, c->aux));
     ord_stride = r.cap;
@@ -1546,26 +1554,28 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         const int64_t total = base[static_cast<size_t>(batch)];
         if (total > 0) {
-            FD_HIP_TRY(c, ensure(c, c->l_idx, sizeof(int32_t) * total));
-            FD_HIP_TRY(c, ensure(c, c->l_lnorm, sizeof(float) * total));
-            FD_HIP_TRY(c, ensure(c, c->l_langle, sizeof(float) * total));
-            a.idx = as<int32_t>(c->l_idx);
+            const size_t sec = (static_cast<size_t>(total) + 63) & ~size_t(63);  // section length (entries)
+            FD_HIP_TRY(c, ensure(c, c->l_lists, sizeof(uint32_t) * 3 * sec));
+            FD_HIP_TRY(c, ensure_host(c->h_lists, sizeof(uint32_t) * 3 * sec));
+            a.idx = as<int32_t>(c->l_lists);
             a.idx_cap = total;
-            a.lnorm = as<float>(c->l_lnorm);
-            a.langle = as<float>(c->l_langle);
+            a.lnorm = reinterpret_cast<float *>(a.idx + sec);
+            a.langle = a.lnorm + sec;
             FD_HIP_TRY(c, fdk::launch_lsd_scatter(a, c->stream));
+            if (!host_sort) {
+                if (!c->aux) FD_HIP_TRY(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+                if (!c->l_ev0) FD_HIP_TRY(c, hipEventCreateWithFlags(&c->l_ev0, hipEventDisableTiming));
+                if (!c->l_ev1) FD_HIP_TRY(c, hipEventCreateWithFlags(&c->l_ev1, hipEventDisableTiming));
+                FD_HIP_TRY(c, hipEventRecord(c->l_ev0, c->stream));  // the lists exist (k_lsd_scatter + k_lsd_values)
+            }
+            // the lists back in one transfer (the PCIe-bound copy is enqueued before the seed sort, which
+            // runs beside it on the side stream)
+            FD_HIP_TRY(c, hipMemcpyAsync(c->h_lists.p, a.idx, sizeof(uint32_t) * 3 * sec, hipMemcpyDeviceToHost, c->stream));
             if (!host_sort) {
                 const int rc2 = lsd_seed_order(c, batch, rows - 1, cols - 1, base, a, ord_stride);
                 if (rc2) return rc2;
                 gpu_seeds = true;
             }
-            FD_HIP_TRY(c, ensure_host(c->h_idx, sizeof(int32_t) * total));
-            FD_HIP_TRY(c, ensure_host(c->h_norm, sizeof(float) * total));
-            FD_HIP_TRY(c, ensure_host(c->h_angle, sizeof(float) * total));
-            FD_HIP_TRY(c, hipMemcpyAsync(c->h_idx.p, a.idx, sizeof(int32_t) * total, hipMemcpyDeviceToHost, c->stream));
-            FD_HIP_TRY(c, hipMemcpyAsync(c->h_norm.p, a.lnorm, sizeof(float) * total, hipMemcpyDeviceToHost, c->stream));
-            FD_HIP_TRY(c, hipMemcpyAsync(c->h_angle.p, a.langle, sizeof(float) * total, hipMemcpyDeviceToHost,
-                                         c->stream));
             FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         }
     } else if (!frames_on_device) {
@@ -1574,8 +1584,9 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     const auto t_gpu = std::chrono::steady_clock::now();
     // host: region growing + rectangles, frames over worker threads
     std::vector<fdl::FrameList> fl(static_cast<size_t>(batch));
-    const int32_t *hidx = static_cast<const int32_t *>(c->h_idx.p);
-    const float *hn = static_cast<const float *>(c->h_norm.p), *ha = static_cast<const float *>(c->h_angle.p);
+    const size_t sec = (static_cast<size_t>(base[static_cast<size_t>(batch)]) + 63) & ~size_t(63);
+    const int32_t *hidx = static_cast<const int32_t *>(c->h_lists.p);
+    const float *hn = reinterpret_cast<const float *>(hidx + sec), *ha = hn + sec;
     for (int b = 0; b < batch; ++b) {
         const int64_t o = base[static_cast<size_t>(b)], n = base[static_cast<size_t>(b) + 1] - o;
         fl[static_cast<size_t>(b)] = fdl::FrameList{n ? hidx + o : nullptr, n ? hn + o : nullptr, n ? ha + o : nullptr, n};
@@ -1585,10 +1596,12 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     // the workers wait for the GPU's seed orders after their first frame's setup (once per call)
     std::once_flag seeds_once;
     hipError_t seeds_err = hipSuccess;
+    auto t_seeds = t_gpu;
     fdl::SeedOrder so{static_cast<const uint32_t *>(c->h_ord.p), ord_stride, static_cast<const uint32_t *>(c->h_sst.p),
                       [&]() {
                           std::call_once(seeds_once, [&]() {
                               seeds_err = hipEventSynchronize(c->l_ev1);
+                              t_seeds = std::chrono::steady_clock::now();
                               if (seeds_err != hipSuccess)  // (reported below; the frames sort on the host)
                                   std::memset(c->h_sst.p, 0, sizeof(uint32_t) * static_cast<size_t>(batch));
                           });
@@ -1606,10 +1619,11 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
             const uint32_t st = static_cast<const uint32_t *>(c->h_sst.p)[b];
             on_gpu += (st & FD_FRAME_RESOLVED) && !(st & (FD_FRAME_UNRESOLVED | FD_FRAME_GUARD));
         }
-        std::fprintf(stderr, "[fd_lsd_lines] batch %d: gpu+d2h %.3f ms, host %.3f ms, valid %lld, seed orders from the "
-                             "gpu %d\n", batch,
+        std::fprintf(stderr, "[fd_lsd_lines] batch %d: gpu+d2h %.3f ms, host %.3f ms (seed orders there at %.3f), valid "
+                             "%lld, seed orders from the gpu %d\n", batch,
                      std::chrono::duration<double, std::milli>(t_gpu - t_start).count(),
                      std::chrono::duration<double, std::milli>(t_end - t_gpu).count(),
+                     std::chrono::duration<double, std::milli>(t_seeds - t_gpu).count(),
                      static_cast<long long>(base[static_cast<size_t>(batch)]), on_gpu);
     }
     if (n0 > 0) {

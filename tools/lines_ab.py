@@ -1,6 +1,7 @@
 """A/B (diagnostic): fd_lsd_lines on BASELINE configs[3] (256 frames of 1920x1080 64-px checker + noise,
 the bench's frames), seed order on the GPU (default) against the host std::sort (FD_LSD_HOST_SORT=1),
-alternating, `reps` timed calls each; the library's phase line (FD_LINES_TIMING) goes to stderr.
+and with the order copied from a device buffer
+(FD_LSD_ORD_MAPPED=0) instead of written into pinned host memory, alternating, `reps` timed calls each; the library's phase line (FD_LINES_TIMING) goes to stderr.
 usage: python3 tools/lines_ab.py [reps] [batch]"""
 import os
 import sys
@@ -20,8 +21,9 @@ batch = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 frames = bench.make_frames(torch, "checker", batch, 1080, 1920, 0, "cuda", period=64)
 torch.cuda.synchronize()
 ref = None
-for mode in ("gpu", "host", "gpu", "host"):
+for mode in ("gpu", "gpu_copy", "host", "gpu", "gpu_copy", "host"):
     os.environ["FD_LSD_HOST_SORT"] = "1" if mode == "host" else "0"
+    os.environ["FD_LSD_ORD_MAPPED"] = "0" if mode == "gpu_copy" else "1"  # (gpu_copy: ord via a device buffer)
     segs = fd.lsd_lines(frames, max_lines=2048)  # warm
     torch.cuda.synchronize()
     t0 = time.perf_counter()

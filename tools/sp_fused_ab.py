@@ -36,8 +36,9 @@ def timed(reps=10):
     return e0.elapsed_time(e1) / reps
 
 
+MODES = os.environ.get("FD_AB_MODES", "fused,c1c64,c64_only64,no_c64,no_conv1,unfused").split(",")  # (subset: A/B of builds)
 for rnd in range(2):
-    for mode in ("fused", "c1c64", "c64_only64", "no_c64", "no_conv1", "unfused"):
+    for mode in MODES:
         for k in ("FD_SP_UNFUSED", "FD_SP_NO_CONV1", "FD_SP_NO_C64", "FD_SP_C64_ONLY64", "FD_SP_C1C64"):
             os.environ.pop(k, None)
         if mode == "c1c64":
