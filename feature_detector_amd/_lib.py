@@ -21,6 +21,7 @@ EXPORTS = (
     "fd_points_response_append", "fd_points_select",
     "fd_lsd_map", "fd_lsd_map_pitched", "fd_lsd_lines", "fd_lsd_lines_state", "fd_brief_compute", "fd_nn_select", "fd_nn_select_list", "fd_nn_descriptors",
     "fd_nn_bias_relu", "fd_nn_conv3x3_c1", "fd_nn_conv3x3_c64", "fd_nn_conv3x3_c1c64",
+    "fd_nn_heat_softmax", "fd_nn_desc_normalize",
     "fd_build_info", "fd_abi_version", "fd_png_info", "fd_png_decode", "fd_png_frames",
     "fd_ingest_create", "fd_ingest_destroy", "fd_ingest_frames", "fd_ingest_submit", "fd_ingest_wait",
 )
@@ -108,6 +109,8 @@ def load() -> ctypes.CDLL:
         "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
         "fd_nn_bias_relu": (i32, [P, P, P, i64, P, i32, i32, i32, i32, i32]),
         "fd_nn_conv3x3_c1": (i32, [P, P, P, P, i64, P, i32, i32, i32]),
+        "fd_nn_heat_softmax": (i32, [P, P, P, i32, i32, i32]),
+        "fd_nn_desc_normalize": (i32, [P, P, P, i64, i32]),
         "fd_nn_conv3x3_c64": (i32, [P, P, P, P, P, i32, i32, i32, i32, i32, i32]),
         "fd_nn_conv3x3_c1c64": (i32, [P, P, P, P, P, P, P, i32, i32, i32, i32]),
         "fd_build_info": (ctypes.c_char_p, []),

@@ -135,7 +135,91 @@ __global__ __launch_bounds__(256) void k_nn_desc(NnDescArgs a) {
     }
 }
 
+// SuperPoint's detector head after convPb (the network's own output stage: softmax over a cell's 65
+// channels, the dustbin dropped, pixel_shuffle(8) into the cell's 8x8 pixels), in one pass from the fp16
+// channels-last logits instead of PyTorch's float copy, softmax, slice and shuffle (four HBM passes over
+// the map). A workgroup takes 32 cells of one cell row: 8 lanes per cell hold 8 channels each (lane 0 of
+// the group also the dustbin), the max and the sum of exp(x - max) are reduced over the 8 lanes, and the
+// probabilities go through LDS so that each of the 8 output rows is written as one contiguous run.
+constexpr int kHeatCells = 32;
+__global__ __launch_bounds__(256) void k_nn_heat_softmax(const _Float16 *semi, float *heat, int hc, int wc) {
+    __shared__ float pr[kHeatCells][65];
+    const int tid = static_cast<int>(threadIdx.x), cell = tid >> 3, part = tid & 7;
+    const int j0 = static_cast<int>(blockIdx.x) * kHeatCells, i = static_cast<int>(blockIdx.y), b = static_cast<int>(blockIdx.z);
+    const int j = j0 + cell;
+    const bool in = j < wc;
+    const _Float16 *src = semi + ((static_cast<int64_t>(b) * hc + i) * wc + (in ? j : 0)) * 65;
+    float v[9];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = static_cast<float>(src[part * 8 + k]);
+    v[8] = part == 0 ? static_cast<float>(src[64]) : -INFINITY;
+    float m = v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, v[k]);
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float e[8], sum = part == 0 ? expf(v[8] - m) : 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        e[k] = expf(v[k] - m);
+        sum += e[k];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) sum += __shfl_xor(sum, o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pr[cell][part * 8 + k] = e[k] / sum;
+    __syncthreads();
+    const int64_t w = static_cast<int64_t>(wc) * 8;
+    float *dst = heat + (static_cast<int64_t>(b) * hc * 8 + static_cast<int64_t>(i) * 8) * w + static_cast<int64_t>(j0) * 8;
+    if (!in) return;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) dst[r * w + tid] = pr[cell][r * 8 + part];
+}
+
+// SuperPoint's descriptor head after convDb: each cell's c-channel vector divided by its L2 norm
+// (clamped to 1e-12), fp16 channels-last in, float channels-last out, one wave per cell (8 channels per
+// lane and round).
+__global__ __launch_bounds__(256) void k_nn_desc_normalize(const _Float16 *x, float *y, int64_t cells, int c) {
+    const int64_t cell = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (cell >= cells) return;
+    const int lane = lane_id(), groups = c >> 3;
+    typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+    const h8v *src = reinterpret_cast<const h8v *>(x + cell * c);
+    float ss = 0.0f;
+    for (int g = lane; g < groups; g += kWave) {
+        const h8v h = src[g];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ss += static_cast<float>(h[k]) * static_cast<float>(h[k]);
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) ss += __shfl_xor(ss, o);
+    const float nrm = fmaxf(sqrtf(ss), 1e-12f);
+    float4 *dst = reinterpret_cast<float4 *>(y + cell * c);
+    for (int g = lane; g < groups; g += kWave) {
+        const h8v h = src[g];
+        dst[2 * g] = make_float4(static_cast<float>(h[0]) / nrm, static_cast<float>(h[1]) / nrm, static_cast<float>(h[2]) / nrm,
+                                 static_cast<float>(h[3]) / nrm);
+        dst[2 * g + 1] = make_float4(static_cast<float>(h[4]) / nrm, static_cast<float>(h[5]) / nrm,
+                                     static_cast<float>(h[6]) / nrm, static_cast<float>(h[7]) / nrm);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_nn_heat_softmax(const void *semi, float *heat, int n, int hc, int wc, hipStream_t s) {
+    if (n <= 0 || hc <= 0 || wc <= 0) return hipSuccess;
+    const dim3 grid(static_cast<unsigned>((wc + kHeatCells - 1) / kHeatCells), static_cast<unsigned>(hc),
+                    static_cast<unsigned>(n));
+    hipLaunchKernelGGL(k_nn_heat_softmax, grid, dim3(256), 0, s, static_cast<const _Float16 *>(semi), heat, hc, wc);
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_desc_normalize(const void *x, float *y, int64_t cells, int c, hipStream_t s) {
+    if (cells <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_nn_desc_normalize, dim3(static_cast<unsigned>((cells + 3) / 4)), dim3(256), 0, s,
+                       static_cast<const _Float16 *>(x), y, cells, c);
+    return hipGetLastError();
+}
 
 hipError_t launch_heat_candidates(const HeatArgs &a, hipStream_t s) {
     if (a.blocks_per_frame == 0 || a.batch == 0) return hipSuccess;

@@ -143,8 +143,8 @@ __global__ __launch_bounds__(256) void k_conv3x3_c1_bias_relu(const _Float16 *x,
 // mfma_f32_16x16x32_f16 steps (fp16 products, f32 sums). One workgroup (4 waves) per CU keeps the packed
 // filter ([tap][co][ci], 72 KiB) in LDS and walks tiles of kCvRows rows x 64 columns: the tile's input
 // pixels are staged in LDS (16-byte chunks of 8 channels, XOR-swizzled by column so that 16 lanes reading
-// 16 pixels hit 8 distinct bank groups), each wave computes 16 columns x 4 rows x 64 channels (16
-// accumulators: 4 A and 4 B fragments per K step), and the epilogue rounds the sum to half, adds the
+// 16 pixels hit 8 distinct bank groups), each wave computes 16 columns x kCvRows rows x 64 channels
+// (4 kCvRows accumulators), and the epilogue rounds the sum to half, adds the
 // bias in float and rounds (as a bias-free convolution + fd_nn_bias_relu), applies the ReLU and the 2x2
 // max within the lane (the accumulator rows are adjacent pixels, the four row blocks adjacent rows),
 // stages the tile in LDS and writes it as whole 128-byte pixels.
@@ -153,8 +153,11 @@ __global__ __launch_bounds__(256) void k_conv3x3_c1_bias_relu(const _Float16 *x,
 #endif
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+#ifndef FD_C64_ROWREUSE
+#define FD_C64_ROWREUSE 1  // K loop by (dx, channel half) with the input rows reused by the three dy taps
+#endif
 #ifndef FD_C64_ROWS
-#define FD_C64_ROWS 4
+#define FD_C64_ROWS 8  // tile rows (with the row reuse: 4 rows 1,671 / 512 us, 8 rows 1,603 / 502 us for conv1b / conv2a)
 #endif
 constexpr int kCvRows = FD_C64_ROWS, kCvCols = 64, kCvInRows = kCvRows + 2, kCvInCols = kCvCols + 2;
 
@@ -289,6 +292,47 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
         for (int m = 0; m < kCvRows; ++m)
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) acc[m][nb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#if FD_C64_ROWREUSE
+        // K loop by (column shift dx, channel half) groups: the wave's A fragments for the group are the
+        // kCvRows + 2 input rows at that shift, loaded once and used by the three taps dy = 0..2 of the
+        // column (row m + dy), so each input fragment is read from LDS once per group instead of once
+        // per tap (A traffic per tile halved: 36 instead of 72 fragment loads at 4 rows). The next
+        // group's rows and the next tap's filter fragments are read ahead of the current MFMAs.
+        auto rows_at = [&](int g, h8 (&A)[kCvRows + 2]) {
+            const int dx = g >> 1, kh = g & 1;
+            const int chunk = kh * 4 + (lane >> 4);
+            const int pc = wv * 16 + (lane & 15) + dx;
+#pragma unroll
+            for (int r = 0; r < kCvRows + 2; ++r)
+                A[r] = __builtin_bit_cast(h8, In[(r * kCvInCols + pc) * 8 + (chunk ^ (pc & 7))]);
+        };
+        auto filt_at = [&](int g, int dy, h8 (&B)[4]) {
+            const int dx = g >> 1, kh = g & 1, tap = dy * 3 + dx;
+            const int chunk = kh * 4 + (lane >> 4);
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                const int co = nb * 16 + (lane & 15);
+                B[nb] = __builtin_bit_cast(h8, Wl[(tap * 64 + co) * 8 + (chunk ^ (co & 7))]);
+            }
+        };
+        h8 Ar[2][kCvRows + 2], Bf[2][4];
+        rows_at(0, Ar[0]);
+        filt_at(0, 0, Bf[0]);
+#pragma unroll
+        for (int g = 0; g < 6; ++g) {
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+                const int it = g * 3 + dy;
+                if (dy == 0 && g + 1 < 6) rows_at(g + 1, Ar[(g + 1) & 1]);
+                if (it + 1 < 18) filt_at(dy == 2 ? g + 1 : g, dy == 2 ? 0 : dy + 1, Bf[(it + 1) & 1]);
+#pragma unroll
+                for (int m = 0; m < kCvRows; ++m)
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ar[g & 1][m + dy], Bf[it & 1][nb], acc[m][nb], 0, 0, 0);
+            }
+        }
+#else
         // the 18 K steps (tap, channel half) with the next step's fragments read from LDS before this
         // step's matrix instructions, so the LDS latency hides behind them (one wave per SIMD: no other
         // wave would cover it)
@@ -323,6 +367,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
                 for (int nb = 0; nb < 4; ++nb)
                     acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1[m], B1[nb], acc[m][nb], 0, 0, 0);
         }
+#endif
         __syncthreads();  // (In is reused as the output staging)
         _Float16 *st = reinterpret_cast<_Float16 *>(In);
         const int col4 = wv * 16 + (lane >> 4) * 4;  // the accumulator's first pixel column in the tile

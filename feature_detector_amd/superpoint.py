@@ -214,6 +214,46 @@ def bias_relu(x, bias, pool: bool = False, out=None, ctx: Context | None = None)
     return out
 
 
+def heat_softmax(semi, ctx: Context | None = None):
+    """fd_nn_heat_softmax: SuperPoint's detector-head output from convPb's logits [N, 65, Hc, Wc]
+    (channels-last fp16, on the device): softmax over the 65 channels in float, the dustbin dropped,
+    pixel_shuffle(8) -> heat [N, 8 Hc, 8 Wc] float32, in one pass (PyTorch: float copy, softmax, slice,
+    shuffle). Within float rounding of torch.softmax(semi.float(), 1)[:, :-1] shuffled."""
+    import torch
+
+    if not (_is_torch_device_tensor(semi) and semi.dtype == torch.float16 and semi.dim() == 4 and semi.shape[1] == 65
+            and semi.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("heat_softmax: semi must be a channels-last float16 [N, 65, Hc, Wc] device tensor")
+    n, _, hc, wc = semi.shape
+    heat = torch.empty((n, 8 * hc, 8 * wc), dtype=torch.float32, device=semi.device)
+    ctx = _resolve_ctx(ctx, semi)
+    _bind_stream(ctx, True)
+    rc = _lib.load().fd_nn_heat_softmax(ctx.ptr, ctypes.c_void_p(semi.data_ptr()), ctypes.c_void_p(heat.data_ptr()),
+                                         int(n), int(hc), int(wc))
+    _lib.check(ctx.ptr, rc)
+    return heat
+
+
+def desc_normalize(desc, ctx: Context | None = None):
+    """fd_nn_desc_normalize: SuperPoint's descriptor-head output from convDb's [N, C, Hc, Wc] (channels-last
+    fp16, on the device): each cell's vector over its L2 norm (clamped to 1e-12) in float -> [N, C, Hc, Wc]
+    float32 channels-last, in one pass (PyTorch: float copy, norm, division). Within float rounding of
+    desc.float() / desc.float().norm(dim=1, keepdim=True).clamp_min(1e-12)."""
+    import torch
+
+    if not (_is_torch_device_tensor(desc) and desc.dtype == torch.float16 and desc.dim() == 4 and desc.shape[1] % 8 == 0
+            and desc.is_contiguous(memory_format=torch.channels_last)):
+        raise ValueError("desc_normalize: desc must be a channels-last float16 [N, C, Hc, Wc] device tensor, C % 8 == 0")
+    n, c, hc, wc = desc.shape
+    out = torch.empty((n, c, hc, wc), dtype=torch.float32, device=desc.device, memory_format=torch.channels_last)
+    ctx = _resolve_ctx(ctx, desc)
+    _bind_stream(ctx, True)
+    rc = _lib.load().fd_nn_desc_normalize(ctx.ptr, ctypes.c_void_p(desc.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                           int(n) * int(hc) * int(wc), int(c))
+    _lib.check(ctx.ptr, rc)
+    return out
+
+
 def conv1_bias_relu(x, weight, bias, out=None, ctx: Context | None = None):
     """fd_nn_conv3x3_c1: the encoder's first layer (1 input channel, 3x3, stride 1, padding 1) with its bias
     and ReLU in one pass: x [N, 1, H, W] fp16 on the device -> [N, C, H, W] fp16 channels-last. The 9
@@ -468,6 +508,16 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             x = self.relu(conv(x))
             return self.pool(x) if pool else x
 
+        @staticmethod
+        def fused_heads(semi, desc):
+            """The heads' output stages run as fd_nn_heat_softmax / fd_nn_desc_normalize when the logits are
+            channels-last fp16 on the device (FD_SP_UNFUSED=1 or FD_SP_TORCH_HEADS=1: PyTorch's ops, A/B)."""
+            return (semi.is_cuda and semi.dtype == torch.float16 and semi.shape[1] == 65
+                    and semi.is_contiguous(memory_format=torch.channels_last)
+                    and desc.is_cuda and desc.dtype == torch.float16 and desc.shape[1] % 8 == 0
+                    and desc.is_contiguous(memory_format=torch.channels_last)
+                    and not _ab_env("FD_SP_UNFUSED") and not _ab_env("FD_SP_TORCH_HEADS"))
+
         def first_layers(self, x):
             """conv1a -> ReLU -> conv1b -> ReLU -> MaxPool2d(2, 2), layer by layer through cbr (conv1a's
             write-bound pass, then conv1b on the matrix cores). The fused pass (conv1ab_bias_relu: conv1a
@@ -496,11 +546,15 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             x = self.cbr(self.conv2b, self.cbr(self.conv2a, x), pool=True)
             x = self.cbr(self.conv3b, self.cbr(self.conv3a, x), pool=True)
             x = self.cbr(self.conv4b, self.cbr(self.conv4a, x))
-            semi = self.convPb(self.cbr(self.convPa, x)).float()
-            prob = torch.softmax(semi, dim=1)[:, :-1]
-            heat = torch.nn.functional.pixel_shuffle(prob, 8)[:, 0]
-            desc = self.convDb(self.cbr(self.convDa, x)).float()
-            desc = desc / desc.norm(dim=1, keepdim=True).clamp_min(1e-12)
+            semi = self.convPb(self.cbr(self.convPa, x))
+            desc = self.convDb(self.cbr(self.convDa, x))
+            if self.fused_heads(semi, desc):  # the heads' output stages in one pass each (fd_nn.hip)
+                heat, desc = heat_softmax(semi), desc_normalize(desc)
+            else:
+                prob = torch.softmax(semi.float(), dim=1)[:, :-1]
+                heat = torch.nn.functional.pixel_shuffle(prob, 8)[:, 0]
+                desc = desc.float()
+                desc = desc / desc.norm(dim=1, keepdim=True).clamp_min(1e-12)
             if not nms:
                 return heat, desc
             kp, sc = top_k_keypoints(simple_nms(heat, 4), top_k)

@@ -411,3 +411,48 @@ def test_bias_relu_matches_torch(sp):
     dd = (desc - rdesc).abs().max().item()
     print(f"fused vs module forward: max |d heat| {dh:.3g} (max heat {rheat.max().item():.3g}), max |d desc| {dd:.3g}")
     assert torch.allclose(heat, rheat, rtol=2e-2, atol=2e-3) and torch.allclose(desc, rdesc, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_heads_match_torch(sp):
+    """fd_nn_heat_softmax (softmax over 65 channels, dustbin dropped, pixel_shuffle(8)) and
+    fd_nn_desc_normalize (per-cell L2 normalisation) on channels-last fp16 logits against PyTorch's float32
+    ops on the same values: within float rounding (the sums run in another order); ragged cell counts
+    (the 32-cell groups of the heat kernel), a 640x480 batch's 1/8 maps, extreme logits; the model's own
+    head tensors take the fused path; argument checks."""
+    import torch
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(31)
+    for n, hc, wc in ((1, 1, 1), (2, 3, 33), (3, 7, 64), (64, 60, 80)):
+        semi = (torch.randn((n, 65, hc, wc), generator=g, device="cuda") * 6).half().contiguous(memory_format=torch.channels_last)
+        ref = torch.nn.functional.pixel_shuffle(torch.softmax(semi.float(), dim=1)[:, :-1], 8)[:, 0]
+        got = sp.heat_softmax(semi)
+        assert tuple(got.shape) == (n, 8 * hc, 8 * wc) and got.dtype == torch.float32
+        assert torch.allclose(got, ref, rtol=1e-5, atol=1e-7), (n, hc, wc, (got - ref).abs().max().item())
+        for c in (8, 256):
+            d = (torch.randn((n, c, hc, wc), generator=g, device="cuda") * 3).half().contiguous(memory_format=torch.channels_last)
+            df = d.float()
+            refd = df / df.norm(dim=1, keepdim=True).clamp_min(1e-12)
+            gotd = sp.desc_normalize(d)
+            assert gotd.is_contiguous(memory_format=torch.channels_last) and gotd.dtype == torch.float32
+            assert torch.allclose(gotd, refd, rtol=1e-5, atol=1e-7), (n, c, (gotd - refd).abs().max().item())
+    big = torch.full((1, 65, 2, 2), 60000.0, device="cuda", dtype=torch.float16).contiguous(memory_format=torch.channels_last)
+    big[:, 3] = -60000.0
+    assert torch.allclose(sp.heat_softmax(big), torch.nn.functional.pixel_shuffle(
+        torch.softmax(big.float(), dim=1)[:, :-1], 8)[:, 0], rtol=1e-5, atol=1e-7)
+    zero = torch.zeros((1, 16, 2, 3), device="cuda", dtype=torch.float16).contiguous(memory_format=torch.channels_last)
+    assert torch.equal(sp.desc_normalize(zero), torch.zeros((1, 16, 2, 3), device="cuda"))
+    with pytest.raises(ValueError):
+        sp.heat_softmax(torch.zeros((1, 65, 2, 2), device="cuda", dtype=torch.float16))  # NCHW
+    with pytest.raises(ValueError):
+        sp.desc_normalize(torch.zeros((1, 12, 2, 2), device="cuda", dtype=torch.float16).contiguous(
+            memory_format=torch.channels_last))  # 12 channels
+    net = sp.build_net(0).cuda().eval().half().to(memory_format=torch.channels_last)
+    x = (torch.rand((2, 1, 96, 128), generator=g, device="cuda")).half().contiguous(memory_format=torch.channels_last)
+    with torch.inference_mode():
+        y = net.cbr(net.conv4b, net.cbr(net.conv4a, torch.zeros((2, 128, 12, 16), device="cuda", dtype=torch.float16)
+                                         .contiguous(memory_format=torch.channels_last)))
+        assert net.fused_heads(net.convPb(net.cbr(net.convPa, y)), net.convDb(net.cbr(net.convDa, y)))
+        heat, desc = net(x)
+    assert tuple(heat.shape) == (2, 96, 128) and tuple(desc.shape) == (2, 256, 12, 16)
