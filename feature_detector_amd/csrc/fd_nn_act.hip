@@ -161,10 +161,27 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int kCvRows = FD_C64_ROWS, kCvCols = 64, kCvInRows = kCvRows + 2, kCvInCols = kCvCols + 2;
 
-__device__ __forceinline__ float cv_epilogue(float acc, float b) {
-    const _Float16 v = static_cast<_Float16>(static_cast<float>(static_cast<_Float16>(acc)) + b);
-    return v > static_cast<_Float16>(0.0f) ? static_cast<float>(v) : 0.0f;
+// The epilogue on packed halves: the two sums rounded to half, the bias added in half (correctly rounded:
+// equal to the float add rounded to half for every pair of finite halves, checked exhaustively), the
+// ReLU as a max with +0 (a NaN gives 0) with the sign bit of a -0 cleared.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2v cv_pair(float a, float b, h2v bias2) {
+    const h2v v = h2v{static_cast<_Float16>(a), static_cast<_Float16>(b)};
+    return v + bias2;
 }
+__device__ __forceinline__ h2v cv_relu2(h2v v) {
+    v = __builtin_elementwise_max(v, h2v{static_cast<_Float16>(0.0f), static_cast<_Float16>(0.0f)});
+    uint32_t u = __builtin_bit_cast(uint32_t, v);
+    const uint32_t sgn = u & 0x80008000u;
+    u &= ~(sgn | (sgn - (sgn >> 15)));
+    return __builtin_bit_cast(h2v, u);
+}
+__device__ __forceinline__ _Float16 cv_relu1(_Float16 v) {
+    v = __builtin_elementwise_max(v, static_cast<_Float16>(0.0f));
+    const uint16_t u = __builtin_bit_cast(uint16_t, v);
+    return __builtin_bit_cast(_Float16, static_cast<uint16_t>((u & 0x8000u) ? 0u : u));
+}
+
 
 // FUSED (SuperPoint conv1a + conv1b, fd_nn_conv3x3_c1c64): the tile's 64-channel input is conv1a itself
 // (1 -> 64 channels, 3x3, bias, ReLU) recomputed from the one-channel frame rows the tile reaches (a
@@ -187,9 +204,9 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
         const int ch = i & 7, row = i >> 3, co = row & 63;
         Wl[row * 8 + (ch ^ (co & 7))] = wpk[i];
     }
-    float bv[4];
+    h2v bv2[4];
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) bv[nb] = static_cast<float>(bias[nb * 16 + (lane & 15)]);
+    for (int nb = 0; nb < 4; ++nb) bv2[nb] = h2v{bias[nb * 16 + (lane & 15)], bias[nb * 16 + (lane & 15)]};
     const int th = (h + kCvRows - 1) / kCvRows, tw = (w + kCvCols - 1) / kCvCols;
     const int total = n * th * tw;  // (< 2^31: checked on the host)
     // FUSED: this thread's conv1a channel group (8 channels) and its weights
@@ -224,14 +241,18 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
                     praw[k] = xf[(static_cast<int64_t>(f) * h + gy) * w + gx];
             }
         } else {
+            // through a buffer resource over the tile's frame: an out-of-frame chunk reads at an
+            // offset past the resource and gets zeros (no zero fill, 32-bit offsets; the host checks
+            // h * w * 128 < 2^31)
+            const auto rs = make_rsrc(x + static_cast<int64_t>(min(f, n - 1)) * h * w * 8, static_cast<uint32_t>(h * w * 128));
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 const int i = tid + k * 256;
                 const int ch = i & 7, px = i >> 3, pc = px % kCvInCols, pr = px / kCvInCols;
                 const int gy = r0 - 1 + pr, gx = c0 - 1 + pc;
-                pre[k] = u4{0u, 0u, 0u, 0u};
-                if (i < kChunks && tile < total && gy >= 0 && gy < h && gx >= 0 && gx < w)
-                    pre[k] = x[((static_cast<int64_t>(f) * h + gy) * w + gx) * 8 + ch];
+                const bool ok = i < kChunks && tile < total && gy >= 0 && gy < h && gx >= 0 && gx < w;
+                const int32_t off = ok ? ((gy * w + gx) * 8 + ch) * 16 : -1;
+                pre[k] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
             }
         }
     };
@@ -380,11 +401,11 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
                 for (int pr = 0; pr < kCvRows / 2; ++pr)
 #pragma unroll
                     for (int q = 0; q < 2; ++q) {
-                        const float v = fmaxf(fmaxf(cv_epilogue(acc[2 * pr][nb][2 * q], bv[nb]),
-                                                    cv_epilogue(acc[2 * pr][nb][2 * q + 1], bv[nb])),
-                                              fmaxf(cv_epilogue(acc[2 * pr + 1][nb][2 * q], bv[nb]),
-                                                    cv_epilogue(acc[2 * pr + 1][nb][2 * q + 1], bv[nb])));
-                        st[(pr * 32 + col4 / 2 + q) * 64 + co] = static_cast<_Float16>(v);
+                        // max of the four biased sums, then the ReLU (= the max of the four ReLUs, NaN
+                        // included: max skips a NaN unless all four are, and the ReLU maps that to 0)
+                        const h2v m2 = __builtin_elementwise_max(cv_pair(acc[2 * pr][nb][2 * q], acc[2 * pr][nb][2 * q + 1], bv2[nb]),
+                                                                 cv_pair(acc[2 * pr + 1][nb][2 * q], acc[2 * pr + 1][nb][2 * q + 1], bv2[nb]));
+                        st[(pr * 32 + col4 / 2 + q) * 64 + co] = cv_relu1(__builtin_elementwise_max(m2.x, m2.y));
                     }
             }
             __syncthreads();
@@ -402,8 +423,11 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
 #pragma unroll
                 for (int m = 0; m < kCvRows; ++m)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        st[(m * kCvCols + col4 + r) * 64 + co] = static_cast<_Float16>(cv_epilogue(acc[m][nb][r], bv[nb]));
+                    for (int r = 0; r < 4; r += 2) {
+                        const h2v v = cv_relu2(cv_pair(acc[m][nb][r], acc[m][nb][r + 1], bv2[nb]));
+                        st[(m * kCvCols + col4 + r) * 64 + co] = v.x;
+                        st[(m * kCvCols + col4 + r + 1) * 64 + co] = v.y;
+                    }
             }
             __syncthreads();
             for (int i = tid; i < kCvRows * kCvCols * 8; i += 256) {

@@ -2053,6 +2053,8 @@ int fd_nn_conv3x3_c64(fd_ctx *c, const void *x, const void *weight_packed, const
         return fail(c, FD_ERR_INVALID, "y_channels must be a multiple of 64 holding [y_offset, y_offset + 64)");
     if (static_cast<int64_t>(n) * ((h + 1) / 2) * ((w + 63) / 64) >= (int64_t(1) << 31))
         return fail(c, FD_ERR_INVALID, "too many tiles");
+    if (static_cast<int64_t>(h) * w * 128 >= (int64_t(1) << 31))  // (one frame's input: 32-bit buffer offsets)
+        return fail(c, FD_ERR_INVALID, "frame too large (h * w * 64 channels * 2 B must be < 2^31)");
     if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weight_packed) | reinterpret_cast<uintptr_t>(y)) & 15 ||
         reinterpret_cast<uintptr_t>(bias) & 1)
         return fail(c, FD_ERR_INVALID, "x, weight, y must be 16-byte aligned");
