@@ -109,8 +109,8 @@ def load() -> ctypes.CDLL:
         "fd_nn_descriptors": (i32, [P, P, i32, i32, i32, i32, i32, i32, P, P, i32, P, i32]),
         "fd_nn_bias_relu": (i32, [P, P, P, i64, P, i32, i32, i32, i32, i32]),
         "fd_nn_conv3x3_c1": (i32, [P, P, P, P, i64, P, i32, i32, i32]),
-        "fd_nn_heat_softmax": (i32, [P, P, P, i32, i32, i32]),
-        "fd_nn_desc_normalize": (i32, [P, P, P, i64, i32]),
+        "fd_nn_heat_softmax": (i32, [P, P, P, P, i32, i32, i32]),
+        "fd_nn_desc_normalize": (i32, [P, P, P, P, i64, i32]),
         "fd_nn_conv3x3_c64": (i32, [P, P, P, P, P, i32, i32, i32, i32, i32, i32]),
         "fd_nn_conv3x3_c1c64": (i32, [P, P, P, P, P, P, P, i32, i32, i32, i32]),
         "fd_build_info": (ctypes.c_char_p, []),

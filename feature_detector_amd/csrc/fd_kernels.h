@@ -316,8 +316,9 @@ hipError_t launch_nn_desc(const NnDescArgs &a, hipStream_t s);
 // SuperPoint heads: softmax + dustbin drop + pixel_shuffle(8) of the fp16 channels-last logits
 // [n][hc][wc][65] into heat [n][8hc][8wc] f32; L2 normalisation of fp16 channels-last cells [cells][c]
 // into f32 (c a multiple of 8)
-hipError_t launch_nn_heat_softmax(const void *semi, float *heat, int n, int hc, int wc, hipStream_t s);
-hipError_t launch_nn_desc_normalize(const void *x, float *y, int64_t cells, int c, hipStream_t s);
+// (bias, optional: the preceding convolution's bias added to its half output first, in half)
+hipError_t launch_nn_heat_softmax(const void *semi, const void *bias, float *heat, int n, int hc, int wc, hipStream_t s);
+hipError_t launch_nn_desc_normalize(const void *x, const void *bias, float *y, int64_t cells, int c, hipStream_t s);
 // (w1, b1 non-null: x is the one-channel frame and conv1a -- 1 -> 64, 3x3, bias, ReLU -- is fused in)
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
                               int y_channels, int y_offset, hipStream_t s, const void *w1 = nullptr,

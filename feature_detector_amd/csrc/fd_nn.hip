@@ -142,17 +142,21 @@ __global__ __launch_bounds__(256) void k_nn_desc(NnDescArgs a) {
 // the group also the dustbin), the max and the sum of exp(x - max) are reduced over the 8 lanes, and the
 // probabilities go through LDS so that each of the 8 output rows is written as one contiguous run.
 constexpr int kHeatCells = 32;
-__global__ __launch_bounds__(256) void k_nn_heat_softmax(const _Float16 *semi, float *heat, int hc, int wc) {
+__global__ __launch_bounds__(256) void k_nn_heat_softmax(const _Float16 *semi, const _Float16 *bias, float *heat, int hc,
+                                                         int wc) {
     __shared__ float pr[kHeatCells][65];
     const int tid = static_cast<int>(threadIdx.x), cell = tid >> 3, part = tid & 7;
     const int j0 = static_cast<int>(blockIdx.x) * kHeatCells, i = static_cast<int>(blockIdx.y), b = static_cast<int>(blockIdx.z);
     const int j = j0 + cell;
     const bool in = j < wc;
     const _Float16 *src = semi + ((static_cast<int64_t>(b) * hc + i) * wc + (in ? j : 0)) * 65;
+    // (bias: convPb's bias added to the bias-free convolution's half output, in half: a half add is the
+    // float add rounded to half)
     float v[9];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = static_cast<float>(src[part * 8 + k]);
-    v[8] = part == 0 ? static_cast<float>(src[64]) : -INFINITY;
+    for (int k = 0; k < 8; ++k)
+        v[k] = static_cast<float>(bias ? static_cast<_Float16>(src[part * 8 + k] + bias[part * 8 + k]) : src[part * 8 + k]);
+    v[8] = part == 0 ? static_cast<float>(bias ? static_cast<_Float16>(src[64] + bias[64]) : src[64]) : -INFINITY;
     float m = v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) m = fmaxf(m, v[k]);
@@ -179,24 +183,32 @@ __global__ __launch_bounds__(256) void k_nn_heat_softmax(const _Float16 *semi, f
 // SuperPoint's descriptor head after convDb: each cell's c-channel vector divided by its L2 norm
 // (clamped to 1e-12), fp16 channels-last in, float channels-last out, one wave per cell (8 channels per
 // lane and round).
-__global__ __launch_bounds__(256) void k_nn_desc_normalize(const _Float16 *x, float *y, int64_t cells, int c) {
-    const int64_t cell = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    if (cell >= cells) return;
-    const int lane = lane_id(), groups = c >> 3;
+// (bias, optional: convDb's bias added in half first, as for the heat). A cell of c <= 256 channels takes
+// c / 8 lanes (several cells per wave); wider cells one wave each.
+__global__ __launch_bounds__(256) void k_nn_desc_normalize(const _Float16 *x, const _Float16 *bias, float *y, int64_t cells,
+                                                           int c) {
+    const int groups = c >> 3;
+    const int span = groups <= 8 ? 8 : groups <= 16 ? 16 : groups <= 32 ? 32 : kWave;  // lanes per cell
+    const int per_wave = kWave / span, lane = lane_id(), sub = lane % span;
+    const int64_t cell = (static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6)) * per_wave + lane / span;
+    const bool in = cell < cells;
     typedef _Float16 h8v __attribute__((ext_vector_type(8)));
-    const h8v *src = reinterpret_cast<const h8v *>(x + cell * c);
+    const h8v *src = reinterpret_cast<const h8v *>(x + (in ? cell : 0) * c);
+    const h8v *bv = reinterpret_cast<const h8v *>(bias);
     float ss = 0.0f;
-    for (int g = lane; g < groups; g += kWave) {
-        const h8v h = src[g];
+    for (int g = sub; g < groups; g += span) {
+        h8v h = src[g];
+        if (bias) h = h + bv[g];
 #pragma unroll
         for (int k = 0; k < 8; ++k) ss += static_cast<float>(h[k]) * static_cast<float>(h[k]);
     }
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) ss += __shfl_xor(ss, o);
+    for (int o = 1; o < span; o <<= 1) ss += __shfl_xor(ss, o);
     const float nrm = fmaxf(sqrtf(ss), 1e-12f);
+    if (!in) return;
     float4 *dst = reinterpret_cast<float4 *>(y + cell * c);
-    for (int g = lane; g < groups; g += kWave) {
-        const h8v h = src[g];
+    for (int g = sub; g < groups; g += span) {
+        h8v h = src[g];
+        if (bias) h = h + bv[g];
         dst[2 * g] = make_float4(static_cast<float>(h[0]) / nrm, static_cast<float>(h[1]) / nrm, static_cast<float>(h[2]) / nrm,
                                  static_cast<float>(h[3]) / nrm);
         dst[2 * g + 1] = make_float4(static_cast<float>(h[4]) / nrm, static_cast<float>(h[5]) / nrm,
@@ -206,18 +218,22 @@ __global__ __launch_bounds__(256) void k_nn_desc_normalize(const _Float16 *x, fl
 
 }  // namespace
 
-hipError_t launch_nn_heat_softmax(const void *semi, float *heat, int n, int hc, int wc, hipStream_t s) {
+hipError_t launch_nn_heat_softmax(const void *semi, const void *bias, float *heat, int n, int hc, int wc, hipStream_t s) {
     if (n <= 0 || hc <= 0 || wc <= 0) return hipSuccess;
     const dim3 grid(static_cast<unsigned>((wc + kHeatCells - 1) / kHeatCells), static_cast<unsigned>(hc),
                     static_cast<unsigned>(n));
-    hipLaunchKernelGGL(k_nn_heat_softmax, grid, dim3(256), 0, s, static_cast<const _Float16 *>(semi), heat, hc, wc);
+    hipLaunchKernelGGL(k_nn_heat_softmax, grid, dim3(256), 0, s, static_cast<const _Float16 *>(semi),
+                       static_cast<const _Float16 *>(bias), heat, hc, wc);
     return hipGetLastError();
 }
 
-hipError_t launch_nn_desc_normalize(const void *x, float *y, int64_t cells, int c, hipStream_t s) {
+hipError_t launch_nn_desc_normalize(const void *x, const void *bias, float *y, int64_t cells, int c, hipStream_t s) {
     if (cells <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_nn_desc_normalize, dim3(static_cast<unsigned>((cells + 3) / 4)), dim3(256), 0, s,
-                       static_cast<const _Float16 *>(x), y, cells, c);
+    const int groups = c >> 3;
+    const int per_wave = groups <= 8 ? 8 : groups <= 16 ? 4 : groups <= 32 ? 2 : 1;
+    const int64_t waves = (cells + per_wave - 1) / per_wave;
+    hipLaunchKernelGGL(k_nn_desc_normalize, dim3(static_cast<unsigned>((waves + 3) / 4)), dim3(256), 0, s,
+                       static_cast<const _Float16 *>(x), static_cast<const _Float16 *>(bias), y, cells, c);
     return hipGetLastError();
 }
 

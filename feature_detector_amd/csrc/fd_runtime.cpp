@@ -2001,28 +2001,28 @@ int fd_nn_bias_relu(fd_ctx *c, const void *x, const void *bias, int64_t bias_len
     return FD_OK;
 }
 
-int fd_nn_heat_softmax(fd_ctx *c, const void *semi, float *heat, int n, int hc, int wc) {
+int fd_nn_heat_softmax(fd_ctx *c, const void *semi, const void *bias, float *heat, int n, int hc, int wc) {
     if (!c) return FD_ERR_INVALID;
     if (!semi || !heat) return fail(c, FD_ERR_INVALID, "bad arguments");
     if (n < 0 || hc < 0 || wc < 0) return fail(c, FD_ERR_INVALID, "need n, hc, wc >= 0");
     if (static_cast<int64_t>(hc) * 8 * wc * 8 >= (int64_t(1) << 31) || hc > 65535 || n > 65535)
         return fail(c, FD_ERR_INVALID, "map too large");
-    if ((reinterpret_cast<uintptr_t>(semi) & 1) || (reinterpret_cast<uintptr_t>(heat) & 3))
-        return fail(c, FD_ERR_INVALID, "pointers must be 2-byte (semi) / 4-byte (heat) aligned");
+    if (((reinterpret_cast<uintptr_t>(semi) | reinterpret_cast<uintptr_t>(bias)) & 1) || (reinterpret_cast<uintptr_t>(heat) & 3))
+        return fail(c, FD_ERR_INVALID, "pointers must be 2-byte (semi, bias) / 4-byte (heat) aligned");
     FD_HIP_TRY(c, hipSetDevice(c->device));
-    FD_HIP_TRY(c, fdk::launch_nn_heat_softmax(semi, heat, n, hc, wc, c->stream));
+    FD_HIP_TRY(c, fdk::launch_nn_heat_softmax(semi, bias, heat, n, hc, wc, c->stream));
     return FD_OK;
 }
 
-int fd_nn_desc_normalize(fd_ctx *c, const void *x, float *y, int64_t cells, int ch) {
+int fd_nn_desc_normalize(fd_ctx *c, const void *x, const void *bias, float *y, int64_t cells, int ch) {
     if (!c) return FD_ERR_INVALID;
     if (!x || !y) return fail(c, FD_ERR_INVALID, "bad arguments");
     if (cells < 0 || ch <= 0 || ch % 8) return fail(c, FD_ERR_INVALID, "need cells >= 0 and c a multiple of 8");
     if ((cells + 3) / 4 >= (int64_t(1) << 31)) return fail(c, FD_ERR_INVALID, "too many cells");
-    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15)
+    if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(bias) | reinterpret_cast<uintptr_t>(y)) & 15)
         return fail(c, FD_ERR_INVALID, "pointers must be 16-byte aligned");
     FD_HIP_TRY(c, hipSetDevice(c->device));
-    FD_HIP_TRY(c, fdk::launch_nn_desc_normalize(x, y, cells, ch, c->stream));
+    FD_HIP_TRY(c, fdk::launch_nn_desc_normalize(x, bias, y, cells, ch, c->stream));
     return FD_OK;
 }
 

@@ -214,42 +214,56 @@ def bias_relu(x, bias, pool: bool = False, out=None, ctx: Context | None = None)
     return out
 
 
-def heat_softmax(semi, ctx: Context | None = None):
+def heat_softmax(semi, bias=None, ctx: Context | None = None):
     """fd_nn_heat_softmax: SuperPoint's detector-head output from convPb's logits [N, 65, Hc, Wc]
     (channels-last fp16, on the device): softmax over the 65 channels in float, the dustbin dropped,
     pixel_shuffle(8) -> heat [N, 8 Hc, 8 Wc] float32, in one pass (PyTorch: float copy, softmax, slice,
-    shuffle). Within float rounding of torch.softmax(semi.float(), 1)[:, :-1] shuffled."""
+    shuffle). bias (65 values): added to semi in half first (semi from a bias-free convolution). Within
+    float rounding of torch.softmax((semi + bias).float(), 1)[:, :-1] shuffled."""
     import torch
 
     if not (_is_torch_device_tensor(semi) and semi.dtype == torch.float16 and semi.dim() == 4 and semi.shape[1] == 65
             and semi.is_contiguous(memory_format=torch.channels_last)):
         raise ValueError("heat_softmax: semi must be a channels-last float16 [N, 65, Hc, Wc] device tensor")
     n, _, hc, wc = semi.shape
+    b = None
+    if bias is not None:
+        if bias.numel() != 65:
+            raise ValueError("heat_softmax: bias must hold 65 values")
+        b = bias.detach().to(device=semi.device, dtype=torch.float16).contiguous()
     heat = torch.empty((n, 8 * hc, 8 * wc), dtype=torch.float32, device=semi.device)
     ctx = _resolve_ctx(ctx, semi)
     _bind_stream(ctx, True)
-    rc = _lib.load().fd_nn_heat_softmax(ctx.ptr, ctypes.c_void_p(semi.data_ptr()), ctypes.c_void_p(heat.data_ptr()),
-                                         int(n), int(hc), int(wc))
+    rc = _lib.load().fd_nn_heat_softmax(ctx.ptr, ctypes.c_void_p(semi.data_ptr()),
+                                         ctypes.c_void_p(b.data_ptr() if b is not None else None),
+                                         ctypes.c_void_p(heat.data_ptr()), int(n), int(hc), int(wc))
     _lib.check(ctx.ptr, rc)
     return heat
 
 
-def desc_normalize(desc, ctx: Context | None = None):
+def desc_normalize(desc, bias=None, ctx: Context | None = None):
     """fd_nn_desc_normalize: SuperPoint's descriptor-head output from convDb's [N, C, Hc, Wc] (channels-last
     fp16, on the device): each cell's vector over its L2 norm (clamped to 1e-12) in float -> [N, C, Hc, Wc]
-    float32 channels-last, in one pass (PyTorch: float copy, norm, division). Within float rounding of
-    desc.float() / desc.float().norm(dim=1, keepdim=True).clamp_min(1e-12)."""
+    float32 channels-last, in one pass (PyTorch: float copy, norm, division). bias (C values): added in
+    half first (desc from a bias-free convolution). Within float rounding of d.float() /
+    d.float().norm(dim=1, keepdim=True).clamp_min(1e-12), d = desc + bias."""
     import torch
 
     if not (_is_torch_device_tensor(desc) and desc.dtype == torch.float16 and desc.dim() == 4 and desc.shape[1] % 8 == 0
             and desc.is_contiguous(memory_format=torch.channels_last)):
         raise ValueError("desc_normalize: desc must be a channels-last float16 [N, C, Hc, Wc] device tensor, C % 8 == 0")
     n, c, hc, wc = desc.shape
+    b = None
+    if bias is not None:
+        if bias.numel() != c:
+            raise ValueError(f"desc_normalize: bias must hold {c} values")
+        b = bias.detach().to(device=desc.device, dtype=torch.float16).contiguous()
     out = torch.empty((n, c, hc, wc), dtype=torch.float32, device=desc.device, memory_format=torch.channels_last)
     ctx = _resolve_ctx(ctx, desc)
     _bind_stream(ctx, True)
-    rc = _lib.load().fd_nn_desc_normalize(ctx.ptr, ctypes.c_void_p(desc.data_ptr()), ctypes.c_void_p(out.data_ptr()),
-                                           int(n) * int(hc) * int(wc), int(c))
+    rc = _lib.load().fd_nn_desc_normalize(ctx.ptr, ctypes.c_void_p(desc.data_ptr()),
+                                           ctypes.c_void_p(b.data_ptr() if b is not None else None),
+                                           ctypes.c_void_p(out.data_ptr()), int(n) * int(hc) * int(wc), int(c))
     _lib.check(ctx.ptr, rc)
     return out
 
@@ -546,11 +560,22 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             x = self.cbr(self.conv2b, self.cbr(self.conv2a, x), pool=True)
             x = self.cbr(self.conv3b, self.cbr(self.conv3a, x), pool=True)
             x = self.cbr(self.conv4b, self.cbr(self.conv4a, x))
-            semi = self.convPb(self.cbr(self.convPa, x))
-            desc = self.convDb(self.cbr(self.convDa, x))
-            if self.fused_heads(semi, desc):  # the heads' output stages in one pass each (fd_nn.hip)
-                heat, desc = heat_softmax(semi), desc_normalize(desc)
+            xp, xd = self.cbr(self.convPa, x), self.cbr(self.convDa, x)
+            semi = desc = None
+            if xp.is_cuda and xp.dtype == torch.float16 and xd.dtype == torch.float16 \
+                    and not _ab_env("FD_SP_UNFUSED") and not _ab_env("FD_SP_TORCH_HEADS"):  # (A/B switches)
+                # bias-free head convolutions: their biases go into the output stages below
+                semi = torch.nn.functional.conv2d(xp, self.convPb.weight, None, self.convPb.stride, self.convPb.padding)
+                desc = torch.nn.functional.conv2d(xd, self.convDb.weight, None, self.convDb.stride, self.convDb.padding)
+                if self.fused_heads(semi, desc):  # the heads' output stages in one pass each (fd_nn.hip)
+                    heat, desc = heat_softmax(semi, self.convPb.bias), desc_normalize(desc, self.convDb.bias)
+                    semi = None
+                else:
+                    semi = semi + self.convPb.bias.view(1, -1, 1, 1)
+                    desc = desc + self.convDb.bias.view(1, -1, 1, 1)
             else:
+                semi, desc = self.convPb(xp), self.convDb(xd)
+            if semi is not None:
                 prob = torch.softmax(semi.float(), dim=1)[:, :-1]
                 heat = torch.nn.functional.pixel_shuffle(prob, 8)[:, 0]
                 desc = desc.float()

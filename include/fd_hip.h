@@ -404,18 +404,19 @@ int fd_nn_conv3x3_c1c64(fd_ctx *ctx, const void *x, const void *weight1, const v
  * fd_nn_heat_softmax -- SuperPoint's detector-head output (the network's last stage after convPb:
  * softmax over a cell's 65 channels, the dustbin channel dropped, pixel_shuffle by 8): semi
  * [n][hc][wc][65] channels-last fp16 logits -> heat [n][8 hc][8 wc] float, heat[8i + r][8j + c] =
- * exp(x_{8r+c} - m) / sum_k exp(x_k - m) over the cell's 65 logits x (m their max), in float. All on
- * the device, 4-byte aligned. Runs on the context's stream.
+ * exp(x_{8r+c} - m) / sum_k exp(x_k - m) over the cell's 65 logits x (m their max), in float. bias
+ * (optional, 65 fp16): convPb's bias, added to a bias-free convolution's output in half first. All on
+ * the device, semi and bias 2-byte, heat 4-byte aligned. Runs on the context's stream.
  */
-int fd_nn_heat_softmax(fd_ctx *ctx, const void *semi, float *heat, int n, int hc, int wc);
+int fd_nn_heat_softmax(fd_ctx *ctx, const void *semi, const void *bias, float *heat, int n, int hc, int wc);
 
 /*
  * fd_nn_desc_normalize -- SuperPoint's descriptor-head output (after convDb): every cell's c-channel
  * vector divided by max(||x||_2, 1e-12), in float: x [cells][c] fp16 (a channels-last map) -> y
- * [cells][c] float, all on the device; c a multiple of 8; x and y 16-byte aligned. Runs on the context's
- * stream.
+ * [cells][c] float, all on the device; bias (optional, c fp16): convDb's bias, added in half first;
+ * c a multiple of 8; x, bias and y 16-byte aligned. Runs on the context's stream.
  */
-int fd_nn_desc_normalize(fd_ctx *ctx, const void *x, float *y, int64_t cells, int c);
+int fd_nn_desc_normalize(fd_ctx *ctx, const void *x, const void *bias, float *y, int64_t cells, int c);
 
 /* ---- build info --------------------------------------------------------------------------------- */
 const char *fd_build_info(void);

@@ -430,13 +430,20 @@ def test_heads_match_torch(sp):
         got = sp.heat_softmax(semi)
         assert tuple(got.shape) == (n, 8 * hc, 8 * wc) and got.dtype == torch.float32
         assert torch.allclose(got, ref, rtol=1e-5, atol=1e-7), (n, hc, wc, (got - ref).abs().max().item())
-        for c in (8, 256):
+        hb = (torch.randn(65, generator=g, device="cuda") * 4).half()  # convPb's bias, added in half first
+        refb = torch.nn.functional.pixel_shuffle(torch.softmax((semi + hb.view(1, -1, 1, 1)).float(), dim=1)[:, :-1], 8)[:, 0]
+        assert torch.allclose(sp.heat_softmax(semi, hb), refb, rtol=1e-5, atol=1e-7), (n, hc, wc)
+        for c in (8, 64, 128, 256, 1024):
             d = (torch.randn((n, c, hc, wc), generator=g, device="cuda") * 3).half().contiguous(memory_format=torch.channels_last)
             df = d.float()
             refd = df / df.norm(dim=1, keepdim=True).clamp_min(1e-12)
             gotd = sp.desc_normalize(d)
             assert gotd.is_contiguous(memory_format=torch.channels_last) and gotd.dtype == torch.float32
             assert torch.allclose(gotd, refd, rtol=1e-5, atol=1e-7), (n, c, (gotd - refd).abs().max().item())
+            db = (torch.randn(c, generator=g, device="cuda") * 2).half()
+            dbf = (d + db.view(1, -1, 1, 1)).float()
+            refdb = dbf / dbf.norm(dim=1, keepdim=True).clamp_min(1e-12)
+            assert torch.allclose(sp.desc_normalize(d, db), refdb, rtol=1e-5, atol=1e-7), (n, c)
     big = torch.full((1, 65, 2, 2), 60000.0, device="cuda", dtype=torch.float16).contiguous(memory_format=torch.channels_last)
     big[:, 3] = -60000.0
     assert torch.allclose(sp.heat_softmax(big), torch.nn.functional.pixel_shuffle(
@@ -453,6 +460,9 @@ def test_heads_match_torch(sp):
     with torch.inference_mode():
         y = net.cbr(net.conv4b, net.cbr(net.conv4a, torch.zeros((2, 128, 12, 16), device="cuda", dtype=torch.float16)
                                          .contiguous(memory_format=torch.channels_last)))
-        assert net.fused_heads(net.convPb(net.cbr(net.convPa, y)), net.convDb(net.cbr(net.convDa, y)))
+        xp, xd = net.cbr(net.convPa, y), net.cbr(net.convDa, y)
+        assert net.fused_heads(torch.nn.functional.conv2d(xp, net.convPb.weight), torch.nn.functional.conv2d(xd, net.convDb.weight))
         heat, desc = net(x)
+        rheat, rdesc = _reference_forward(net, x)
     assert tuple(heat.shape) == (2, 96, 128) and tuple(desc.shape) == (2, 256, 12, 16)
+    assert torch.allclose(heat, rheat, rtol=2e-2, atol=2e-3) and torch.allclose(desc, rdesc, rtol=2e-2, atol=2e-3)
