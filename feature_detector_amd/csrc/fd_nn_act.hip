@@ -153,6 +153,9 @@ __global__ __launch_bounds__(256) void k_conv3x3_c1_bias_relu(const _Float16 *x,
 #endif
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+#ifndef FD_C1_MFMA
+#define FD_C1_MFMA 1  // fused conv1a on the matrix cores (0: the float FMA chain of k_conv3x3_c1_bias_relu, bit-equal to it)
+#endif
 #ifndef FD_C64_ROWREUSE
 #define FD_C64_ROWREUSE 1  // K loop by (dx, channel half) with the input rows reused by the three dy taps
 #endif
@@ -209,6 +212,24 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
     for (int nb = 0; nb < 4; ++nb) bv2[nb] = h2v{bias[nb * 16 + (lane & 15)], bias[nb * 16 + (lane & 15)]};
     const int th = (h + kCvRows - 1) / kCvRows, tw = (w + kCvCols - 1) / kCvCols;
     const int total = n * th * tw;  // (< 2^31: checked on the host)
+#if FD_C1_MFMA
+    // FUSED: conv1a on the matrix cores, D[16 channels][16 pixels] = W[16][K = 32] x P[K][16]: the 9 taps in
+    // K 0..8 (zeros above), this lane's A fragment = channels 16 cb + (lane & 15), taps 8 (lane >> 4) ..;
+    // the bias pairs of the 4 consecutive channels the lane's D fragment holds (16 cb + 4 (lane >> 4) ..)
+    h8 w1a[4];
+    h2v b1p[4][2];
+    if constexpr (FUSED) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+            const int c = cb * 16 + (lane & 15), g = lane >> 4;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w1a[cb][e] = 8 * g + e < 9 ? w1[c * 9 + 8 * g + e] : static_cast<_Float16>(0.0f);
+            const int cd = cb * 16 + 4 * g;
+            b1p[cb][0] = h2v{b1[cd], b1[cd + 1]};
+            b1p[cb][1] = h2v{b1[cd + 2], b1[cd + 3]};
+        }
+    }
+#else
     // FUSED: this thread's conv1a channel group (8 channels) and its weights
     const int cg = tid & 7;
     f2 w1f[4][9], b1f[4];
@@ -221,6 +242,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
             b1f[k2] = f2{static_cast<float>(b1[cg * 8 + 2 * k2]), static_cast<float>(b1[cg * 8 + 2 * k2 + 1])};
         }
     }
+#endif
     // the input tile goes through registers: the next tile's loads are issued before this tile's K loop
     // and stored to LDS after it, so their latency hides behind the matrix work (FUSED: the raw rows)
     constexpr int kChunks = kCvInRows * kCvInCols * 8, kPer = FUSED ? 1 : (kChunks + 255) / 256;
@@ -269,6 +291,39 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
             }
             __syncthreads();
             fetch(tile + static_cast<int>(gridDim.x));
+#if FD_C1_MFMA
+            // conv1a over the tile's input pixels, 16 at a time per wave: the lane's patch fragment (taps
+            // 8 (lane >> 4) .. of pixel lane & 15) from the raw rows, one matrix step per 16 channels, the
+            // sum rounded to half, the bias added in half, the ReLU, and the lane's 4 channels of the pixel
+            // written as 8 bytes into its 16-byte chunk (zero outside the frame: conv1b's padding)
+            constexpr int kInPx = kCvInRows * kCvInCols;
+            for (int pb = wv; pb * 16 < kInPx; pb += 4) {
+                const int px = pb * 16 + (lane & 15), g = lane >> 4;
+                const int pxc = min(px, kInPx - 1);
+                const int pr = pxc / kCvInCols, pc = pxc - pr * kCvInCols;
+                h8 pt;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) pt[e] = static_cast<_Float16>(0.0f);
+                if (g == 0) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) pt[e] = raw[pr + e / 3][pc + e % 3];
+                } else if (g == 1) {
+                    pt[0] = raw[pr + 2][pc + 2];
+                }
+                const int gy = r0 - 1 + pr, gx = c0 - 1 + pc;
+                const bool inframe = gy >= 0 && gy < h && gx >= 0 && gx < w;
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) {
+                    const f4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1a[cb], pt, f4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+                    const h2v lo = cv_relu2(cv_pair(d[0], d[1], b1p[cb][0])), hi = cv_relu2(cv_pair(d[2], d[3], b1p[cb][1]));
+                    const int ch = cb * 16 + 4 * g;  // the lane's first channel: chunk ch / 8, half (ch & 4) / 4
+                    uint2 v = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+                    if (!inframe) v = make_uint2(0u, 0u);
+                    if (px < kInPx)
+                        reinterpret_cast<uint2 *>(In)[(pxc * 8 + ((ch >> 3) ^ (pc & 7))) * 2 + ((ch >> 2) & 1)] = v;
+                }
+            }
+#else
             // conv1a over the tile's input pixels (6 x 66), 8 channels per item
             for (int px = tid >> 3; px < kCvInRows * kCvInCols; px += 32) {
                 const int pr = px / kCvInCols, pc = px - pr * kCvInCols;
@@ -297,6 +352,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
                 }
                 In[px * 8 + (cg ^ (pc & 7))] = o;
             }
+#endif
             __syncthreads();
         } else {
 #pragma unroll

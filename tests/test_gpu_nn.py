@@ -331,11 +331,12 @@ def test_conv64_bias_relu_matches_torch(sp):
 
 @pytest.mark.gpu
 def test_conv1ab_fused_matches_layers(sp):
-    """fd_nn_conv3x3_c1c64 (SuperPoint conv1a fused into conv1b's tile staging: the 64-channel
-    full-resolution activation never goes to memory) equals the two layer kernels in sequence bit for
-    bit -- conv64_bias_relu(conv1_bias_relu(x)), pooled and not -- and PyTorch's float32
-    relu(conv1b(relu(conv1a(x)))) within the fp16 roundings; ragged tiles (sizes off the 4 x 64 tile) and
-    a 640x480 batch."""
+    """fd_nn_conv3x3_c1c64 (SuperPoint conv1a fused into conv1b's tile staging, on the matrix cores: the
+    64-channel full-resolution activation never goes to memory) against the two layer kernels in sequence
+    -- conv64_bias_relu(conv1_bias_relu(x)), pooled and not -- and PyTorch's float32
+    relu(conv1b(relu(conv1a(x)))), both within the fp16 roundings (the fused conv1a sums its 9 products
+    on the matrix cores, the layer kernel in an FMA chain: a sum may round to the neighbouring half);
+    ragged tiles (sizes off the tile) and a 640x480 batch."""
     import torch
 
     g = torch.Generator(device="cuda")
@@ -347,18 +348,20 @@ def test_conv1ab_fused_matches_layers(sp):
         w2 = (torch.randn((64, 64, 3, 3), generator=g, device="cuda") * 0.06).half()
         b2 = (torch.randn(64, generator=g, device="cuda") * 0.2).half()
         a = sp.conv1_bias_relu(x, w1, b1)
+        conv1 = torch.relu(torch.nn.functional.conv2d(x.float(), w1.float(), b1.float(), 1, 1))
+        conv2 = torch.nn.functional.conv2d(conv1, w2.float(), None, 1, 1)
+        # bound: conv1a's two roundings (2^-10 relative) carried through conv1b's weights, then conv1b's own
+        # two roundings of the sum (2^-10 relative)
+        carried = torch.nn.functional.conv2d(conv1.abs(), w2.float().abs(), None, 1, 1) * 2.0 ** -10
+        tol_full = carried + (conv2.abs() + 1.0) * 2.0 ** -10 + 2.0 ** -14
         for pool in (True, False):
             ref = sp.conv64_bias_relu(a, w2, b2, pool=pool)
             got = sp.conv1ab_bias_relu(x, w1, b1, w2, b2, pool=pool)
             assert got.is_contiguous(memory_format=torch.channels_last)
-            assert torch.equal(got, ref), (n, h, w, pool)
-        conv1 = torch.relu(torch.nn.functional.conv2d(x.float(), w1.float(), b1.float(), 1, 1))
-        conv2 = torch.nn.functional.conv2d(conv1, w2.float(), None, 1, 1)
+            tol = torch.nn.functional.max_pool2d(tol_full, 2, 2) if pool else tol_full
+            assert bool(((got.float() - ref.float()).abs() <= 2 * tol).all()), (n, h, w, pool)
         f32 = torch.nn.functional.max_pool2d(torch.relu(conv2 + b2.float().view(1, -1, 1, 1)), 2, 2)
-        # bound: conv1a's two roundings (2^-10 relative) carried through conv1b's weights, then conv1b's own
-        # two roundings of the sum (2^-10 relative)
-        carried = torch.nn.functional.conv2d(conv1.abs(), w2.float().abs(), None, 1, 1) * 2.0 ** -10
-        tol = torch.nn.functional.max_pool2d(carried + (conv2.abs() + 1.0) * 2.0 ** -10 + 2.0 ** -14, 2, 2)
+        tol = torch.nn.functional.max_pool2d(tol_full, 2, 2)
         err = (sp.conv1ab_bias_relu(x, w1, b1, w2, b2).float() - f32).abs()
         assert bool((err <= tol).all()), (n, h, w, err.max().item())
     with pytest.raises(ValueError):
