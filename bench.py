@@ -51,35 +51,49 @@ TRAFFIC_FILE = latest_profile("traffic.json")
 SQ_FILE = latest_profile("sq.json")
 KSTATS_FILE = latest_profile("bench_kernel_stats.csv")  # rocprofv3 --kernel-trace of bench.py, by bench leg
 STAMPS_FILE = latest_profile("select_stamps.txt")  # k_select phase clocks (FD_SELECT_STAMPS) at the headline
+# the two above in one JSON (tools/make_bench_ref.py): the GPU box's upload skips profiles/*.csv / *.txt
+REF_FILE = latest_profile("bench_ref.json")
+
+
+def _bench_ref():
+    try:
+        with open(REF_FILE or "") as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
 
 
 def rocprof_kernel(phase_name, name_part):
     """(avg us, calls, source) of a kernel in a bench leg of the committed rocprofv3 summary, or None."""
     import csv
 
-    if not KSTATS_FILE:
-        return None
+    rows, src = None, None
     try:
-        with open(KSTATS_FILE) as fh:
-            rows = [r for r in csv.reader(l for l in fh if not l.startswith("#"))]
+        with open(KSTATS_FILE or "") as fh:
+            rows = [r for r in csv.reader(l for l in fh if not l.startswith("#"))][1:]
+        src = os.path.relpath(KSTATS_FILE, ROOT)
     except OSError:
-        return None
-    for r in rows[1:]:
+        ref = _bench_ref()
+        rows, src = ref.get("kernel_stats"), ref.get("kernel_stats_source")
+    for r in rows or []:
         if len(r) >= 4 and r[0] == "fdbench:" + phase_name and name_part in r[1]:
-            return float(r[3]), int(r[2]), os.path.relpath(KSTATS_FILE, ROOT)
+            return float(r[3]), int(r[2]), src
     return None
 
 
 def select_phase_cycles():
     """k_select's phase clocks of the first headline frame in the committed stamps file (FD_SELECT_STAMPS;
     tools/select_stamps.py), or None: {phase: cycles} and the greedy scan's share of the total."""
-    if not STAMPS_FILE:
-        return None
+    src = os.path.relpath(STAMPS_FILE, ROOT) if STAMPS_FILE else None
     try:
-        with open(STAMPS_FILE) as fh:
+        with open(STAMPS_FILE or "") as fh:
             lines = fh.readlines()
+    except OSError:
+        ref = _bench_ref()
+        lines, src = ref.get("select_stamps_lines") or [], ref.get("select_stamps_source")
+    try:
         i = next(k for k, l in enumerate(lines) if l.startswith("k_select cycles:"))
-    except (OSError, StopIteration):
+    except StopIteration:
         return None
     toks = lines[i].replace("|", " ").split()[2:]
     ph = {}
@@ -93,7 +107,7 @@ def select_phase_cycles():
         ph["scan_other_batches"] = int(fine[11])
     tot = sum(ph.values())
     serial = ph.get("greedy", 0) + ph.get("scan_first_batch", 0) + ph.get("scan_other_batches", 0)
-    return {"source": os.path.relpath(STAMPS_FILE, ROOT), "cycles": ph,
+    return {"source": src, "cycles": ph,
             "greedy_share": round(serial / tot, 3) if tot else None}
 
 
