@@ -12,12 +12,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1] if len(sys.argv) > 1 else "r05"
 kfile = os.path.join("profiles", f"{tag}_bench_kernel_stats.csv")
 sfile = os.path.join("profiles", f"{tag}_select_stamps.txt")
-out = {"_what": "extract of " + kfile + " (fdbench:* legs) and " + sfile + " (k_select cycles lines) for bench.py",
+out = {"_what": "extract of " + kfile + " (the headline and roofline_kernel legs) and " + sfile + " (k_select cycles lines) for bench.py",
        "kernel_stats_source": kfile, "kernel_stats": [], "select_stamps_source": sfile, "select_stamps_lines": []}
 with open(os.path.join(ROOT, kfile)) as fh:
     rows = list(csv.reader(l for l in fh if not l.startswith("#")))
 for r in rows[1:]:
-    if len(r) >= 4 and r[0].startswith("fdbench:"):
+    if len(r) >= 4 and r[0] in ("fdbench:headline", "fdbench:roofline_kernel"):  # (the legs bench.py looks up)
         out["kernel_stats"].append([r[0], r[1], int(r[2]), float(r[3])])
 with open(os.path.join(ROOT, sfile)) as fh:
     lines = fh.readlines()
