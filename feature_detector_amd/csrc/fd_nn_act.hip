@@ -81,6 +81,20 @@ __global__ __launch_bounds__(256) void k_bias_relu_pool(const u4 *x, const u4 *b
 // float FMA accumulation in tap order, the sum rounded to half, then + bias in float rounded to half and
 // the ReLU (as the bias-free convolution + fd_nn_bias_relu path rounds), one 16-byte store.
 constexpr int kConv1MaxW = 4096;  // frame width the row staging holds
+#ifndef FD_NN_NT_STORES
+#define FD_NN_NT_STORES 1  // conv1a's activation written with nontemporal stores (A/B: 0): 589 -> 449 us
+#endif
+#ifndef FD_C64_NT_STORES
+#define FD_C64_NT_STORES 1  // K10's outputs likewise (A/B: 0): conv2a / conv1b +22 / +27 us alone, but the forward
+                            // 4.54-4.61 vs 4.69-4.71 ms (the layers after them find the caches unpolluted)
+#endif
+__device__ __forceinline__ void nn_store(u4 *p, u4 v) {
+#if FD_C64_NT_STORES
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 
 __global__ __launch_bounds__(256) void k_conv3x3_c1_bias_relu(const _Float16 *x, const _Float16 *wt,
                                                               const _Float16 *bias, u4 *y, int n, int h, int w,
@@ -131,7 +145,11 @@ __global__ __launch_bounds__(256) void k_conv3x3_c1_bias_relu(const _Float16 *x,
                 }
                 o[k2] = packed;
             }
+#if FD_NN_NT_STORES
+            __builtin_nontemporal_store(o, &yrow[xx * cvec + cv]);  // (2.5 GB per SuperPoint batch: streamed past the caches)
+#else
             yrow[xx * cvec + cv] = o;
+#endif
         }
         __syncthreads();  // (rin reused by the next row)
     }
@@ -469,7 +487,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
             for (int i = tid; i < kCvRows / 2 * 32 * 8; i += 256) {
                 const int ch = i & 7, px = i >> 3, pc = px & 31, pr = px >> 5;
                 const int gy = r0 / 2 + pr, gx = c0 / 2 + pc;
-                if (gy < ho && gx < wo) y[((static_cast<int64_t>(f) * ho + gy) * wo + gx) * ystride + yoff + ch] = In[px * 8 + ch];
+                if (gy < ho && gx < wo) nn_store(&y[((static_cast<int64_t>(f) * ho + gy) * wo + gx) * ystride + yoff + ch], In[px * 8 + ch]);
             }
         } else {
             // staging [kCvRows rows][64 columns][64 channels]
@@ -489,7 +507,7 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
             for (int i = tid; i < kCvRows * kCvCols * 8; i += 256) {
                 const int ch = i & 7, px = i >> 3, pc = px % kCvCols, pr = px / kCvCols;
                 const int gy = r0 + pr, gx = c0 + pc;
-                if (gy < h && gx < w) y[((static_cast<int64_t>(f) * h + gy) * w + gx) * ystride + yoff + ch] = In[px * 8 + ch];
+                if (gy < h && gx < w) nn_store(&y[((static_cast<int64_t>(f) * h + gy) * w + gx) * ystride + yoff + ch], In[px * 8 + ch]);
             }
         }
     }
