@@ -126,3 +126,9 @@ def test_seed_order_on_gpu(oracle, monkeypatch, capfd):
         assert "seed orders from the gpu 0" in capfd.readouterr().err
         monkeypatch.delenv("FD_LSD_HOST_SORT")
         assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(got, host))
+        # the order through a device buffer and a copy instead of written into pinned host memory
+        monkeypatch.setenv("FD_LSD_ORD_MAPPED", "0")
+        copied = fd.lsd_lines(frames)
+        assert f"seed orders from the gpu {frames.shape[0]}" in capfd.readouterr().err
+        monkeypatch.delenv("FD_LSD_ORD_MAPPED")
+        assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(got, copied))
