@@ -1480,7 +1480,11 @@ int lsd_seed_order(fd_ctx *c, int batch, int map_rows, int map_cols, const std::
     s.need = 0xFFFFFFFFu;
     s.status = as<uint32_t>(c->l_sst);
     s.cand_n = s.status + batch;
-    const bool wide = static_cast<int64_t>(map_rows) * map_cols >= (int64_t{1} << 20);
+    // (no multi-workgroup prelude: every frame is sorted, all workgroups are busy anyway, and the ~30
+    // prelude launches cost more than its first levels save: seed orders 0.35-0.6 ms after the lists
+    // instead of 0.58-0.87, profiles/r05_lines_seed_order.txt; FD_LSD_WIDE=1: with it, A/B)
+    bool wide = false;
+    if (const char *e = ab_env("FD_LSD_WIDE")) wide = std::atoi(e) != 0;
     FD_HIP_TRY(c, hipStreamWaitEvent(c->aux, c->l_ev0, 0));
     // order_only never reads ord back: the kernel may write it straight into the pinned host buffer
     // (FD_LSD_ORD_MAPPED=0: a device buffer and a copy, A/B)

@@ -21,9 +21,14 @@ batch = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 frames = bench.make_frames(torch, "checker", batch, 1080, 1920, 0, "cuda", period=64)
 torch.cuda.synchronize()
 ref = None
-for mode in ("gpu", "gpu_copy", "host", "gpu", "gpu_copy", "host"):
+MODES = os.environ.get("FD_AB_MODES", "gpu,gpu_copy,host").split(",")  # (gpu_narrow: no wide prelude)
+for mode in MODES + MODES:
     os.environ["FD_LSD_HOST_SORT"] = "1" if mode == "host" else "0"
     os.environ["FD_LSD_ORD_MAPPED"] = "0" if mode == "gpu_copy" else "1"  # (gpu_copy: ord via a device buffer)
+    if mode == "gpu_narrow":
+        os.environ["FD_LSD_WIDE"] = "0"
+    else:
+        os.environ.pop("FD_LSD_WIDE", None)
     segs = fd.lsd_lines(frames, max_lines=2048)  # warm
     torch.cuda.synchronize()
     t0 = time.perf_counter()
