@@ -106,8 +106,9 @@ def test_config4_batch_spot_check(oracle):
 def test_seed_order_on_gpu(oracle, monkeypatch, capfd):
     # the seed order (sorted_pixels_, feature_line_detector.cpp:88-94) comes from the GPU
     # (k_select_reference in push order) for every frame, including a ramp whose norms are all equal
-    # (the introsort's equal-key paths) and frames large enough for the wide prelude; the segments are
-    # the oracle's and those of the host std::sort (FD_LSD_HOST_SORT=1)
+    # (the introsort's equal-key paths) and a 1080p frame; the segments are the oracle's and those of
+    # the host std::sort (FD_LSD_HOST_SORT=1), and with the multi-workgroup prelude (FD_LSD_WIDE=1) or
+    # the order through a device buffer (FD_LSD_ORD_MAPPED=0) the same
     import feature_detector_amd as fd
 
     r, c = np.mgrid[0:400, 0:600]
@@ -132,3 +133,8 @@ def test_seed_order_on_gpu(oracle, monkeypatch, capfd):
         assert f"seed orders from the gpu {frames.shape[0]}" in capfd.readouterr().err
         monkeypatch.delenv("FD_LSD_ORD_MAPPED")
         assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(got, copied))
+        monkeypatch.setenv("FD_LSD_WIDE", "1")
+        wide = fd.lsd_lines(frames)
+        assert f"seed orders from the gpu {frames.shape[0]}" in capfd.readouterr().err
+        monkeypatch.delenv("FD_LSD_WIDE")
+        assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(got, wide))
