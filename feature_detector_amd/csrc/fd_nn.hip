@@ -145,18 +145,24 @@ constexpr int kHeatCells = 32;
 __global__ __launch_bounds__(256) void k_nn_heat_softmax(const _Float16 *semi, const _Float16 *bias, float *heat, int hc,
                                                          int wc) {
     __shared__ float pr[kHeatCells][65];
+    __shared__ _Float16 lg[kHeatCells * 65 + 65];  // the group's logits (contiguous in memory), then the bias
     const int tid = static_cast<int>(threadIdx.x), cell = tid >> 3, part = tid & 7;
     const int j0 = static_cast<int>(blockIdx.x) * kHeatCells, i = static_cast<int>(blockIdx.y), b = static_cast<int>(blockIdx.z);
+    const int cn = min(kHeatCells, wc - j0);
+    // the group's cells are one contiguous run of cn * 65 halves: staged with coalesced loads
+    const _Float16 *src = semi + ((static_cast<int64_t>(b) * hc + i) * wc + j0) * 65;
+    for (int k = tid; k < cn * 65; k += 256) lg[k] = src[k];
+    if (tid < 65) lg[kHeatCells * 65 + tid] = bias ? bias[tid] : static_cast<_Float16>(0.0f);
+    __syncthreads();
     const int j = j0 + cell;
     const bool in = j < wc;
-    const _Float16 *src = semi + ((static_cast<int64_t>(b) * hc + i) * wc + (in ? j : 0)) * 65;
     // (bias: convPb's bias added to the bias-free convolution's half output, in half: a half add is the
-    // float add rounded to half)
+    // float add rounded to half; a zero bias adds nothing)
+    const _Float16 *cl = lg + (in ? cell : 0) * 65, *bl = lg + kHeatCells * 65;
     float v[9];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        v[k] = static_cast<float>(bias ? static_cast<_Float16>(src[part * 8 + k] + bias[part * 8 + k]) : src[part * 8 + k]);
-    v[8] = part == 0 ? static_cast<float>(bias ? static_cast<_Float16>(src[64] + bias[64]) : src[64]) : -INFINITY;
+    for (int k = 0; k < 8; ++k) v[k] = static_cast<float>(static_cast<_Float16>(cl[part * 8 + k] + bl[part * 8 + k]));
+    v[8] = part == 0 ? static_cast<float>(static_cast<_Float16>(cl[64] + bl[64])) : -INFINITY;
     float m = v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) m = fmaxf(m, v[k]);
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(256) void k_nn_heat_softmax(const _Float16 *semi, c
     float *dst = heat + (static_cast<int64_t>(b) * hc * 8 + static_cast<int64_t>(i) * 8) * w + static_cast<int64_t>(j0) * 8;
     if (!in) return;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) dst[r * w + tid] = pr[cell][r * 8 + part];
+    for (int r = 0; r < 8; ++r) __builtin_nontemporal_store(pr[cell][r * 8 + part], &dst[r * w + tid]);
 }
 
 // SuperPoint's descriptor head after convDb: each cell's c-channel vector divided by its L2 norm
@@ -205,14 +211,16 @@ __global__ __launch_bounds__(256) void k_nn_desc_normalize(const _Float16 *x, co
     for (int o = 1; o < span; o <<= 1) ss += __shfl_xor(ss, o);
     const float nrm = fmaxf(sqrtf(ss), 1e-12f);
     if (!in) return;
-    float4 *dst = reinterpret_cast<float4 *>(y + cell * c);
+    float *dst = y + cell * c;
     for (int g = sub; g < groups; g += span) {
         h8v h = src[g];
         if (bias) h = h + bv[g];
-        dst[2 * g] = make_float4(static_cast<float>(h[0]) / nrm, static_cast<float>(h[1]) / nrm, static_cast<float>(h[2]) / nrm,
-                                 static_cast<float>(h[3]) / nrm);
-        dst[2 * g + 1] = make_float4(static_cast<float>(h[4]) / nrm, static_cast<float>(h[5]) / nrm,
-                                     static_cast<float>(h[6]) / nrm, static_cast<float>(h[7]) / nrm);
+        // (plain stores: nontemporal ones measured 92 -> 114 us here)
+        float4 *dv = reinterpret_cast<float4 *>(dst);
+        dv[2 * g] = make_float4(static_cast<float>(h[0]) / nrm, static_cast<float>(h[1]) / nrm, static_cast<float>(h[2]) / nrm,
+                                static_cast<float>(h[3]) / nrm);
+        dv[2 * g + 1] = make_float4(static_cast<float>(h[4]) / nrm, static_cast<float>(h[5]) / nrm,
+                                    static_cast<float>(h[6]) / nrm, static_cast<float>(h[7]) / nrm);
     }
 }
 
