@@ -57,3 +57,19 @@ def test_bench_reads_round_files():
     assert traffic and src.endswith("_traffic.json")
     issue = bench.north_star_issue()
     assert issue and 0.0 < issue["simd_valu_utilisation"] < 1.0
+
+
+def test_bench_ref_extract_matches_sources(monkeypatch):
+    """profiles/<tag>_bench_ref.json (what the GPU box reads instead of the csv / txt profiles, which its
+    upload skips) gives bench.py the same rocprof kernel rows and k_select phase clocks as the files."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    from_files = (bench.rocprof_kernel("headline", "k_select<"), bench.rocprof_kernel("roofline_kernel", "k_corner"),
+                  bench.select_phase_cycles())
+    assert all(from_files)
+    monkeypatch.setattr(bench, "KSTATS_FILE", None)
+    monkeypatch.setattr(bench, "STAMPS_FILE", None)
+    from_ref = (bench.rocprof_kernel("headline", "k_select<"), bench.rocprof_kernel("roofline_kernel", "k_corner"),
+                bench.select_phase_cycles())
+    assert from_ref == from_files
