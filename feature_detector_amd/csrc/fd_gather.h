@@ -30,8 +30,9 @@ struct GatherView {
     const uint32_t *hist;    // the frame's level-0 histogram (complete)
     uint32_t key_base;
     int key_lz, tie_desc;
-    uint64_t *pk;            // the frame's pre_keys [kSelectChunk]
-    uint32_t *pcount;        // the frame's pre_count
+    uint64_t *pk;            // the frame's pre_keys [kSelectChunk] (k_gather) or wide_keys [kWideKeys] (k_wide_gather)
+    uint32_t *pcount;        // the frame's pre_count / wide_count
+    uint32_t limit;          // keys the chunk may hold: kSelectChunk or kWideKeys
 };
 
 struct GatherLds {
@@ -77,7 +78,7 @@ __device__ __forceinline__ void gather_first_chunk(const GatherView &v, int g, i
     int lo = 0, hi = kHistBins;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (L.S[mid] <= static_cast<uint32_t>(kSelectChunk)) hi = mid; else lo = mid + 1;
+        if (L.S[mid] <= v.limit) hi = mid; else lo = mid + 1;
     }
     if (lo >= kHistBins || L.S[lo] == 0) return;  // top bin alone exceeds a chunk (k_select descends)
     const uint32_t k32lo = static_cast<uint32_t>(lo) << 20;
@@ -108,7 +109,7 @@ __device__ __forceinline__ void gather_first_chunk(const GatherView &v, int g, i
             const int k = __builtin_ctz(hm);
             hm &= hm - 1u;
             const int64_t i = base + tid + static_cast<int64_t>(k) * NT;
-            if (pos < static_cast<uint32_t>(kSelectChunk))
+            if (pos < v.limit)
                 v.pk[pos] = sel_key64(r[k], v.lidx[i], v.key_base, v.key_lz, v.tie_desc);
             ++pos;
         }

@@ -122,6 +122,12 @@ struct SelectArgs {
     int nseg;               // segments per frame
     uint64_t *wide_keys;  // [batch][kWideKeys] scratch of the wide pass, or null (one list pass per chunk)
     int wide_eager;       // wide pass with the first chunk (FAST) instead of at the first later list pass
+    // k_wide_cut + k_wide_gather (batch x wide_groups workgroups of 256 threads, before k_select): the wide pass of a
+    // wide_eager frame spread over the frame's list, keys into wide_keys, their number into wide_count
+    // (reset by k_select); null wide_count: k_select makes the pass itself, one workgroup per frame
+    uint32_t *wide_count;
+    uint32_t *wide_cut;  // [batch] k_wide_cut's level-0 bin cut (kHistBins: none), read by k_wide_gather
+    int wide_groups;
     int first_sub;     // sorted-segment corner frames: first chunk cut at one sub-chunk (kSubChunk keys)
     int grid_at_d0;    // distance 0 still tests the grid (1-pixel cells): caller lists may name a pixel twice
     int dup_keys;      // equal selection keys possible (caller lists): the orderings rank them stably
@@ -167,6 +173,7 @@ struct RefSortArgs {
     uint32_t *wfr;   // [1 + batch] the prelude's compact list: count, flagged frames
     int wide;        // set by the launcher: the prelude ran (push order and the first levels are done)
     int order_only;  // the visiting order alone (ord, every window; no greedy, no outputs): LSD seed order
+    int guard_limit;  // iterations of the window x level loop before the frame is failed (0: 1 << 16); diagnostic override
 };
 
 // fd_points_select: caller candidates (response, x, y at [f * stride], counts[f]) -> list format.
@@ -293,7 +300,7 @@ hipError_t launch_fast_mask_scan(const uint32_t *mask, int mask_wpr, int batch, 
 hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t s);
 hipError_t launch_corner_lp_any(int kind, const PointsArgs &a, hipStream_t s);  // k_corner_lp (a.px != 0)
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s);
-hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (if a.pre_keys) + k_select
+hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s);  // k_gather (a.pre_keys) / k_wide_gather (a.wide_count) + k_select
 hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int n_frames, hipStream_t s);
 // libstdc++ std::sort order emulated on the GPU for the frames k_select flagged (FD_FRAME_TIES)
 // wide: run the multi-workgroup prelude first (r.ctl, r.wcnt set): frames of >= 1 Mpx

@@ -157,7 +157,8 @@ private:
 
     // sorted_pixels_: the scan-ordered list under the reference's comparator (:92-94). The GPU's order
     // (the same libstdc++ introsort permutation, emulated by k_select_reference) is taken when it is a
-    // permutation of this frame's valid pixels; otherwise, and without one, std::sort here.
+    // permutation of this frame's valid pixels in non-increasing norm; otherwise (a broken emulation,
+    // a stale buffer), and without one, std::sort here.
     void order_seeds(const uint32_t *ord) {
 #ifdef FD_LINES_PHASES
         const auto ts = std::chrono::steady_clock::now();
@@ -172,6 +173,10 @@ private:
             }
             const int32_t e = entry_of_[i];
             if (state_[e] & kSeen) {
+                ok = false;
+                break;
+            }
+            if (k > 0 && norm_[e] > norm_[seeds_[k - 1].second]) {  // not sorted by the comparator
                 ok = false;
                 break;
             }

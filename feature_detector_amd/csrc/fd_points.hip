@@ -23,6 +23,9 @@ namespace {
 // bytes over and only 4 fit.
 constexpr int kStage = FD_STAGE_CORNER;
 constexpr int kStageFast = FD_STAGE_FAST;  // FAST: fewer flushes (each drains the wave's stores)
+#ifndef FD_FAST_PIPE
+#define FD_FAST_PIPE 1  // k_fast: score-table loads consumed one row step after they are issued (0: same step, A/B)
+#endif
 
 // Per-wave candidate sink. Detect mode: stage in LDS, append to the frame's list with one atomic per
 // flush. Raster mode: write the (row, tile) segment in column order.
@@ -531,6 +534,81 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
 #pragma unroll
     for (int s = 0; s < 7; ++s) P[s] = L[s] = R[s] = 0;
 
+    // Scan index k of each pixel among mask-true pixels (the offset counter of :85-93), the response
+    // score + o_k (:88), the candidate test (:89) and the emission, for output row `orow` whose scores
+    // are known.
+    auto finish_row = [&](int orow, uint32_t live, const int (&score)[4]) {
+        float resp[4];
+        bool fl[4];
+        if constexpr (MASKED) {
+            int32_t kbase = 0;
+            uint32_t mword = 0;
+            const int64_t rb = static_cast<int64_t>(f) * rows + orow;
+            kbase = a.row_base[rb];
+            if (c0 >= 0 && c0 < cols) {
+                const int w = c0 >> 5;
+                kbase += a.word_pref[rb * a.mask_wpr + w];
+                mword = a.mask[rb * a.mask_wpr + w];
+                if (w == 0) mword &= ~7u;
+            }
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const bool lv = (live >> (8 * m + 7)) & 1u;
+                const int32_t k = kbase + __popc(mword & ((1u << ((c0 + m) & 31)) - 1u));  // earlier pixels in the word
+                resp[m] = 0.0f;
+                if (lv && (score[m] > 0 || k >= off.k0))
+                    resp[m] = static_cast<float>(score[m]) + fast_offset(off.nseg, seg_k, seg_o, seg_inc, k);
+                fl[m] = lv && resp[m] > a.thr;
+            }
+        } else {
+            const int32_t krow = (orow - 3) * (cols - 6) - 3;  // k = krow + column
+            const int32_t kmin = krow + cmin, kmax = krow + cmax;
+            while (sg + 1 < off.nseg && seg_k[sg + 1] <= kmin) ++sg;  // (uniform; rows only move forward)
+            if (sg + 1 >= off.nseg || seg_k[sg + 1] > kmax) {     // the whole row step in one segment
+                const float os = seg_o[sg], inc = seg_inc[sg];
+                const int32_t kr = krow + c0 - seg_k[sg];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    resp[m] = static_cast<float>(score[m]) + __builtin_fmaf(static_cast<float>(kr + m), inc, os);
+                    fl[m] = colv[m] && resp[m] > a.thr;
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    resp[m] = 0.0f;
+                    if (colv[m]) resp[m] = static_cast<float>(score[m]) +
+                                           fast_offset(off.nseg, seg_k, seg_o, seg_inc, krow + c0 + m);
+                    fl[m] = colv[m] && resp[m] > a.thr;
+                }
+            }
+        }
+        const uint64_t b[4] = {ballot(fl[0]), ballot(fl[1]), ballot(fl[2]), ballot(fl[3])};
+        emit_row<RASTER, kSegFast>(sk, a, f, tx, orow, c0, b, fl, resp);
+        if constexpr (RASTER) {
+            if (a.resp_map != nullptr) {
+                float *mrow = a.resp_map + (static_cast<int64_t>(f) * rows + orow) * cols;
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    if (fl[m]) mrow[c0 + m] = resp[m];
+            }
+        }
+    };
+#if FD_FAST_PIPE
+    // Software pipeline over the rows: a row's score-table loads (L1/L2 hits, several hundred cycles) are
+    // issued in the step that classifies it and consumed in the next step, after that step's own row
+    // load and table loads are in flight -- not waited for at once in the step that issued them.
+    bool pend = false;  // (wave-uniform) a classified row waits for its scores
+    int p_orow = 0;
+    uint32_t p_live = 0, p_pass = 0;
+    uint32_t p_sb[4] = {0u, 0u, 0u, 0u}, p_sd[4] = {0u, 0u, 0u, 0u};
+    auto finish_pending = [&]() {
+        int score[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) score[m] = ((p_pass >> (8 * m + 7)) & 1u) ? static_cast<int>(max(p_sb[m], p_sd[m])) : 0;
+        finish_row(p_orow, p_live, score);
+    };
+#endif
+
     const int n_in = (y1 - y0) + 6;
     uint32_t nxt = load_px4<ALIGNED>(rs, (y0 - 3) * cols + c0);  // one row of prefetch
     for (int i0 = 0; i0 < n_in; i0 += 7) {
@@ -564,7 +642,7 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
             const uint32_t b4 = bright(v4), b8 = bright(v8), b12 = bright(v12);
             const uint32_t d4 = dark(v4), d8 = dark(v8), d12 = dark(v12);
             const uint32_t pass = ((b4 & b8 & b12) | (d4 & d8 & d12)) & live;
-            int score[4] = {0, 0, 0, 0};
+            uint32_t sb[4] = {0u, 0u, 0u, 0u}, sd[4] = {0u, 0u, 0u, 0u};  // score-table entries (bright, dark)
             if (ballot(pass != 0u) != 0ull) {  // wave-uniform
                 // ring masks, 8 samples per half: acc = bfi(kH, g, acc >> 1) inserts sample k at bit 7;
                 // after 8 insertions sample k of the half sits at bit k - 8*half of each byte.
@@ -598,70 +676,34 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
                         const uint32_t sel = 0x0C0C0000u | (static_cast<uint32_t>(4 + m) << 8) | static_cast<uint32_t>(m);
                         const uint32_t ib = __builtin_amdgcn_perm(bhi, blo, sel);  // bits 0-7 | 8-15
                         const uint32_t id = __builtin_amdgcn_perm(dhi, dlo, sel);
-                        score[m] = static_cast<int>(max(buf_load_u8(lut, static_cast<int32_t>(ib)),
-                                                        buf_load_u8(lut, static_cast<int32_t>(id))));
+                        sb[m] = buf_load_u8(lut, static_cast<int32_t>(ib));
+                        sd[m] = buf_load_u8(lut, static_cast<int32_t>(id));
                     }
                 }
             }
 #undef ROW
-            // Scan index k of each pixel among mask-true pixels (the offset counter of :85-93) and the
-            // response score + o_k (:88).
-            float resp[4];
-            bool fl[4];
-            if constexpr (MASKED) {
-                int32_t kbase = 0;
-                uint32_t mword = 0;
-                const int64_t rb = static_cast<int64_t>(f) * rows + orow;
-                kbase = a.row_base[rb];
-                if (c0 >= 0 && c0 < cols) {
-                    const int w = c0 >> 5;
-                    kbase += a.word_pref[rb * a.mask_wpr + w];
-                    mword = a.mask[rb * a.mask_wpr + w];
-                    if (w == 0) mword &= ~7u;
-                }
+#if FD_FAST_PIPE
+            if (pend) finish_pending();  // the previous row, its table loads issued one step ago
+            pend = true;
+            p_orow = orow;
+            p_live = live;
+            p_pass = pass;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const bool lv = (live >> (8 * m + 7)) & 1u;
-                    const int32_t k = kbase + __popc(mword & ((1u << ((c0 + m) & 31)) - 1u));  // earlier pixels in the word
-                    resp[m] = 0.0f;
-                    if (lv && (score[m] > 0 || k >= off.k0))
-                        resp[m] = static_cast<float>(score[m]) + fast_offset(off.nseg, seg_k, seg_o, seg_inc, k);
-                    fl[m] = lv && resp[m] > a.thr;
-                }
-            } else {
-                const int32_t krow = (orow - 3) * (cols - 6) - 3;  // k = krow + column
-                const int32_t kmin = krow + cmin, kmax = krow + cmax;
-                while (sg + 1 < off.nseg && seg_k[sg + 1] <= kmin) ++sg;  // (uniform; rows only move forward)
-                if (sg + 1 >= off.nseg || seg_k[sg + 1] > kmax) {     // the whole row step in one segment
-                    const float os = seg_o[sg], inc = seg_inc[sg];
-                    const int32_t kr = krow + c0 - seg_k[sg];
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        resp[m] = static_cast<float>(score[m]) + __builtin_fmaf(static_cast<float>(kr + m), inc, os);
-                        fl[m] = colv[m] && resp[m] > a.thr;
-                    }
-                } else {
-#pragma unroll
-                    for (int m = 0; m < 4; ++m) {
-                        resp[m] = 0.0f;
-                        if (colv[m]) resp[m] = static_cast<float>(score[m]) +
-                                               fast_offset(off.nseg, seg_k, seg_o, seg_inc, krow + c0 + m);
-                        fl[m] = colv[m] && resp[m] > a.thr;
-                    }
-                }
+            for (int m = 0; m < 4; ++m) {
+                p_sb[m] = sb[m];
+                p_sd[m] = sd[m];
             }
-            const uint64_t b[4] = {ballot(fl[0]), ballot(fl[1]), ballot(fl[2]), ballot(fl[3])};
-            emit_row<RASTER, kSegFast>(sk, a, f, tx, orow, c0, b, fl, resp);
-            if constexpr (RASTER) {
-                if (a.resp_map != nullptr) {
-                    float *mrow = a.resp_map + (static_cast<int64_t>(f) * rows + orow) * cols;
+#else
+            int score[4];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m)
-                        if (fl[m]) mrow[c0 + m] = resp[m];
-                }
-            }
+            for (int m = 0; m < 4; ++m) score[m] = ((pass >> (8 * m + 7)) & 1u) ? static_cast<int>(max(sb[m], sd[m])) : 0;
+            finish_row(orow, live, score);
+#endif
         }
     }
+#if FD_FAST_PIPE
+    if (pend) finish_pending();
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -73,6 +73,12 @@ struct fd_ctx {
     hipStream_t aux = nullptr;
     hipEvent_t l_ev0 = nullptr, l_ev1 = nullptr;
     HostBuf h_png;  // fd_png_frames: decoded samples of a batch (pinned)
+    // host-output selection calls: status words, counts and features come back in one copy into h_res
+    // (pinned); the status words stay cached on the host (h_status) for fd_ctx_frame_status until the
+    // next selection call
+    HostBuf h_res;
+    std::vector<uint32_t> h_status;
+    bool h_status_valid = false;
     DevBuf d_png;
     std::vector<int32_t> st_idx;
     std::vector<float> st_norm, st_angle;
@@ -373,7 +379,7 @@ int64_t detect_list_cap(int kind, int rows, int cols) {
 }
 
 struct SelectBufs {
-    uint32_t *hist0, *list_count, *pre_count, *seg_bad;
+    uint32_t *hist0, *list_count, *pre_count, *seg_bad, *wide_count, *wide_cut;
     uint64_t *pre_keys, *wide_keys;
     uint32_t *status, *cand_n;
 };
@@ -384,7 +390,7 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     FD_HIP_TRY(c, ensure(c, c->list_idx, sizeof(uint32_t) * cap * batch));
     FD_HIP_TRY(c, ensure(c, c->pre_keys, sizeof(uint64_t) * fdk::kSelectChunk * batch));
     FD_HIP_TRY(c, ensure(c, c->wide_keys, sizeof(uint64_t) * fdk::kWideKeys * batch));
-    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 3);
+    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 5);
     if (c->selctl.n < ctl) {
         FD_HIP_TRY(c, ensure(c, c->selctl, ctl));
         c->sel_dirty = true;
@@ -398,6 +404,8 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     sb.list_count = base + static_cast<size_t>(batch) * fdk::kHistBins;
     sb.pre_count = sb.list_count + batch;
     sb.seg_bad = sb.pre_count + batch;
+    sb.wide_count = sb.seg_bad + batch;
+    sb.wide_cut = sb.wide_count + batch;
     sb.pre_keys = as<uint64_t>(c->pre_keys);
     sb.wide_keys = as<uint64_t>(c->wide_keys);
     FD_HIP_TRY(c, ensure(c, c->status, sizeof(uint32_t) * 2 * static_cast<size_t>(batch)));
@@ -478,6 +486,9 @@ int ref_buffers(fd_ctx *c, int batch, int rows, int cols, int64_t cap, fdk::RefS
     r.rpos = as<uint32_t>(c->r_rpos);
     r.ord = as<uint32_t>(c->r_ord);
     r.cap = rcap;
+    // diagnostic (FD_DEBUG_AB=1): a low bound on k_select_reference's window x level loop, so that tests
+    // reach its failure path (FD_FRAME_UNRESOLVED, host fallback) on small inputs
+    if (const char *e = ab_env("FD_REF_GUARD")) r.guard_limit = std::max(0, std::atoi(e));
     return FD_OK;
 }
 
@@ -629,19 +640,31 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     }
     float *dxy = out_xy;
     int32_t *dcnt = out_counts;
+    c->h_status_valid = false;
+    // Host outputs: the counts and features are written behind the status words (status | candidate
+    // counts | feature counts | features, one buffer), so that all of it returns in one copy into
+    // pinned memory and one synchronisation (three pageable copies and a status read cost ~40 us more
+    // per 640x480 frame).
+    const size_t res_head = (sizeof(uint32_t) * 3 * static_cast<size_t>(batch) + 15) & ~size_t(15);
+    const size_t res_bytes = res_head + sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch;
+    SelectBufs sbl = sb;
     if (!outputs_on_device) {
-        FD_HIP_TRY(c, ensure(c, c->out_xy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch));
-        FD_HIP_TRY(c, ensure(c, c->out_counts, sizeof(int32_t) * batch));
-        dxy = as<float>(c->out_xy);
-        dcnt = as<int32_t>(c->out_counts);
+        if (c->status.n < res_bytes) {  // (grow: the selection's status words move with it)
+            FD_HIP_TRY(c, ensure(c, c->status, res_bytes));
+            sbl.status = as<uint32_t>(c->status);
+            sbl.cand_n = sbl.status + batch;
+        }
+        FD_HIP_TRY(c, ensure_host(c->h_res, res_bytes));
+        dcnt = reinterpret_cast<int32_t *>(as<uint32_t>(c->status) + 2 * static_cast<size_t>(batch));
+        dxy = reinterpret_cast<float *>(static_cast<uint8_t *>(c->status.p) + res_head);
     }
     s.out_xy = dxy;
     s.out_stride = out_stride;
     s.out_counts = dcnt;
     s.key_base = q.key_base;
     s.key_lz = q.key_lz;
-    s.status = sb.status;
-    s.cand_n = sb.cand_n;
+    s.status = sbl.status;
+    s.cand_n = sbl.cand_n;
     // Small batches of large frames: spread the first chunk's gather over ~256 workgroups in its own
     // kernel (~9 us of fixed cost: pays off once one workgroup's pass over the list costs more, i.e.
     // from about a megapixel per frame; measured at 640x480: break-even).
@@ -657,6 +680,18 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     // top bins and the greedy scan runs over several chunks (1280x720 noise: ~5k), so the wide pass
     // comes with the first chunk; the corner detectors usually finish within it (wide pass deferred).
     s.wide_eager = q.wide_eager ? 1 : 0;
+    // ... and its list pass is spread over the frame's list by k_wide_gather, ~16k entries per workgroup
+    // at FAST's ~30 % candidate density on noise (one workgroup read the whole list before: 1280x720,
+    // ~55k of k_select's ~130k cycles per frame). FD_WIDE_GROUPS=0: off (A/B).
+    if (s.wide_eager && s.wide_keys && !s.pre_keys && !q.value_flag) {
+        const int64_t est = static_cast<int64_t>(rows) * cols * 3 / 10;
+        s.wide_groups = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, (est + 16383) / 16384)));
+        if (const char *e = ab_env("FD_WIDE_GROUPS")) s.wide_groups = std::max(0, std::atoi(e));
+        if (s.wide_groups > 0) {
+            s.wide_count = sb.wide_count;
+            s.wide_cut = sb.wide_cut;
+        }
+    }
     if (q.segdesc && !s.pre_keys) {
         s.segdesc = q.segdesc;
         s.seghead = q.seghead;
@@ -709,7 +744,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     }
     if (c->tie_order == FD_TIES_REFERENCE && !q.tie_idx_desc) {
         if (host_ties_env()) {  // the round-3 host path (A/B and checker): every flagged frame sorted on the host
-            const int rc = resolve_ties(c, s, batch, sb, q.push_order, FD_FRAME_TIES);
+            const int rc = resolve_ties(c, s, batch, sbl, q.push_order, FD_FRAME_TIES);
             if (rc) return rc;
         } else {
             fdk::RefSortArgs r{};
@@ -762,18 +797,20 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
                                      h[8 * b + 1], h[8 * b + 2], h[8 * b + 3], h[8 * b + 4]);
             }
             if (!outputs_on_device) {  // the call synchronises anyway: frames left to the host
-                const int rc2 = resolve_ties(c, s, batch, sb, q.push_order, FD_FRAME_UNRESOLVED);
+                const int rc2 = resolve_ties(c, s, batch, sbl, q.push_order, FD_FRAME_UNRESOLVED);
                 if (rc2) return rc2;
             }
         }
     }
     if (!outputs_on_device) {
-        std::vector<uint32_t> st(static_cast<size_t>(batch));
-        FD_HIP_TRY(c, hipMemcpyAsync(out_xy, dxy, sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch,
-                                     hipMemcpyDeviceToHost, c->stream));
-        FD_HIP_TRY(c, hipMemcpyAsync(out_counts, dcnt, sizeof(int32_t) * batch, hipMemcpyDeviceToHost, c->stream));
-        FD_HIP_TRY(c, hipMemcpyAsync(st.data(), sb.status, sizeof(uint32_t) * batch, hipMemcpyDeviceToHost, c->stream));
+        FD_HIP_TRY(c, hipMemcpyAsync(c->h_res.p, c->status.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
+        const uint32_t *st = static_cast<const uint32_t *>(c->h_res.p);
+        std::memcpy(out_counts, st + 2 * static_cast<size_t>(batch), sizeof(int32_t) * batch);
+        std::memcpy(out_xy, static_cast<const uint8_t *>(c->h_res.p) + res_head,
+                    sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch);
+        c->h_status.assign(st, st + batch);
+        c->h_status_valid = true;
         for (int b = 0; b < batch; ++b) {
             if (st[b] & FD_FRAME_VALUE_RANGE)
                 return fail(c, FD_ERR_INVALID, "frame " + std::to_string(b) + ": " + q.value_msg);
@@ -862,7 +899,7 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->r_rpos,   &c->r_ord,    &c->r_ctl,       &c->r_wcnt,      &c->r_wfr,
                       &c->l_sresp,  &c->l_sidx,   &c->l_sst};
     if (c->aux) (void)hipStreamSynchronize(c->aux);
-    for (HostBuf *b : {&c->h_lists, &c->h_png, &c->h_ord, &c->h_sst}) release(*b);
+    for (HostBuf *b : {&c->h_lists, &c->h_png, &c->h_ord, &c->h_sst, &c->h_res}) release(*b);
     release(c->d_png);
     for (DevBuf *b : bufs) release(*b);
     if (c->xev) (void)hipEventDestroy(c->xev);
@@ -926,6 +963,17 @@ int fd_ctx_frame_status(fd_ctx *c, uint32_t *dst, int batch, int async) {
         return fail(c, FD_ERR_INVALID, "the last selection call had " + std::to_string(c->status_batch) + " frames");
     if (batch == 0) return FD_OK;
     FD_HIP_TRY(c, hipSetDevice(c->device));
+    if (c->h_status_valid && static_cast<size_t>(batch) <= c->h_status.size()) {
+        // the last selection call returned host outputs and left its status words here: a host
+        // destination is served without a device round trip (device memory still gets a copy)
+        hipPointerAttribute_t at{};
+        const hipError_t e = hipPointerGetAttributes(&at, dst);
+        if (e != hipSuccess) (void)hipGetLastError();  // (unregistered host memory on some runtimes)
+        if (e != hipSuccess || at.type == hipMemoryTypeHost || at.type == hipMemoryTypeUnregistered) {
+            std::memcpy(dst, c->h_status.data(), sizeof(uint32_t) * batch);
+            return FD_OK;
+        }
+    }
     FD_HIP_TRY(c, hipMemcpyAsync(dst, c->status.p, sizeof(uint32_t) * batch, hipMemcpyDefault, c->stream));
     if (!async) FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
     return FD_OK;
@@ -1530,6 +1578,15 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
     const bool host_sort = ab_env("FD_LSD_HOST_SORT") && std::atoi(ab_env("FD_LSD_HOST_SORT")) != 0;
     bool gpu_seeds = false;
     int64_t ord_stride = 0;
+    // Once the seed sort is launched on the side stream it uses the context's shared scratch (the
+    // k_select_reference buffers, h_ord): every return from here on drains it first, so that no later
+    // call on the context stream races it (the normal path has waited for it already).
+    struct AuxDrain {
+        hipStream_t s = nullptr;
+        ~AuxDrain() {
+            if (s) (void)hipStreamSynchronize(s);
+        }
+    } drain;
     const auto t_start = std::chrono::steady_clock::now();
     FD_HIP_TRY(c, hipSetDevice(c->device));
     const uint8_t *dframes = nullptr;
@@ -1576,6 +1633,7 @@ int fd_lsd_lines(fd_ctx *c, const uint8_t *frames, int frames_on_device, int bat
             // runs beside it on the side stream)
             FD_HIP_TRY(c, hipMemcpyAsync(c->h_lists.p, a.idx, sizeof(uint32_t) * 3 * sec, hipMemcpyDeviceToHost, c->stream));
             if (!host_sort) {
+                drain.s = c->aux;
                 const int rc2 = lsd_seed_order(c, batch, rows - 1, cols - 1, base, a, ord_stride);
                 if (rc2) return rc2;
                 gpu_seeds = true;

@@ -186,6 +186,8 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     uint32_t *const grid_g = a.grid_global ? a.grid_global + static_cast<int64_t>(f) * cells : nullptr;
     const uint32_t prior = a.prior_counts ? static_cast<uint32_t>(a.prior_counts[f]) : 0u;
     const uint32_t *fmask = a.mask ? a.mask + static_cast<int64_t>(f) * rows * a.mask_wpr : nullptr;
+    // k_wide_gather's key count (the previous kernel), loaded now: it lands during the histogram scan
+    const uint32_t wide_pre_n = (WIDE && a.wide_count) ? a.wide_count[f] : 0xFFFFFFFFu;
     if (a.stamps && tid == 0)
         for (int i = 0; i < 32; ++i) L.st[i] = 0;
     FD_STAMP(0);
@@ -234,7 +236,9 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             pre_key[k] = a.seghead[(static_cast<int64_t>(f) * a.nseg + sgc) * kSegHead + e];
         }
     }
-    if (!a.pre_keys && !seg_mode) {
+    // (not for a pre-gathered wide pass: its first chunk comes from the wide scratch)
+    const bool list_prefetch = !a.pre_keys && !seg_mode && !(WIDE && a.wide_count);
+    if (list_prefetch) {
         const uint32_t last = static_cast<uint32_t>(min(a.list_cap, static_cast<int64_t>(0xFFFFFFFF))) - 1u;
 #pragma unroll
         for (int k = 0; k < kRegGather; ++k)
@@ -529,10 +533,15 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         const int wl = first_le(suf0, 0, hi_bin + 1, suf0[hi_bin + 1], static_cast<uint32_t>(kWideKeys));
         if (wl > hi_bin) return;  // the bin alone holds more than kWideKeys keys
         const uint32_t k32hi = hi_bin == kHistBins - 1 ? 0xFFFFFFFFu : (static_cast<uint32_t>(hi_bin + 1) << 20) - 1u;
-        wide_gather(static_cast<uint32_t>(wl) << 20, k32hi);
         const uint32_t expect = suf0[wl] - suf0[hi_bin + 1];
-        if (tid == 0 && gcount != expect)  // consistency guard: gathered == histogram count
-            atomicOr(&a.status[f], 0x04000000u);
+        // k_wide_gather took the same cut from the same histogram (the top bins holding <= kWideKeys
+        // keys) and already holds them in wk; a different count means it did not (e.g. the top bin alone
+        // exceeds kWideKeys there): this workgroup makes the pass itself
+        if (!(hi_bin == kHistBins - 1 && wide_pre_n == expect)) {
+            wide_gather(static_cast<uint32_t>(wl) << 20, k32hi);
+            if (tid == 0 && gcount != expect)  // consistency guard: gathered == histogram count
+                atomicOr(&a.status[f], 0x04000000u);
+        }
         wide_lo = wl;
         wide_hi = hi_bin;
         wide_n = min(expect, static_cast<uint32_t>(kWideKeys));
@@ -640,7 +649,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             } else {
                 if (a.pre_keys && tid == 0)  // consistency guard: k_gather saw a different cut
                     atomicOr(&a.status[f], 0x02000000u);
-                gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, (a.pre_keys || seg_mode) ? nullptr : pre_lds);
+                gather_exact(static_cast<uint32_t>(lo_b) << 20, 0xFFFFFFFFu, list_prefetch ? pre_lds : nullptr);
             }
             first_ready = true;
         }
@@ -650,7 +659,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     if (use_grid && grid_in_lds) {  // the first round's LDS-direct loads are consumed (or never used)
         // vmcnt(0): no load still landing in this space (only if they were issued: the wait would
         // also hold for this thread's outstanding global stores and atomics, a memory round trip)
-        if (!a.pre_keys && !seg_mode) __builtin_amdgcn_s_waitcnt(0x0F70);
+        if (list_prefetch) __builtin_amdgcn_s_waitcnt(0x0F70);
         __syncthreads();
         for (int i = tid; i < cells; i += nthr) grid_lds[i] = grid_empty(rows, cols, d);
         __syncthreads();
@@ -1187,6 +1196,10 @@ __device__ __forceinline__ void finish_frame(const SelectArgs &a, const int f) {
         __hip_atomic_store(&a.list_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.pre_count) __hip_atomic_store(&a.pre_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.seg_bad) __hip_atomic_store(&a.seg_bad[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (wide_cut too: the control block's layout depends on the batch, so a word left non-zero here
+        // could be a histogram bin of a later call with another batch size)
+        if (a.wide_count) __hip_atomic_store(&a.wide_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.wide_cut) __hip_atomic_store(&a.wide_cut[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1201,8 +1214,143 @@ __global__ __launch_bounds__(1024) void k_gather(SelectArgs a) {
     const GatherView v{a.list_resp + static_cast<int64_t>(f) * a.list_cap, a.list_idx + static_cast<int64_t>(f) * a.list_cap,
                        min(static_cast<int64_t>(a.list_count[f]), a.list_cap), a.hist0 + static_cast<int64_t>(f) * kHistBins,
                        a.key_base, a.key_lz, a.tie_idx_desc, a.pre_keys + static_cast<int64_t>(f) * kSelectChunk,
-                       a.pre_count + f};
+                       a.pre_count + f, static_cast<uint32_t>(kSelectChunk)};
     gather_first_chunk<1024>(v, g, G, L);
+}
+
+// Wide pass (FAST, SelectArgs::wide_count) in two kernels: k_wide_cut finds each frame's cut (the top
+// level-0 bins holding <= kWideKeys candidates) once, from the complete histogram; k_wide_gather then
+// streams the frame's list over wide_groups workgroups and appends the keys at or above the cut to the
+// frame's wide scratch. In k_select one workgroup made this pass (FAST on 1280x720 noise: ~270k
+// candidates, ~55k of ~130k cycles per frame); a cut per gather workgroup cost more than the pass.
+__global__ __launch_bounds__(256) void k_wide_cut(SelectArgs a) {
+    __shared__ uint32_t wt[4];
+    __shared__ int res;
+    const int f = blockIdx.x, tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    static_assert(kHistBins == 256 * 16, "16 bins per thread");
+    const uint4 *h = reinterpret_cast<const uint4 *>(a.hist0 + static_cast<int64_t>(f) * kHistBins) + 4 * tid;
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint4 q = h[j];
+        v[4 * j] = q.x;
+        v[4 * j + 1] = q.y;
+        v[4 * j + 2] = q.z;
+        v[4 * j + 3] = q.w;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sum += v[j];
+    const uint32_t incl = wave_suffix_add(sum);  // this thread's bins and every higher thread's in the wave
+    if (lane == 0) wt[wave] = incl;
+    if (tid == 0) res = kHistBins;
+    __syncthreads();
+    uint32_t run = incl - sum;  // keys in bins above this thread's, within the wave ...
+    for (int w = wave + 1; w < 4; ++w) run += wt[w];  // ... and in the higher waves
+    // smallest bin b with (keys in bins >= b) <= kWideKeys: the suffix is non-increasing in b
+    int best = kHistBins;
+    uint32_t best_s = 0;
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+        run += v[j];
+        if (run <= static_cast<uint32_t>(kWideKeys)) {
+            best = 16 * tid + j;
+            best_s = run;
+        }
+    }
+    if (best < kHistBins) atomicMin(&res, best);
+    __syncthreads();
+    __shared__ uint32_t res_s;
+    if (tid == 0) res_s = 0;
+    __syncthreads();
+    if (best == res) res_s = best_s;  // (one thread: the bins are disjoint)
+    __syncthreads();
+    if (tid == 0) {
+        // no keys at or above the cut (none at all, or the bin below it alone holds more than kWideKeys),
+        // or the top bin alone holds more: nothing to gather (k_select descends itself), as in k_select's
+        // own wide pass
+        const bool none = res >= kHistBins || res_s == 0u;
+        a.wide_cut[f] = none ? static_cast<uint32_t>(kHistBins) : static_cast<uint32_t>(res);
+    }
+}
+
+constexpr int kWidePer = 16;      // list entries per thread and round of k_wide_gather (4 x 16-byte loads)
+constexpr int kWideThreads = 1024;  // k_wide_gather workgroup
+// One reservation on the frame's key counter per workgroup and round (a block prefix of the waves' hit
+// counts): same-address device atomics serialise at the memory side (256-thread workgroups with one
+// atomic per wave measured 41-60 us for 64 frames of 1280x720 FAST, slower with more workgroups).
+__global__ __launch_bounds__(kWideThreads) void k_wide_gather(SelectArgs a) {
+    __shared__ uint32_t wsum[kWideThreads / kWave];
+    __shared__ uint32_t wg_base;
+    const int G = a.wide_groups;
+    const int f = blockIdx.x / G, g = blockIdx.x % G;
+    const uint32_t cut = a.wide_cut[f];
+    if (cut >= static_cast<uint32_t>(kHistBins)) return;
+    const uint32_t k32lo = cut << 20;
+    const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+    const uint32_t n = static_cast<uint32_t>(min(static_cast<int64_t>(a.list_count[f]), a.list_cap));
+    const float *lresp = a.list_resp + static_cast<int64_t>(f) * a.list_cap;
+    const uint32_t *lidx = a.list_idx + static_cast<int64_t>(f) * a.list_cap;
+    // (list_cap < 2^30 entries, checked on the host: the byte offsets fit the resource; loads past the
+    // frame's capacity read 0)
+    const auto rres = make_rsrc(lresp, static_cast<uint32_t>(a.list_cap) * 4u);
+    const auto ridx = make_rsrc(lidx, static_cast<uint32_t>(a.list_cap) * 4u);
+    uint64_t *wk = a.wide_keys + static_cast<int64_t>(f) * kWideKeys;
+    constexpr uint32_t kRound = static_cast<uint32_t>(kWideThreads) * kWidePer;
+    // (the loop bounds are uniform across the workgroup: every thread reaches every barrier)
+    for (uint32_t base = static_cast<uint32_t>(g) * kRound; base < n; base += static_cast<uint32_t>(G) * kRound) {
+        // wave w reads the contiguous 4 KiB [base + 1024 w, +1024): its lanes' 16-byte loads side by side
+        const uint32_t i0 = base + static_cast<uint32_t>(wave) * (kWave * kWidePer) + 4u * static_cast<uint32_t>(lane);
+        float r[kWidePer];
+#pragma unroll
+        for (int j = 0; j < kWidePer / 4; ++j) {
+            const auto q = __builtin_amdgcn_raw_buffer_load_b128(rres, static_cast<int>(4u * (i0 + 256u * j)), 0, 0);
+            r[4 * j] = __uint_as_float(q[0]);
+            r[4 * j + 1] = __uint_as_float(q[1]);
+            r[4 * j + 2] = __uint_as_float(q[2]);
+            r[4 * j + 3] = __uint_as_float(q[3]);
+        }
+        auto at = [&](int j) { return i0 + 256u * static_cast<uint32_t>(j >> 2) + static_cast<uint32_t>(j & 3); };
+        uint32_t hm = 0;
+#pragma unroll
+        for (int j = 0; j < kWidePer; ++j)
+            hm |= static_cast<uint32_t>(at(j) < n && sel_key32(r[j], a.key_base, a.key_lz) >= k32lo) << j;
+        const uint32_t cnt = __popc(hm);
+        const uint32_t incl = wave_incl_add(cnt);
+        if (lane == kWave - 1) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kWideThreads / kWave; ++w) {
+            const uint32_t v = wsum[w];
+            before += w < wave ? v : 0u;
+            total += v;
+        }
+        if (tid == 0) wg_base = total ? atomicAdd(&a.wide_count[f], total) : 0u;
+        __syncthreads();
+        uint32_t pos = wg_base + before + incl - cnt;
+        if (hm) {
+            // the pixel indices of this thread's entries in one round trip (not one dependent load per hit)
+            uint32_t ix[kWidePer];
+#pragma unroll
+            for (int j = 0; j < kWidePer / 4; ++j) {
+                const auto q = __builtin_amdgcn_raw_buffer_load_b128(ridx, static_cast<int>(4u * (i0 + 256u * j)), 0, 0);
+                ix[4 * j] = q[0];
+                ix[4 * j + 1] = q[1];
+                ix[4 * j + 2] = q[2];
+                ix[4 * j + 3] = q[3];
+            }
+#pragma unroll
+            for (int j = 0; j < kWidePer; ++j) {
+                if ((hm >> j) & 1u) {
+                    if (pos < static_cast<uint32_t>(kWideKeys))
+                        wk[pos] = sel_key64(r[j], ix[j], a.key_base, a.key_lz, a.tie_idx_desc);
+                    ++pos;
+                }
+            }
+        }
+        __syncthreads();  // (wsum / wg_base reused by the next round)
+    }
 }
 
 template <int NT, bool WIDE>
@@ -1304,6 +1452,12 @@ hipError_t launch_select_ordered(const SelectArgs &a, const OrderedArgs &o, int 
 hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
     if (a.pre_keys) {
         hipLaunchKernelGGL(k_gather, dim3(static_cast<unsigned>(batch * a.gather_groups)), dim3(1024), 0, s, a);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (a.wide_count && a.wide_keys && a.wide_groups > 0) {
+        hipLaunchKernelGGL(k_wide_cut, dim3(static_cast<unsigned>(batch)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_wide_gather, dim3(static_cast<unsigned>(batch * a.wide_groups)), dim3(kWideThreads), 0, s, a);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

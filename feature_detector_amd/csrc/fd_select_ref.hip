@@ -733,7 +733,13 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
     if (wv == 0) set_active(L, kSelectChunk);
     __syncthreads();
 
-    for (int guard = 0; guard < 1 << 16; ++guard) {  // windows x levels (bounded: each level halves)
+    // windows x levels (bounded: each level halves). A frame whose emulation has not finished when the
+    // bound runs out -- LSD seed orders of ~10M entries would need that many -- is failed (code 8), not
+    // reported resolved with an unwritten tail of ord. (r.guard_limit: diagnostic override only.)
+    const int guard_lim = r.guard_limit > 0 ? r.guard_limit : 1 << 16;
+    bool finished = false;  // (uniform: set where every thread leaves the loop together)
+    bool wrote = false;     // a window's greedy has written features (out_xy no longer k_select's)
+    for (int guard = 0; guard < guard_lim; ++guard) {
         const int m = L.m_act;
         if (m > 0) {
             // ---- active ranges at the depth limit: std::__partial_sort(first, last, last) -----------------
@@ -755,7 +761,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
             const uint64_t t_level = a.stamps && tid == 0 ? __builtin_readcyclecounter() : 0ull;
             if (tid < m) {
                 const uint32_t lo = L.r_lo[c][tid], hi = L.r_hi[c][tid];
-                if (L.r_dep[c][tid] == 0u) L.fail = 1;  // std::__partial_sort: not emulated
+                if (L.r_dep[c][tid] == 0u) L.fail = 1;  // invariant: depth-0 ranges were heapsorted above
                 const uint32_t mid = lo + (hi - lo) / 2u;
                 const uint2 xa = X[FD_REF_IDX(lo + 1, n, 2)], xb = X[FD_REF_IDX(mid, n, 2)], xc = X[FD_REF_IDX(hi - 1, n, 2)];
                 const uint32_t ch = median_pos(as_f(xa.x), as_f(xb.x), as_f(xc.x), lo + 1, mid, hi - 1);
@@ -1202,6 +1208,7 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         }
         for (uint32_t base = fin; base < fin_new && !r.order_only; base += kSelectChunk) {
             if (L.s_done) break;
+            wrote = true;
             const int cn = static_cast<int>(min(static_cast<uint32_t>(kSelectChunk), fin_new - base));
             for (int i = tid; i < cn; i += NT) {
                 uint32_t idx = ord[FD_REF_IDX(base + i, n, 18)];
@@ -1236,7 +1243,10 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         }
         FD_REF_MARK(21);  // greedy over the finished window
         FD_REF_COUNT(22, 1u);
-        if (L.s_done || fin_new >= n) break;
+        if (L.s_done || fin_new >= n) {
+            finished = true;
+            break;
+        }
         if (wv == 0) {
             if (lane == 0) L.fin = fin_new;
             __builtin_amdgcn_s_waitcnt(0);
@@ -1244,8 +1254,14 @@ __global__ __launch_bounds__(NT) void k_select_reference(SelectArgs a, RefSortAr
         }
         __syncthreads();
     }
+    __syncthreads();
     if (tid == 0) {
+        if (!finished && !L.fail) L.fail = 8;  // the loop bound ran out
         if (L.fail) {
+            // Device outputs of a failed frame: k_select's features (raster tie order) while no window
+            // has been scanned; else the features the reference order accepted so far -- a prefix of the
+            // reference's result, not a mix of the two orders. Host-output calls resolve it on the host.
+            if (wrote) a.out_counts[f] = L.s_acc;
             atomicOr(&a.status[f], FD_FRAME_UNRESOLVED);
         } else {
             if (!r.order_only) a.out_counts[f] = L.s_acc;

@@ -348,7 +348,9 @@ def conv1ab_bias_relu(x, weight1, bias1, weight, bias, pool: bool = True, out=No
     """fd_nn_conv3x3_c1c64: the encoder's first two layers in one pass -- conv1a (1 -> 64, 3x3, bias, ReLU)
     recomputed inside conv1b's tiles (64 -> 64, 3x3, bias, ReLU, and the 2x2 max pool when pool), so the
     full-resolution 64-channel activation never goes to memory. x [N, 1, H, W] fp16 on the device ->
-    [N, 64, H(/2), W(/2)] fp16 channels-last; equal bit for bit to conv64_bias_relu(conv1_bias_relu(x))."""
+    [N, 64, H(/2), W(/2)] fp16 channels-last; equal to conv64_bias_relu(conv1_bias_relu(x)) within fp16
+    rounding (conv1a runs on the matrix cores here, in a different summation order than conv1_bias_relu's
+    FMA chain, so a conv1a value may round to the neighbouring half)."""
     import torch
 
     if not (x.is_cuda and x.dtype == torch.float16 and x.dim() == 4 and x.shape[1] == 1

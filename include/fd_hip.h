@@ -75,10 +75,13 @@ int fd_ctx_reserve(fd_ctx *ctx, int kind, int batch, int rows, int cols, int64_t
  *                      (GCC 11) std::sort leaves the raster-ordered candidates in (its introsort is
  *                      emulated over the visited prefix; FD_FRAME_RESOLVED). Frames without such a tie
  *                      are identical in both modes. Asynchronous and graph-capturable (reserve first,
- *                      fd_ctx_reserve after fd_ctx_set_tie_order). If the sort would reach its depth limit
- *                      (heapsort) inside the visited prefix, the frame gets FD_FRAME_UNRESOLVED instead:
- *                      host-output calls then resolve it on the host; device-output calls leave its
- *                      features undefined and the flag in fd_ctx_frame_status.
+ *                      fd_ctx_reserve after fd_ctx_set_tie_order). The depth limit's heapsort is emulated
+ *                      too. A frame that breaks one of the emulation's capacity guards or its loop bound
+ *                      gets FD_FRAME_UNRESOLVED instead: host-output calls then resolve it on the host;
+ *                      device-output calls return k_select's raster-order features for it (if no window
+ *                      of the reference order was scanned) or the features the reference order selected
+ *                      before the stop (a prefix of the reference's result), with the flag in
+ *                      fd_ctx_frame_status.
  * SuperPoint's fd_nn_select has a defined order (std::multimap) and ignores this setting.
  */
 enum fd_tie_order { FD_TIES_RASTER = 0, FD_TIES_REFERENCE = 1 };
@@ -92,7 +95,7 @@ int fd_ctx_set_tie_order(fd_ctx *ctx, int order);
  */
 #define FD_FRAME_TIES 0x00000001u       /* equal responses met in the greedy scan (order defined by the mode) */
 #define FD_FRAME_RESOLVED 0x00000002u   /* re-selected in the reference's std::sort order (FD_TIES_REFERENCE) */
-#define FD_FRAME_UNRESOLVED 0x00000004u /* FD_TIES_REFERENCE: not emulated on the GPU (see fd_tie_order) */
+#define FD_FRAME_UNRESOLVED 0x00000004u /* FD_TIES_REFERENCE: the GPU emulation stopped (see fd_tie_order) */
 #define FD_FRAME_VALUE_RANGE 0x40000000u /* fd_nn_select: a heatmap value above fd_nn_opts::max_response */
 #define FD_FRAME_GUARD 0xBE000000u      /* internal consistency guard tripped (host-output calls fail FD_ERR_HIP) */
 int fd_ctx_frame_status(fd_ctx *ctx, uint32_t *dst, int batch, int async);
@@ -393,9 +396,10 @@ int fd_nn_conv3x3_c64(fd_ctx *ctx, const void *x, const void *weight_packed, con
  * fd_nn_conv3x3_c1c64 -- SuperPoint's first two layers in one pass: conv1a (1 -> 64 channels, 3x3, bias,
  * ReLU) fused into conv1b (64 -> 64, 3x3, bias, ReLU, with pool = 1 the 2x2 max pool): x [n][h][w] fp16,
  * weight1 [64][1][3][3] fp16, bias1 [64], weight_packed / bias as fd_nn_conv3x3_c64, y [n][h(/2)][w(/2)][64]
- * channels-last fp16, all on the device. Equal to fd_nn_conv3x3_c1 followed by fd_nn_conv3x3_c64 bit for
- * bit (conv1a is recomputed per conv1b tile with the same arithmetic; its full-resolution 64-channel output
- * never goes to memory). w <= 4096; x 2-byte, y and weight_packed 16-byte aligned; pool needs even h, w.
+ * channels-last fp16, all on the device. Equal to fd_nn_conv3x3_c1 followed by fd_nn_conv3x3_c64 within
+ * fp16 rounding: conv1a is recomputed per conv1b tile on the matrix cores, whose summation order differs
+ * from fd_nn_conv3x3_c1's FMA chain, so a conv1a value may round to the neighbouring half (its
+ * full-resolution 64-channel output never goes to memory). w <= 4096; x 2-byte, y and weight_packed 16-byte aligned; pool needs even h, w.
  */
 int fd_nn_conv3x3_c1c64(fd_ctx *ctx, const void *x, const void *weight1, const void *bias1, const void *weight_packed,
                         const void *bias, void *y, int n, int h, int w, int pool);

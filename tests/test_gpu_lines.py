@@ -138,3 +138,22 @@ def test_seed_order_on_gpu(oracle, monkeypatch, capfd):
         assert f"seed orders from the gpu {frames.shape[0]}" in capfd.readouterr().err
         monkeypatch.delenv("FD_LSD_WIDE")
         assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(got, wide))
+
+
+def test_seed_order_guard_failure_falls_back(oracle, monkeypatch, capfd):
+    # the seed sort's loop bound cut short (FD_REF_GUARD, diagnostic) right after a full GPU call of the
+    # same frames: every frame must be reported unresolved -- not resolved with the previous call's order
+    # still in the pinned buffer's tail -- and be sorted on the host, with the oracle's segments
+    import feature_detector_amd as fd
+
+    frames = np.stack([oracle.make_frame("checker", 21, 400, 600, 24), oracle.make_frame("noise", 22, 400, 600, 16)])
+    monkeypatch.setenv("FD_DEBUG_AB", "1")
+    monkeypatch.setenv("FD_LINES_TIMING", "1")
+    capfd.readouterr()
+    full = _check(fd, oracle, frames)
+    assert f"seed orders from the gpu {frames.shape[0]}" in capfd.readouterr().err
+    for guard in (1, 3):
+        monkeypatch.setenv("FD_REF_GUARD", str(guard))
+        got = _check(fd, oracle, frames)
+        assert "seed orders from the gpu 0" in capfd.readouterr().err
+        assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(got, full))

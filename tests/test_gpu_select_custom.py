@@ -201,3 +201,34 @@ def test_reference_order_depth_limit(fd, oracle, n):
         g.replay()
         torch.cuda.synchronize()
         assert np.array_equal(xy[0, :int(cnt[0])].cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("guard", [1, 2, 4, 12])
+def test_reference_order_guard_failure(fd, oracle, image_png, monkeypatch, guard):
+    """k_select_reference's window x level loop cut short (FD_REF_GUARD, a diagnostic bound): the frame
+    must come out FRAME_UNRESOLVED -- never FRAME_RESOLVED with an unfinished order -- and its device
+    features must be either k_select's raster-order selection (no window scanned yet) or a prefix of the
+    reference's result, not a mix of the two orders; host outputs fall back to the host sort and equal
+    the reference. A frame the bound does not cut stays resolved and equal to the reference."""
+    monkeypatch.setenv("FD_DEBUG_AB", "1")
+    monkeypatch.setenv("FD_REF_GUARD", str(guard))
+    rows, cols = image_png.shape
+    lst = gradient_candidates(image_png)  # integer responses: ties fill the visited prefix
+    for dist, need in ((20, 200), (3, 2000)):
+        exp0 = oracle.select(*lst, rows, cols, dist, need, None, sort_mode=0)
+        exp1 = oracle.select(*lst, rows, cols, dist, need, None, sort_mode=1)
+        host = fd.select_points([lst], rows, cols, need, dist, ties="reference")
+        assert np.array_equal(host.features(0), exp0), ("host", dist, need)
+        dev = fd.select_points(_dev_lists([lst]), rows, cols, need, dist, ties="reference")
+        st = int(dev.frame_flags()[0])
+        got = dev.features(0)
+        assert st & fd.points.FRAME_TIES, hex(st)
+        if st & fd.points.FRAME_UNRESOLVED:
+            assert not st & fd.points.FRAME_RESOLVED, hex(st)
+            assert (np.array_equal(got, exp1) or
+                    (len(got) < len(exp0) and np.array_equal(got, exp0[:len(got)]))), ("mixed", dist, need, len(got))
+        else:
+            assert st & fd.points.FRAME_RESOLVED, hex(st)
+            assert np.array_equal(got, exp0), ("resolved", dist, need)
+    if guard == 1:  # one iteration cannot finish a frame of thousands of candidates
+        assert st & fd.points.FRAME_UNRESOLVED, hex(st)
