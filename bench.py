@@ -596,12 +596,27 @@ def ranked_time_ms(torch, fn, reps, barrier, max_fn):
 
 
 def copy_bandwidth(torch, dev, nbytes=1 << 30, reps=5):
-    """Measured device-to-device copy bandwidth (read + write bytes / time): the practical HBM ceiling."""
+    """Measured device-to-device copy bandwidth (read + write bytes / time): the practical HBM ceiling.
+    A float4 (16 B per lane) nontemporal grid-stride copy kernel (tools/calib/copy_kernel.hip, the form
+    MI355X_MICROARCH.md measures at ~6.3 TB/s); torch's copy_ beside it for comparison."""
+    import ctypes
+
     a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     b = torch.empty_like(a)
-    ms = graph_time_ms(torch, lambda: b.copy_(a), reps)
+    out = {"torch_copy_gbs": round(2 * nbytes / (graph_time_ms(torch, lambda: b.copy_(a), reps) * 1e-3) / 1e9, 1)}
+    so = os.path.join(ROOT, "tools", "calib", "libcopybw.so")
+    if os.path.exists(so):
+        lib = ctypes.CDLL(so)
+        lib.fdcal_copy16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+
+        def kcopy():
+            rc = lib.fdcal_copy16(b.data_ptr(), a.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
+            assert rc == 0, rc
+
+        out["kernel_copy_gbs"] = round(2 * nbytes / (graph_time_ms(torch, kcopy, reps) * 1e-3) / 1e9, 1)
     del a, b
-    return round(2 * nbytes / (ms * 1e-3) / 1e9, 1)
+    out["device_copy_gbs"] = max(out.values())
+    return out
 
 
 def run_end_to_end(torch, fd, args, seconds=3.0):
@@ -1022,7 +1037,9 @@ def main():
                                              max_fn=max_fn)
     out["ranks"], out["process_group"] = rank_layout(dist, world, rank, local, dev_index, ndev)
     with phase(torch, "device_copy"):
-        out["device_copy_gbs"] = copy_bandwidth(torch, dev)
+        cb = copy_bandwidth(torch, dev)
+        out["device_copy_gbs"] = cb.pop("device_copy_gbs")
+        out["device_copy"] = cb
     if world == 1:
         with phase(torch, "end_to_end"):
             out["end_to_end_host_frames"] = run_end_to_end(torch, fd, args)

@@ -1,0 +1,38 @@
+// HBM copy ceiling for bench.py (`device_copy_gbs`): a float4 (16 B per lane) grid-stride streaming copy,
+// the form MI355X_MICROARCH.md measures at ~6.3 TB/s (read + write bytes / time). Not part of the
+// product library: bench.py loads it beside libfdhip.so to report the practical HBM ceiling of the
+// byte-moving kernels (the LSD map) next to their achieved rates.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_copy16(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, size_t n16) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+    size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    // 4 independent 16-byte loads per thread in flight per iteration
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const u32x4 a = __builtin_nontemporal_load(src + i);
+        const u32x4 b = __builtin_nontemporal_load(src + i + stride);
+        const u32x4 c = __builtin_nontemporal_load(src + i + 2 * stride);
+        const u32x4 d = __builtin_nontemporal_load(src + i + 3 * stride);
+        __builtin_nontemporal_store(a, dst + i);
+        __builtin_nontemporal_store(b, dst + i + stride);
+        __builtin_nontemporal_store(c, dst + i + 2 * stride);
+        __builtin_nontemporal_store(d, dst + i + 3 * stride);
+    }
+    for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+}  // namespace
+
+// bytes: a multiple of 16; src / dst 16-byte aligned device memory. Enqueued on `stream`.
+extern "C" int fdcal_copy16(void *dst, const void *src, size_t bytes, void *stream) {
+    const size_t n16 = bytes / 16;
+    const unsigned blocks = 256u * 8u;  // 8 workgroups of 256 threads per CU
+    hipLaunchKernelGGL(k_copy16, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       static_cast<const u32x4 *>(src), static_cast<u32x4 *>(dst), n16);
+    return static_cast<int>(hipGetLastError());
+}
