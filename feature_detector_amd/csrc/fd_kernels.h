@@ -81,7 +81,20 @@ struct PointsArgs {
     uint2 *segdesc;
     uint32_t *seg_bad;
     uint64_t *seghead;  // [batch][blocks_per_frame][kSegHead] the segments' first keys (selection keys)
+    // FAST emission cut (detect mode, raster tie order): a candidate whose response is
+    // below the float *emit_cut (bits; null: none) is counted in skipped[f] instead of emitted; workgroup 0
+    // sets *emit_cut_next to +inf, the identity of the selection's proposals for the next call. redo_status:
+    // the second pass, where only the frames whose status word has kFrameRedo run (emitting everything).
+    const uint32_t *emit_cut;
+    uint32_t *emit_cut_next;
+    uint32_t *skipped;
+    const uint32_t *redo_status;
 };
+
+// Internal status bit (SelectArgs::status): the selection ran out of emitted keys of a frame whose
+// per-pixel pass skipped some (FAST emission cut); the frame is detected and selected again in the same
+// call (redo pass), which clears the bit.
+constexpr uint32_t kFrameRedo = 0x00000100u;
 
 struct SelectArgs {
     const float *list_resp;
@@ -122,12 +135,22 @@ struct SelectArgs {
     int nseg;               // segments per frame
     uint64_t *wide_keys;  // [batch][kWideKeys] scratch of the wide pass, or null (one list pass per chunk)
     int wide_eager;       // wide pass with the first chunk (FAST) instead of at the first later list pass
+    int fast_sub;         // FAST's selection shape (k_select<.., true>, whole-superchunk sub-chunks) without a wide
+                          // pass (wide_keys null): the short lists of the emission cut
     // k_wide_cut + k_wide_gather (batch x wide_groups workgroups of 256 threads, before k_select): the wide pass of a
     // wide_eager frame spread over the frame's list, keys into wide_keys, their number into wide_count
     // (reset by k_select); null wide_count: k_select makes the pass itself, one workgroup per frame
     uint32_t *wide_count;
     uint32_t *wide_cut;  // [batch] k_wide_cut's level-0 bin cut (kHistBins: none), read by k_wide_gather
     int wide_groups;
+    // FAST emission cut (PointsArgs::emit_cut): skipped [batch] (reset here), the cut this call used and the
+    // word the frames' proposals for the next call go to (atomicMin of float bits); redo_status: the redo
+    // pass, in which only frames flagged kFrameRedo run (k_wide_cut / k_wide_gather / k_select)
+    uint32_t *skipped;
+    const uint32_t *cut_cur;
+    uint32_t *cut_next;
+    const uint32_t *redo_status;
+    int batch;  // frames of the call (the redo pass's workgroups loop over them)
     int first_sub;     // sorted-segment corner frames: first chunk cut at one sub-chunk (kSubChunk keys)
     int grid_at_d0;    // distance 0 still tests the grid (1-pixel cells): caller lists may name a pixel twice
     int dup_keys;      // equal selection keys possible (caller lists): the orderings rank them stably

@@ -459,44 +459,68 @@ __device__ __forceinline__ float fast_offset(int nseg, const int32_t *ks, const 
 
 template <bool RASTER, bool MASKED, bool ALIGNED>
 __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int32_t *seg_k,
-                                          const float *seg_o, const float *seg_inc, int f, int ty, int tx, Sink &sk);
+                                          const float *seg_o, const float *seg_inc, int f, int ty, int tx, Sink &sk,
+                                          float cut, uint32_t &skip);
 
 template <bool RASTER, bool MASKED, bool ALIGNED>
 __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
     __shared__ DetectLdsT<kStageFast> lds_all[1];
     __shared__ int32_t seg_k[kMaxOffsetSegs];
     __shared__ float seg_o[kMaxOffsetSegs], seg_inc[kMaxOffsetSegs];
+    __shared__ uint32_t seg_ovf;
+    __shared__ uint32_t seg_wtot[4], seg_base;
+    int f, ty, tx;
+    const bool active = decode_tile(a, f, ty, tx);
+    if (a.emit_cut_next && blockIdx.x == 0 && threadIdx.x == 0) *a.emit_cut_next = 0x7F800000u;  // +inf
+    const float cut = a.emit_cut ? __uint_as_float(*a.emit_cut) : -__builtin_inff();
     for (int i = threadIdx.x; i < off.nseg; i += blockDim.x) {
         seg_k[i] = static_cast<int32_t>(off.k_start[i]);  // frames < 2^31 px (checked on the host)
         seg_o[i] = static_cast<float>(off.o_start[i]);     // exact: a float of the sequence
         seg_inc[i] = static_cast<float>(off.inc[i]);       // exact: a difference of two nearby floats
     }
-    int f, ty, tx;
-    const bool active = decode_tile(a, f, ty, tx);
-    __shared__ uint32_t seg_ovf;
-    Sink sk{nullptr, nullptr, nullptr, 0, &seg_ovf};
-    if constexpr (!RASTER) {
-        const int wv = threadIdx.x >> 6;
-        sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0, &seg_ovf};
-        sk.ehist = sk.hist;  // FAST: histogram counted at emit time (measured faster than at flush)
-        sk.hist = nullptr;
-        sk.cap = kStageFast;
-        if (threadIdx.x == 0) seg_ovf = 0;
-        if (a.hist0) hist_clear(lds_all[0].hist);  // (includes the barrier for the segment table)
-        else __syncthreads();
-    } else {
-        __syncthreads();
-    }
-    if (active) fast_tile<RASTER, MASKED, ALIGNED>(a, off, seg_k, seg_o, seg_inc, f, ty, tx, sk);
-    if constexpr (!RASTER) {
-        if (a.segdesc) {
-            __shared__ uint32_t seg_wtot[4], seg_base;
-            seg_flush(sk, a, f, active, lds_all[0], seg_wtot, seg_base);
+    // one frame's tile: staging, the row walk, the flush (every thread of the workgroup)
+    auto run = [&](int fr) {
+        uint32_t skip = 0;  // (wave-uniform) candidates below the cut
+        Sink sk{nullptr, nullptr, nullptr, 0, &seg_ovf};
+        if constexpr (!RASTER) {
+            const int wv = threadIdx.x >> 6;
+            sk = Sink{lds_all[0].resp[wv], lds_all[0].idx[wv], a.hist0 ? lds_all[0].hist : nullptr, 0, &seg_ovf};
+            sk.ehist = sk.hist;  // FAST: histogram counted at emit time (measured faster than at flush)
+            sk.hist = nullptr;
+            sk.cap = kStageFast;
+            if (threadIdx.x == 0) seg_ovf = 0;
+            if (a.hist0) hist_clear(lds_all[0].hist);  // (includes the barrier for the segment table)
+            else __syncthreads();
         } else {
-            if (active) sink_flush(sk, a, f);
-            if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(f) * kHistBins);
+            __syncthreads();
         }
+        if (active) fast_tile<RASTER, MASKED, ALIGNED>(a, off, seg_k, seg_o, seg_inc, fr, ty, tx, sk, cut, skip);
+        if (a.skipped && skip && lane_id() == 0) atomicAdd(&a.skipped[fr], skip);
+        if constexpr (!RASTER) {
+            if (a.segdesc) {
+                seg_flush(sk, a, fr, active, lds_all[0], seg_wtot, seg_base);
+            } else {
+                if (active) sink_flush(sk, a, fr);
+                if (a.hist0) hist_flush(lds_all[0].hist, a.hist0 + static_cast<int64_t>(fr) * kHistBins);
+            }
+        }
+    };
+    if (a.redo_status) {
+        // Redo pass (kFrameRedo), launched with one frame's workgroups: this workgroup's tile of every
+        // flagged frame, one frame after another (the flags of 64 frames per load and ballot; usually none)
+        for (int base = 0; base < a.batch; base += kWave) {
+            const int fr = base + lane_id();
+            uint64_t m = ballot(fr < a.batch && (a.redo_status[min(fr, a.batch - 1)] & kFrameRedo));
+            while (m) {  // (uniform)
+                const int j = __builtin_ctzll(m);
+                m &= m - 1ull;
+                __syncthreads();  // (the previous frame's flush has read the staging)
+                run(base + j);
+            }
+        }
+        return;
     }
+    run(f);
 }
 
 // K3: FAST-12 (feature_point_fast_detector.cpp:11-98). Same tile walk as K1 with a 7-row register
@@ -510,7 +534,8 @@ __global__ __launch_bounds__(256) void k_fast(PointsArgs a, FastOffsets off) {
 //  * response = score + o_k (:88) with o_k from the segment table (one fma).
 template <bool RASTER, bool MASKED, bool ALIGNED>
 __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets &off, const int32_t *seg_k,
-                                          const float *seg_o, const float *seg_inc, int f, int ty, int tx, Sink &sk) {
+                                          const float *seg_o, const float *seg_inc, int f, int ty, int tx, Sink &sk,
+                                          float cut, uint32_t &skip) {
     const int lane = lane_id();
     const int rows = a.rows, cols = a.cols;
     const int c0 = tx * kTileW + 4 * (lane - 1);
@@ -580,6 +605,16 @@ __device__ __forceinline__ void fast_tile(const PointsArgs &a, const FastOffsets
                                            fast_offset(off.nseg, seg_k, seg_o, seg_inc, krow + c0 + m);
                     fl[m] = colv[m] && resp[m] > a.thr;
                 }
+            }
+        }
+        if constexpr (!RASTER) {
+            // emission cut (PointsArgs::emit_cut): candidates below it are counted, not emitted
+            bool em[4];
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                em[m] = fl[m] && resp[m] >= cut;
+                skip += static_cast<uint32_t>(popc64(ballot(fl[m] && !em[m])));
+                fl[m] = em[m];
             }
         }
         const uint64_t b[4] = {ballot(fl[0]), ballot(fl[1]), ballot(fl[2]), ballot(fl[3])};
@@ -849,7 +884,8 @@ hipError_t launch_corner(int kind, bool raster, const PointsArgs &a, hipStream_t
 }
 
 hipError_t launch_fast(bool raster, const PointsArgs &a, const FastOffsets &off, hipStream_t s) {
-    const dim3 grid(blocks_for_waves(a)), block(256);
+    // (the redo pass: one frame's workgroups, each looping over the flagged frames)
+    const dim3 grid(a.redo_status ? a.blocks_per_frame : blocks_for_waves(a)), block(256);
     const bool masked = a.mask != nullptr, aligned = a.aligned4 != 0;
 #define FD_FAST(RS, M)                                                                          \
     do {                                                                                        \

@@ -61,6 +61,8 @@ struct fd_ctx {
     DevBuf ord, ord_meta;  // FD_TIES_REFERENCE host path: host-computed visiting orders of flagged frames
     DevBuf r_x, r_lpos, r_rpos, r_ord, r_ctl, r_wcnt, r_wfr;  // FD_TIES_REFERENCE on the GPU (k_select_reference scratch)
     DevBuf run_lut;        // FAST score per 16-bit ring mask (FastOffsets::run_lut), filled once
+    DevBuf fast_cut;       // FAST emission cut: two float words, read / proposed alternately per call
+    int fast_cut_parity = 0;
     // fd_lsd_lines: compact lists (device), their pinned host copies, frame 0's final state
     // (l_lists: one buffer of three sections, map index | norm | angle, copied back in one transfer)
     DevBuf l_lists, l_fbase;
@@ -379,7 +381,7 @@ int64_t detect_list_cap(int kind, int rows, int cols) {
 }
 
 struct SelectBufs {
-    uint32_t *hist0, *list_count, *pre_count, *seg_bad, *wide_count, *wide_cut;
+    uint32_t *hist0, *list_count, *pre_count, *seg_bad, *wide_count, *wide_cut, *skipped;
     uint64_t *pre_keys, *wide_keys;
     uint32_t *status, *cand_n;
 };
@@ -390,7 +392,7 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     FD_HIP_TRY(c, ensure(c, c->list_idx, sizeof(uint32_t) * cap * batch));
     FD_HIP_TRY(c, ensure(c, c->pre_keys, sizeof(uint64_t) * fdk::kSelectChunk * batch));
     FD_HIP_TRY(c, ensure(c, c->wide_keys, sizeof(uint64_t) * fdk::kWideKeys * batch));
-    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 5);
+    const size_t ctl = sizeof(uint32_t) * static_cast<size_t>(batch) * (fdk::kHistBins + 6);
     if (c->selctl.n < ctl) {
         FD_HIP_TRY(c, ensure(c, c->selctl, ctl));
         c->sel_dirty = true;
@@ -406,6 +408,7 @@ int select_buffers(fd_ctx *c, int batch, int64_t cap, SelectBufs &sb) {
     sb.seg_bad = sb.pre_count + batch;
     sb.wide_count = sb.seg_bad + batch;
     sb.wide_cut = sb.wide_count + batch;
+    sb.skipped = sb.wide_cut + batch;
     sb.pre_keys = as<uint64_t>(c->pre_keys);
     sb.wide_keys = as<uint64_t>(c->wide_keys);
     FD_HIP_TRY(c, ensure(c, c->status, sizeof(uint32_t) * 2 * static_cast<size_t>(batch)));
@@ -449,6 +452,13 @@ struct SelectCall {
     bool push_order = false;  // lists hold the caller's push order (fd_points_select), not raster order
     bool dup_keys = false;    // a pixel may be listed twice with one response (caller lists): equal keys
     bool grid_at_d0 = false;  // distance 0 tests the grid too (1-pixel cells; set with push_order)
+    // FAST emission cut (PointsArgs::emit_cut): the per-pixel launch of this call (re-run for the frames
+    // the selection flags, kFrameRedo), its offsets, the skipped counters and the cut words
+    const fdk::PointsArgs *redo_points = nullptr;
+    const fdk::FastOffsets *redo_off = nullptr;
+    uint32_t *skipped = nullptr;
+    const uint32_t *cut_cur = nullptr;
+    uint32_t *cut_next = nullptr;
     const char *value_msg = "a value above the declared maximum (fd_nn_opts::max_response)";
 };
 
@@ -620,6 +630,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     s.list_cap = q.cap;
     s.rows = rows;
     s.cols = cols;
+    s.batch = batch;
     s.tie_idx_desc = q.tie_idx_desc;
     s.value_flag = q.value_flag ? 1 : 0;
     s.mask = pi.mask;
@@ -680,10 +691,17 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     // top bins and the greedy scan runs over several chunks (1280x720 noise: ~5k), so the wide pass
     // comes with the first chunk; the corner detectors usually finish within it (wide pass deferred).
     s.wide_eager = q.wide_eager ? 1 : 0;
+    if (q.skipped && ab_env("FD_CUT_NO_WIDE")) {  // (A/B: the cut's short lists gathered chunk by chunk instead)
+        s.wide_keys = nullptr;
+        s.wide_eager = 0;
+        s.fast_sub = 1;
+    }
     // ... and its list pass is spread over the frame's list by k_wide_gather, ~16k entries per workgroup
     // at FAST's ~30 % candidate density on noise (one workgroup read the whole list before: 1280x720,
     // ~55k of k_select's ~130k cycles per frame). FD_WIDE_GROUPS=0: off (A/B).
-    if (s.wide_eager && s.wide_keys && !s.pre_keys && !q.value_flag) {
+    // (not under FAST's emission cut: its lists of a few tens of thousands of keys are cheaper to pass once
+    // inside k_select -- 85 us vs 73 + 13 + 5 us for k_select, k_wide_gather and k_wide_cut at configs[2])
+    if (s.wide_eager && s.wide_keys && !s.pre_keys && !q.value_flag && !q.skipped) {
         const int64_t est = static_cast<int64_t>(rows) * cols * 3 / 10;
         s.wide_groups = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, (est + 16383) / 16384)));
         if (const char *e = ab_env("FD_WIDE_GROUPS")) s.wide_groups = std::max(0, std::atoi(e));
@@ -705,7 +723,28 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         FD_HIP_TRY(c, hipMemsetAsync(c->dbg.p, 0, sizeof(uint64_t) * 32 * batch, c->stream));
         s.stamps = as<uint64_t>(c->dbg);
     }
+    s.skipped = q.skipped;
+    s.cut_cur = q.cut_cur;
+    s.cut_next = q.cut_next;
     FD_HIP_TRY(c, fdk::launch_select(s, batch, c->stream));
+    if (q.redo_points) {
+        // the frames whose selection ran out of emitted keys with candidates left below the cut (kFrameRedo):
+        // detected again without the cut and selected again, in stream order; every other workgroup of
+        // these launches exits at once (graph-capturable: no host round trip)
+        fdk::PointsArgs pr = *q.redo_points;
+        pr.emit_cut = nullptr;
+        pr.emit_cut_next = nullptr;
+        pr.skipped = nullptr;
+        pr.redo_status = s.status;
+        FD_HIP_TRY(c, fdk::launch_fast(false, pr, *q.redo_off, c->stream));
+        fdk::SelectArgs s2 = s;
+        s2.skipped = nullptr;
+        s2.cut_cur = nullptr;
+        s2.cut_next = nullptr;
+        s2.redo_status = s.status;
+        s2.stamps = nullptr;
+        FD_HIP_TRY(c, fdk::launch_select(s2, batch, c->stream));
+    }
     c->sel_dirty = false;
     c->status_batch = batch;
     if (stamps) {
@@ -894,7 +933,7 @@ void fd_ctx_destroy(fd_ctx *c) {
                       &c->c_counts, &c->l_norm,   &c->l_angle,     &c->l_valid,      &c->l_cnt,   &c->l_base,
                       &c->l_idx,    &c->l_counts, &c->l_bits, &c->b_uv,     &c->b_counts,    &c->b_bits,       &c->b_valid,
                       &c->n_heat,   &c->n_map,    &c->n_xy,        &c->n_counts,     &c->n_out,
-                      &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut,
+                      &c->segdesc,  &c->seghead,  &c->status,  &c->ord,   &c->ord_meta, &c->run_lut, &c->fast_cut,
                       &c->l_lists,  &c->l_fbase, &c->wide_keys, &c->r_x, &c->r_lpos,
                       &c->r_rpos,   &c->r_ord,    &c->r_ctl,       &c->r_wcnt,      &c->r_wfr,
                       &c->l_sresp,  &c->l_sidx,   &c->l_sst};
@@ -1015,6 +1054,10 @@ int fd_ctx_reserve(fd_ctx *c, int kind, int batch, int rows, int cols, int64_t m
     if (kind == FD_FAST) {
         rc = build_offsets(c, std::max<int64_t>(0, static_cast<int64_t>(rows - 6) * (cols - 6)), c->off_thr);
         if (rc) return rc;
+        if (!c->fast_cut.p) {  // the emission cut's words (fd_points_detect; zero: no cut)
+            FD_HIP_TRY(c, ensure(c, c->fast_cut, 2 * sizeof(uint32_t)));
+            FD_HIP_TRY(c, hipMemsetAsync(c->fast_cut.p, 0, c->fast_cut.n, c->stream));
+        }
         if (max_prior_total > 0) {  // masked FAST: the mask scan's prefix tables
             FD_HIP_TRY(c, ensure(c, c->row_base, sizeof(int32_t) * static_cast<size_t>(batch) * rows));
             FD_HIP_TRY(c, ensure(c, c->word_pref, sizeof(int32_t) * static_cast<size_t>(batch) * rows * ((cols + 31) / 32)));
@@ -1091,6 +1134,14 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     }
     key_map(kind, opts->min_valid_response, kind == FD_FAST && !g.empty ? &c->off : nullptr,
             static_cast<int64_t>(rows - 6) * (cols - 6), a.key_base, a.key_lz);
+    // FAST's emission cut (PointsArgs::emit_cut): only in the raster tie order (the
+    // reference order's emulation needs every candidate in push order). FD_FAST_CUT=0: off (A/B).
+    const bool fast_cut = kind == FD_FAST && !g.empty && c->tie_order == FD_TIES_RASTER &&
+                          !(ab_env("FD_FAST_CUT") && std::atoi(ab_env("FD_FAST_CUT")) == 0);
+    if (fast_cut && !c->fast_cut.p) {  // (zero: no cut, until a selection proposes one)
+        FD_HIP_TRY(c, ensure(c, c->fast_cut, 2 * sizeof(uint32_t)));
+        FD_HIP_TRY(c, hipMemsetAsync(c->fast_cut.p, 0, c->fast_cut.n, c->stream));
+    }
     c->sel_dirty = true;  // until k_select is enqueued: it resets the control block
     if (!g.empty) {
         if (kind == FD_FAST) {
@@ -1102,6 +1153,15 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
                                                          as<int32_t>(c->word_pref), c->stream));
                 a.row_base = as<int32_t>(c->row_base);
                 a.word_pref = as<int32_t>(c->word_pref);
+            }
+            if (fast_cut) {
+                // the emission cut of this call (written by the previous FAST call's selection) and the word
+                // this call's selection proposes the next one in: two words, alternating per call
+                const int p = c->fast_cut_parity;
+                c->fast_cut_parity ^= 1;
+                a.emit_cut = as<uint32_t>(c->fast_cut) + p;
+                a.emit_cut_next = as<uint32_t>(c->fast_cut) + (p ^ 1);
+                a.skipped = sb.skipped;
             }
             FD_HIP_TRY(c, fdk::launch_fast(false, a, c->off, c->stream));
         } else {
@@ -1122,6 +1182,13 @@ int fd_points_detect(fd_ctx *c, int kind, const uint8_t *frames, int frames_on_d
     sc.seghead = a.seghead;
     sc.nseg = g.blocks_per_frame;
     sc.wide_eager = kind == FD_FAST;
+    if (fast_cut) {
+        sc.redo_points = &a;
+        sc.redo_off = &c->off;
+        sc.skipped = sb.skipped;
+        sc.cut_cur = a.emit_cut;
+        sc.cut_next = a.emit_cut_next;
+    }
     return run_select(c, sc, pi, sb, out_xy, out_stride, out_counts, outputs_on_device, frames_on_device);
 }
 

@@ -99,6 +99,17 @@ constexpr int kKnockOut = FD_KO;
 // histogram scan and first cut, 2 the first gather, 3 the first sub-chunk's ordering), so that the
 // differences of the kernel times are the phases' costs without clock stamps.
 constexpr int kExitAt = FD_EXIT;
+// FAST emission cut's margin (SelectArgs::cut_next): the proposal keeps max(FD_CUT_MUL x V, V + FD_CUT_ADD)
+// emitted keys, V = the keys down to the lowest level-0 bin the frame's scan gathered
+#ifndef FD_PICK_U
+#define FD_PICK_U 2  // wide-scratch keys per thread in flight in wide_pick
+#endif
+#ifndef FD_CUT_MUL
+#define FD_CUT_MUL 4
+#endif
+#ifndef FD_CUT_ADD
+#define FD_CUT_ADD 4096
+#endif
 constexpr int kBucketMax = 64;  // largest bin of a sub-chunk ordered by bucket placement (else merge sort)
 // k_select workgroup size (launch_select). Its phases are chains of dependent LDS operations per wave;
 // with 256 threads (4x the items per wave) the headline frame's selection measured 1.3x slower.
@@ -263,7 +274,13 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
             atomicOr(&a.status[f], FD_FRAME_VALUE_RANGE);  // candidate outside the key map
     }
     if (n == 0) {  // RETURN_TRUE_IF(candidates_.empty()) (:55)
-        if (tid == 0) a.out_counts[f] = 0;
+        if (tid == 0) {
+            a.out_counts[f] = 0;
+            if (a.cut_next) {  // (FAST emission cut) candidates below the cut only: select again without it
+                if (a.skipped[f]) atomicOr(&a.status[f], kFrameRedo);
+                atomicMin(a.cut_next, 0u);
+            }
+        }
         return;
     }
     if (kExitAt == 9) return;  // (diagnostic: launch and prologue only)
@@ -510,17 +527,29 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
     auto wide_pick = [&](uint64_t klo, uint64_t khi) {
         if (tid == 0) gcount = 0;
         __syncthreads();
-        for (uint32_t i0 = static_cast<uint32_t>(wave) * kWave; i0 < wide_n; i0 += static_cast<uint32_t>(nthr)) {
-            const uint32_t i = i0 + lane;
-            const uint64_t key = i < wide_n ? wk[i] : 0ull;
-            const bool hit = i < wide_n && key >= klo && key <= khi;
-            const uint64_t m = ballot(hit);
-            if (m) {
-                uint32_t off = 0;
-                if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
-                off = __builtin_amdgcn_readfirstlane(off);
-                const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
-                if (hit && pos < static_cast<uint32_t>(kSelectChunk)) sup[pos] = key;
+        // kPickU keys per thread loaded before any is used: one memory round trip per kPickU x 1024 keys
+        // (all 8 at once spill registers in this instance)
+        constexpr int kPickU = FD_PICK_U;
+        for (uint32_t i0 = static_cast<uint32_t>(wave) * kWave; i0 < wide_n; i0 += static_cast<uint32_t>(kPickU * nthr)) {
+            uint64_t kv[kPickU];
+#pragma unroll
+            for (int u = 0; u < kPickU; ++u) {
+                const uint32_t i = i0 + u * nthr + lane;
+                kv[u] = i < wide_n ? wk[i] : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < kPickU; ++u) {
+                const uint32_t i = i0 + u * nthr + lane;
+                const uint64_t key = kv[u];
+                const bool hit = i < wide_n && key >= klo && key <= khi;
+                const uint64_t m = ballot(hit);
+                if (m) {
+                    uint32_t off = 0;
+                    if (lane == 0) off = atomicAdd(&gcount, static_cast<uint32_t>(popc64(m)));
+                    off = __builtin_amdgcn_readfirstlane(off);
+                    const uint32_t pos = static_cast<uint32_t>(mbcnt64(m, static_cast<int>(off)));
+                    if (hit && pos < static_cast<uint32_t>(kSelectChunk)) sup[pos] = key;
+                }
             }
         }
         __syncthreads();
@@ -797,7 +826,7 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
                     pcell[pos] = (udiv16q(y, s1, rcp_s1) + 1) * static_cast<uint32_t>(gw2) + (udiv16q(x, s1, rcp_s1) + 1);
             };
             // Sub-chunks of <= kSubChunk keys from the top bins of the superchunk (already in LDS):
-            const uint32_t sub_lim = static_cast<uint32_t>((WIDE && a.wide_eager) ? kSubChunkFast : kSubChunk);
+            const uint32_t sub_lim = static_cast<uint32_t>((WIDE && (a.wide_eager || a.fast_sub)) ? kSubChunkFast : kSubChunk);
             // the greedy usually stops within the first few hundred keys.
             int shi = hi;
             while (shi >= lo && !s_done) {
@@ -1177,6 +1206,33 @@ __device__ __forceinline__ void select_frame(const SelectArgs &a, const int f, S
         }
         hi = lo - 1;
     }
+    if (a.cut_next) {
+        // FAST emission cut (PointsArgs::emit_cut). Out of emitted keys before `need` with candidates left
+        // below the cut: the frame runs again without it (redo pass, same call) -- the reference's scan
+        // would continue past the cut. Either way, this frame's proposal for the next call's cut: the
+        // lower edge of the highest level-0 bin with at least max(4 V, V + 4096) emitted keys at or above
+        // it, V = the keys in the bins down to the lowest one the scan gathered (a margin for frames of the
+        // same kind); with fewer emitted keys than that, 1.0 below this call's cut; 0 (no cut) for a frame
+        // that ran out.
+        const bool done = s_done != 0;
+        uint32_t prop = 0u;
+        if (done && L.have_prev_min) {
+            const uint32_t vis = suf0[min(static_cast<int>(L.prev_min >> 20), kHistBins - 1)];
+            const uint32_t target = max(static_cast<uint32_t>(FD_CUT_MUL) * vis, vis + static_cast<uint32_t>(FD_CUT_ADD));
+            const int x0 = first_le(suf0, 0, kHistBins, 0u, target - 1u);  // (all threads: barriers)
+            if (x0 > 0) {
+                const uint32_t fk = a.key_base + ((static_cast<uint32_t>(x0 - 1) << 20) >> a.key_lz);
+                prop = (fk & 0x80000000u) ? (fk & 0x7FFFFFFFu) : 0u;  // the bin's lowest response (a positive float)
+            } else {
+                const float cur = __uint_as_float(*a.cut_cur);
+                prop = cur > 1.0f ? __float_as_uint(cur - 1.0f) : 0u;
+            }
+        }
+        if (tid == 0) {
+            if (!done && a.skipped[f]) atomicOr(&a.status[f], kFrameRedo);
+            atomicMin(a.cut_next, prop);
+        }
+    }
     if (tid == 0) a.out_counts[f] = s_acc;  // (flags, if any, are in a.status[f])
     FD_STAMP(7);
     if (a.stamps && tid == 0)
@@ -1200,6 +1256,7 @@ __device__ __forceinline__ void finish_frame(const SelectArgs &a, const int f) {
         // could be a histogram bin of a later call with another batch size)
         if (a.wide_count) __hip_atomic_store(&a.wide_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.wide_cut) __hip_atomic_store(&a.wide_cut[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.skipped) __hip_atomic_store(&a.skipped[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1361,6 +1418,35 @@ __global__ __launch_bounds__(NT) void k_select(SelectArgs a) {
     finish_frame(a, f);
 }
 
+// The redo pass (kFrameRedo; FAST's emission cut), a few workgroups: workgroup w owns frames w, w + G, ...
+// (a static assignment: select_frame clears a frame's status word, which no other workgroup reads), their
+// flags one load per lane, broadcast; usually none is set. Its own kernel: a loop around select_frame in
+// k_select itself cost that kernel ~30 more spilled registers.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_select_redo(SelectArgs a) {
+    __shared__ SelectLds L;
+    __shared__ uint64_t mine;
+    const int G = static_cast<int>(gridDim.x), w = static_cast<int>(blockIdx.x);
+    for (int base = 0; base < a.batch; base += kWave * G) {
+        if (threadIdx.x < kWave) {
+            const int fr = base + G * static_cast<int>(threadIdx.x) + w;
+            const uint64_t b = ballot(fr < a.batch && (a.redo_status[min(fr, a.batch - 1)] & kFrameRedo));
+            if (threadIdx.x == 0) mine = b;
+        }
+        __syncthreads();
+        uint64_t m = mine;
+        __syncthreads();  // (mine is rewritten by the next round)
+        while (m) {
+            const int f = base + G * __builtin_ctzll(m) + w;
+            m &= m - 1ull;
+            select_frame<NT, true>(a, f, L);
+            if (threadIdx.x == 0) atomicOr(&a.status[f], FD_FRAME_REDETECTED);
+            finish_frame(a, f);
+            __syncthreads();  // (LDS reused by the next frame)
+        }
+    }
+}
+
 // Greedy selection in a given order (FD_TIES_REFERENCE): the frame's candidates as raster indices in
 // the order the reference's std::sort leaves them (computed on the host for frames k_select flagged),
 // visited chunk by chunk with the same greedy as k_select (SelectGoodFeatures :62-72): decode, prior
@@ -1455,6 +1541,12 @@ hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
+    if (a.redo_status) {  // (redo pass: a few workgroups loop over the flagged frames, no wide-pass kernels)
+        hipLaunchKernelGGL(k_select_redo<kSelectThreads>, dim3(static_cast<unsigned>(std::min(batch, 8))),
+                           dim3(kSelectThreads), 0, s, a);
+        return hipGetLastError();
+    }
+    const unsigned sel_grid = static_cast<unsigned>(batch);
     if (a.wide_count && a.wide_keys && a.wide_groups > 0) {
         hipLaunchKernelGGL(k_wide_cut, dim3(static_cast<unsigned>(batch)), dim3(256), 0, s, a);
         hipLaunchKernelGGL(k_wide_gather, dim3(static_cast<unsigned>(batch * a.wide_groups)), dim3(kWideThreads), 0, s, a);
@@ -1463,10 +1555,10 @@ hipError_t launch_select(const SelectArgs &a, int batch, hipStream_t s) {
     }
     // the wide pass (k_select<.., true>) for FAST and for list mode; the corner detectors' small frames
     // (sorted segments) keep the leaner instance
-    if (a.wide_keys && (a.wide_eager || !a.segdesc))
-        hipLaunchKernelGGL((k_select<kSelectThreads, true>), dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
+    if ((a.wide_keys && (a.wide_eager || !a.segdesc)) || a.fast_sub)
+        hipLaunchKernelGGL((k_select<kSelectThreads, true>), dim3(sel_grid), dim3(kSelectThreads), 0, s, a);
     else
-        hipLaunchKernelGGL((k_select<kSelectThreads, false>), dim3(static_cast<unsigned>(batch)), dim3(kSelectThreads), 0, s, a);
+        hipLaunchKernelGGL((k_select<kSelectThreads, false>), dim3(sel_grid), dim3(kSelectThreads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@ KINDS = {"harris": FD_HARRIS, "shi_tomasi": FD_SHI_TOMASI, "fast": FD_FAST}
 # order of equal responses in the selection (include/fd_hip.h fd_ctx_set_tie_order)
 TIES = {"raster": 0, "reference": 1}
 FRAME_TIES, FRAME_RESOLVED, FRAME_UNRESOLVED, FRAME_VALUE_RANGE, FRAME_GUARD = 0x1, 0x2, 0x4, 0x40000000, 0xBE000000
+FRAME_REDETECTED = 0x8  # FAST, raster order: selected a second time without the adaptive emission cut
 
 _ctx_lock = threading.Lock()
 _contexts: dict[int, "Context"] = {}

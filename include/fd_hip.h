@@ -96,6 +96,8 @@ int fd_ctx_set_tie_order(fd_ctx *ctx, int order);
 #define FD_FRAME_TIES 0x00000001u       /* equal responses met in the greedy scan (order defined by the mode) */
 #define FD_FRAME_RESOLVED 0x00000002u   /* re-selected in the reference's std::sort order (FD_TIES_REFERENCE) */
 #define FD_FRAME_UNRESOLVED 0x00000004u /* FD_TIES_REFERENCE: the GPU emulation stopped (see fd_tie_order) */
+#define FD_FRAME_REDETECTED 0x00000008u /* FAST, FD_TIES_RASTER: detected and selected a second time in the same call,
+                                           without the adaptive emission cut (it was too high for this frame) */
 #define FD_FRAME_VALUE_RANGE 0x40000000u /* fd_nn_select: a heatmap value above fd_nn_opts::max_response */
 #define FD_FRAME_GUARD 0xBE000000u      /* internal consistency guard tripped (host-output calls fail FD_ERR_HIP) */
 int fd_ctx_frame_status(fd_ctx *ctx, uint32_t *dst, int batch, int async);

@@ -3,6 +3,11 @@ import os
 import sys
 
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+for kv in sys.argv[1:]:  # VAR=VALUE settings for the library (A/B switches), before it is loaded
+    k, v = kv.split("=", 1)
+    os.environ[k] = v
+os.environ.setdefault("FD_DEBUG_AB", "1")
+os.environ.setdefault("FD_SELECT_STAMPS", "1")
 import torch  # noqa: E402
 
 import feature_detector_amd as fd  # noqa: E402
