@@ -607,13 +607,15 @@ def copy_bandwidth(torch, dev, nbytes=1 << 30, reps=5):
     so = os.path.join(ROOT, "tools", "calib", "libcopybw.so")
     if os.path.exists(so):
         lib = ctypes.CDLL(so)
-        lib.fdcal_copy16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        for name, key in (("fdcal_copy16", "kernel_copy_nt_gbs"), ("fdcal_copy16_flat", "kernel_copy_gbs")):
+            fn = getattr(lib, name)
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
 
-        def kcopy():
-            rc = lib.fdcal_copy16(b.data_ptr(), a.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
-            assert rc == 0, rc
+            def kcopy(fn=fn):
+                rc = fn(b.data_ptr(), a.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
+                assert rc == 0, rc
 
-        out["kernel_copy_gbs"] = round(2 * nbytes / (graph_time_ms(torch, kcopy, reps) * 1e-3) / 1e9, 1)
+            out[key] = round(2 * nbytes / (graph_time_ms(torch, kcopy, reps) * 1e-3) / 1e9, 1)
     del a, b
     out["device_copy_gbs"] = max(out.values())
     return out

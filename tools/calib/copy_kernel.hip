@@ -26,7 +26,20 @@ __global__ __launch_bounds__(256) void k_copy16(const u32x4 *__restrict__ src, u
     for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
+// the plain form: one 16-byte element per thread, default cache policy, one workgroup per 4 KiB
+__global__ __launch_bounds__(256) void k_copy16_flat(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, size_t n16) {
+    const size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+}
+
 }  // namespace
+
+extern "C" int fdcal_copy16_flat(void *dst, const void *src, size_t bytes, void *stream) {
+    const size_t n16 = bytes / 16;
+    hipLaunchKernelGGL(k_copy16_flat, dim3(static_cast<unsigned>((n16 + 255) / 256)), dim3(256), 0,
+                       static_cast<hipStream_t>(stream), static_cast<const u32x4 *>(src), static_cast<u32x4 *>(dst), n16);
+    return static_cast<int>(hipGetLastError());
+}
 
 // bytes: a multiple of 16; src / dst 16-byte aligned device memory. Enqueued on `stream`.
 extern "C" int fdcal_copy16(void *dst, const void *src, size_t bytes, void *stream) {
