@@ -1,0 +1,41 @@
+"""K10 (fd_nn_conv3x3_c64) alone at one SuperPoint layer's shape (64 frames of 640x480 input), for
+rocprofv3 kernel-trace / PMC passes and quick timing: random fp16 channels-last input and filter, `--calls`
+calls after one warm-up call; prints the event-timed average per call and the layer's MFMA floor.
+usage: python3 tools/sp_k10_probe.py [--layer conv1b|conv2a|conv2b|conv3a] [--calls N]"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+import feature_detector_amd as fd  # noqa: E402
+from feature_detector_amd import superpoint as sp  # noqa: E402
+
+LAYERS = {"conv1b": (480, 640, 64, True), "conv2a": (240, 320, 64, False), "conv2b": (240, 320, 64, True),
+          "conv3a": (120, 160, 128, False)}
+ap = argparse.ArgumentParser()
+ap.add_argument("--layer", default="conv1b", choices=sorted(LAYERS))
+ap.add_argument("--calls", type=int, default=5)
+ap.add_argument("--frames", type=int, default=64)
+a = ap.parse_args()
+h, w, co, pool = LAYERS[a.layer]
+fd.load()
+g = torch.Generator(device="cuda")
+g.manual_seed(7)
+x = (torch.rand((a.frames, 64, h, w), generator=g, device="cuda") * 2).half().contiguous(memory_format=torch.channels_last)
+wt = (torch.randn((co, 64, 3, 3), generator=g, device="cuda") * 0.05).half()
+b = (torch.randn((co,), generator=g, device="cuda") * 0.1).half()
+packed = [sp.pack_conv3x3_weight(wt[k:k + 64]) for k in range(0, co, 64)]
+out = sp.conv64_bias_relu(x, wt, b, pool=pool, packed=packed)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(a.calls):
+    sp.conv64_bias_relu(x, wt, b, pool=pool, out=out, packed=packed)
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / a.calls
+flop = 2.0 * a.frames * h * w * co * 64 * 9
+print(f"{a.layer}: {ms * 1e3:.1f} us per call, {flop / ms / 1e9:.1f} TFLOP/s "
+      f"(MFMA floor at 2.4 GHz {flop / 2.5e15 * 1e6:.0f} us)", flush=True)
