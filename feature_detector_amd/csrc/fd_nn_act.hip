@@ -513,6 +513,215 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
     }
 }
 
+// K10, two tiles in flight per CU (the default for fd_nn_conv3x3_c64; the kernel above stays for the fused
+// conv1a path and as the A/B baseline, FD_C64_PP=0). With one wave per SIMD the tile's staging and epilogue
+// ran between its matrix phases and the matrix cores idled half the time (rocprofv3 at conv1b:
+// SQ_VALU_MFMA_BUSY_CYCLES 49.5 % of the kernel's cycles, gpurun_out k10 r06). Here a workgroup of 8 waves
+// holds the packed filter once (72 KiB) and two 8 x 32-pixel input tiles (43 KiB each): waves 0-3 and 4-7
+// are two groups, and in each phase (one barrier per phase) one group runs the K loop of its tile while the
+// other, on the same SIMDs, writes its previous tile's outputs, stages its next tile into LDS from
+// registers and issues the loads of the tile after -- vector-memory and VALU work beside the partner's
+// matrix instructions. A wave computes 16 columns x 4 rows x 64 channels (16 accumulators) with the
+// operands swapped relative to the kernel above (D = W x P: a lane holds 4 consecutive channels of one
+// pixel), so the epilogue stores from registers: v_permlane16_swap pairs the lanes of adjacent channel
+// quads into 16-byte runs of 8 channels (whole 2 KiB per 16 pixels per row, no LDS staging), and the 2x2
+// pool takes its column partner by DPP. Persistent grid, one workgroup per CU, tiles dealt so that the 32
+// workgroups of an XCD work on neighbouring tiles (their halo rows and columns come from that XCD's L2).
+// Same arithmetic as the kernel above: fp16 products summed in f32, the sum rounded to half, the bias
+// added in half (= the float add rounded), ReLU, pool = max of the four biased sums then the ReLU.
+#ifndef FD_C64_PP
+#define FD_C64_PP 1
+#endif
+constexpr int kPpRows = 8, kPpCols = 32, kPpInRows = kPpRows + 2, kPpInCols = kPpCols + 2;
+constexpr int kPpInChunks = kPpInRows * kPpInCols * 8;  // 16-byte chunks of a group's input tile
+constexpr int kPpPer = (kPpInChunks + 255) / 256;       // per thread of a group
+
+template <bool POOL>
+__global__ __launch_bounds__(512) void k_conv3x3_c64_pp(const u4 *x, const u4 *wpk, const _Float16 *bias, u4 *y,
+                                                        int n, int h, int w, int ystride, int yoff) {
+    __shared__ u4 Wl[9 * 64 * 8];
+    __shared__ u4 In[2][kPpInChunks];
+    const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
+    const int grp = wv >> 2, cb = wv & 1, rh = (wv >> 1) & 1, gtid = tid & 255;
+    for (int i = tid; i < 9 * 64 * 8; i += 512) {
+        const int ch = i & 7, row = i >> 3, co = row & 63;
+        Wl[row * 8 + (ch ^ (co & 7))] = wpk[i];
+    }
+    // the lane's channels of block nb: nb * 16 + 4 (lane >> 4) + 0..3, as two bias pairs
+    const int g4 = lane >> 4, px = lane & 15;
+    h2v bz[4][2];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+        const int c = nb * 16 + 4 * g4;
+        bz[nb][0] = h2v{bias[c], bias[c + 1]};
+        bz[nb][1] = h2v{bias[c + 2], bias[c + 3]};
+    }
+    const int th = (h + kPpRows - 1) / kPpRows, tw = (w + kPpCols - 1) / kPpCols;
+    const int total = n * th * tw;  // (< 2^31: checked on the host)
+    const int G = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
+    const int L = G == 256 ? (b & 7) * 32 + (b >> 3) : b;  // (blocks b, b + 8, ... share an XCD)
+    const int K = L < total ? (total - L + G - 1) / G : 0;  // this workgroup's tiles: k G + L, k < K
+    u4 *const in = In[grp];
+    u4 pre[kPpPer];
+    auto fetch = [&](int k) {
+        const int tile = k * G + L;
+        const int tx = tile % tw, t2 = tile / tw, ty = t2 % th, f = t2 / th;
+        const int r0 = ty * kPpRows, c0 = tx * kPpCols;
+        // a buffer resource over the tile's frame: out-of-frame chunks read past it and get zeros
+        const auto rs = make_rsrc(x + static_cast<int64_t>(f) * h * w * 8, static_cast<uint32_t>(h * w * 128));
+#pragma unroll
+        for (int k2 = 0; k2 < kPpPer; ++k2) {
+            const int i = gtid + k2 * 256;
+            const int ch = i & 7, p = i >> 3, pr = p / kPpInCols, pc = p - pr * kPpInCols;
+            const int gy = r0 - 1 + pr, gx = c0 - 1 + pc;
+            const bool ok = i < kPpInChunks && gy >= 0 && gy < h && gx >= 0 && gx < w;
+            const int32_t off = ok ? ((gy * w + gx) * 8 + ch) * 16 : -1;
+            pre[k2] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        }
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (int k2 = 0; k2 < kPpPer; ++k2) {
+            const int i = gtid + k2 * 256;
+            const int p = i >> 3, pc = p % kPpInCols;
+            if (i < kPpInChunks) in[p * 8 + ((i & 7) ^ (pc & 7))] = pre[k2];
+        }
+    };
+    f4 acc[4][4];
+    // the K loop of one tile: groups (column shift dx, channel half) of the 6 input rows the wave's 4 rows
+    // reach, each used by the three row taps; the next group's rows and the next tap's filter fragments
+    // are read ahead of the current matrix instructions
+    auto kloop = [&]() {
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) acc[m][nb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        auto rows_at = [&](int g, h8 (&A)[6]) {
+            const int dx = g >> 1, kh = g & 1;
+            const int chunk = kh * 4 + g4;
+            const int pc = cb * 16 + px + dx;
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+                A[r] = __builtin_bit_cast(h8, in[((rh * 4 + r) * kPpInCols + pc) * 8 + (chunk ^ (pc & 7))]);
+        };
+        auto filt_at = [&](int g, int dy, h8 (&B)[4]) {
+            const int dx = g >> 1, kh = g & 1, tap = dy * 3 + dx;
+            const int chunk = kh * 4 + g4;
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                const int co = nb * 16 + px;
+                B[nb] = __builtin_bit_cast(h8, Wl[(tap * 64 + co) * 8 + (chunk ^ (co & 7))]);
+            }
+        };
+        h8 Ar[2][6], Bf[2][4];
+        rows_at(0, Ar[0]);
+        filt_at(0, 0, Bf[0]);
+#pragma unroll
+        for (int g = 0; g < 6; ++g) {
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+                const int it = g * 3 + dy;
+                if (dy == 0 && g + 1 < 6) rows_at(g + 1, Ar[(g + 1) & 1]);
+                if (it + 1 < 18) filt_at(dy == 2 ? g + 1 : g, dy == 2 ? 0 : dy + 1, Bf[(it + 1) & 1]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int nb = 0; nb < 4; ++nb)
+                        acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Bf[it & 1][nb], Ar[g & 1][m + dy], acc[m][nb], 0, 0, 0);
+            }
+        }
+    };
+    // a lane's 4 channels of block nb (row m) rounded, biased and ReLU'd, as two dwords
+    auto quad = [&](int m, int nb, uint32_t &lo, uint32_t &hi) {
+        lo = __builtin_bit_cast(uint32_t, cv_relu2(cv_pair(acc[m][nb][0], acc[m][nb][1], bz[nb][0])));
+        hi = __builtin_bit_cast(uint32_t, cv_relu2(cv_pair(acc[m][nb][2], acc[m][nb][3], bz[nb][1])));
+    };
+    // channel blocks (2 pr, 2 pr + 1) of rows a lane holds as 4 dwords -> 8 consecutive channels: after the
+    // swap, lane row g4 holds block 2 pr + (g4 & 1), channels 8 (g4 >> 1) .. + 7 (chunk 2 (2 pr + (g4 & 1)) + (g4 >> 1))
+    auto pair_swap = [&](uint32_t (&v)[4]) {  // v = {lo(nb0), hi(nb0), lo(nb1), hi(nb1)} -> one 16-byte run
+        typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+        const u2v s0 = __builtin_bit_cast(u2v, __builtin_amdgcn_permlane16_swap(v[0], v[2], false, false));
+        const u2v s1 = __builtin_bit_cast(u2v, __builtin_amdgcn_permlane16_swap(v[1], v[3], false, false));
+        v[0] = s0[0], v[2] = s0[1], v[1] = s1[0], v[3] = s1[1];
+    };
+    auto epilogue = [&](int k) {
+        const int tile = k * G + L;
+        const int tx = tile % tw, t2 = tile / tw, ty = t2 % th, f = t2 / th;
+        const int r0 = ty * kPpRows + rh * 4, c0 = tx * kPpCols + cb * 16;
+        if constexpr (POOL) {
+            const int ho = h >> 1, wo = w >> 1;
+            const int gx = (c0 + px) >> 1;
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+                const int gy = (r0 >> 1) + pr;
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp) {
+                    uint32_t v[4];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int nb = 2 * pp + j;
+#pragma unroll
+                        for (int hf = 0; hf < 2; ++hf) {
+                            // max of the two rows' biased sums, then of the column pair (lane ^ 1), then the ReLU
+                            h2v m2 = __builtin_elementwise_max(cv_pair(acc[2 * pr][nb][2 * hf], acc[2 * pr][nb][2 * hf + 1], bz[nb][hf]),
+                                                               cv_pair(acc[2 * pr + 1][nb][2 * hf], acc[2 * pr + 1][nb][2 * hf + 1], bz[nb][hf]));
+                            const uint32_t mu = __builtin_bit_cast(uint32_t, m2);
+                            const uint32_t nbr = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+                                static_cast<int>(mu), static_cast<int>(mu), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+                            m2 = __builtin_elementwise_max(m2, __builtin_bit_cast(h2v, nbr));
+                            v[2 * j + hf] = __builtin_bit_cast(uint32_t, cv_relu2(m2));
+                        }
+                    }
+                    pair_swap(v);
+                    const int chunk = 2 * (2 * pp + (g4 & 1)) + (g4 >> 1);
+                    if (!(px & 1) && gy < ho && gx < wo)
+                        nn_store(&y[((static_cast<int64_t>(f) * ho + gy) * wo + gx) * ystride + yoff + chunk],
+                                 u4{v[0], v[1], v[2], v[3]});
+                }
+            }
+        } else {
+            const int gx = c0 + px;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int gy = r0 + m;
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp) {
+                    uint32_t v[4];
+                    quad(m, 2 * pp, v[0], v[1]);
+                    quad(m, 2 * pp + 1, v[2], v[3]);
+                    pair_swap(v);
+                    const int chunk = 2 * (2 * pp + (g4 & 1)) + (g4 >> 1);
+                    if (gy < h && gx < w)
+                        nn_store(&y[((static_cast<int64_t>(f) * h + gy) * w + gx) * ystride + yoff + chunk], u4{v[0], v[1], v[2], v[3]});
+                }
+            }
+        }
+    };
+    // prologue: group 0 stages tile 0 and holds tile 2 in registers, group 1 holds tile 1
+    if (grp == 0) {
+        if (K > 0) {
+            fetch(0);
+            stage();
+        }
+        if (K > 2) fetch(2);
+    } else if (K > 1) {
+        fetch(1);
+    }
+    __syncthreads();
+    // phase p: group p & 1 computes tile p; the other group writes tile p - 1, stages tile p + 1 and loads
+    // tile p + 3 (all its own tiles: k = grp mod 2). Every wave runs the K + 1 phases (one barrier each).
+    for (int p = 0; p <= K; ++p) {
+        if ((p & 1) == grp) {
+            if (p < K) kloop();
+        } else {
+            if (p >= 1) epilogue(p - 1);
+            if (p + 1 < K) stage();
+            if (p + 3 < K) fetch(p + 3);
+        }
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
@@ -525,6 +734,17 @@ hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, 
     const _Float16 *bv = static_cast<const _Float16 *>(bias), *w1h = static_cast<const _Float16 *>(w1),
                    *b1h = static_cast<const _Float16 *>(b1);
     u4 *yv = static_cast<u4 *>(y);
+#if FD_C64_PP
+    if (!w1) {  // two tiles in flight per CU, a persistent grid of one workgroup per CU
+        const int64_t pt = static_cast<int64_t>(n) * ((h + kPpRows - 1) / kPpRows) * ((w + kPpCols - 1) / kPpCols);
+        const unsigned pg = static_cast<unsigned>(std::min<int64_t>(pt, 256));
+        if (pool)
+            hipLaunchKernelGGL(k_conv3x3_c64_pp<true>, dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff);
+        else
+            hipLaunchKernelGGL(k_conv3x3_c64_pp<false>, dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff);
+        return hipGetLastError();
+    }
+#endif
     if (w1) {  // conv1a fused into the staging (fd_nn_conv3x3_c1c64)
         if (pool)
             hipLaunchKernelGGL((k_conv3x3_c64_mfma<true, true>), dim3(grid), dim3(256), 0, s, xv, wv, bv, yv, n, h, w, ystride,
