@@ -616,8 +616,27 @@ def copy_bandwidth(torch, dev, nbytes=1 << 30, reps=5):
                 assert rc == 0, rc
 
             out[key] = round(2 * nbytes / (graph_time_ms(torch, kcopy, reps) * 1e-3) / 1e9, 1)
+        # write-only, and the LSD map's traffic shape: 1 B read + 9 B written per pixel (its bytes without its
+        # arithmetic), each as a nontemporal grid-stride kernel and a flat default-policy one
+        npx = nbytes // 10 // 64 * 64
+        nrm = b[:4 * npx]
+        ang = a[:4 * npx]  # (the copy source is free now)
+        src, val = a[4 * npx:5 * npx], a[5 * npx:6 * npx]
+        for name, key in (("fdcal_fill16", "kernel_fill_nt_gbs"), ("fdcal_fill16_flat", "kernel_fill_gbs")):
+            fill = getattr(lib, name)
+            fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+            out[key] = round(nbytes / (graph_time_ms(
+                torch, lambda fill=fill: fill(b.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream), reps)
+                * 1e-3) / 1e9, 1)
+        for name, key in (("fdcal_lsd_shape", "lsd_shape_nt_gbs"), ("fdcal_lsd_shape_flat", "lsd_shape_flat_gbs")):
+            shape = getattr(lib, name)
+            shape.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_size_t, ctypes.c_void_p]
+            out[key] = round(10 * npx / (graph_time_ms(
+                torch, lambda shape=shape: shape(src.data_ptr(), nrm.data_ptr(), ang.data_ptr(), val.data_ptr(), npx,
+                                                 torch.cuda.current_stream().cuda_stream), reps) * 1e-3) / 1e9, 1)
+        out["lsd_shape_gbs"] = max(out["lsd_shape_nt_gbs"], out["lsd_shape_flat_gbs"])
     del a, b
-    out["device_copy_gbs"] = max(out.values())
+    out["device_copy_gbs"] = max(v for k, v in out.items() if "copy" in k)
     return out
 
 
@@ -1042,6 +1061,10 @@ def main():
         cb = copy_bandwidth(torch, dev)
         out["device_copy_gbs"] = cb.pop("device_copy_gbs")
         out["device_copy"] = cb
+        lsd = out.get("config4_lsd_map")
+        if lsd and cb.get("lsd_shape_gbs"):  # the map against a kernel that moves the same bytes and nothing else
+            lsd["roofline"]["shape_ceiling_gbs"] = cb["lsd_shape_gbs"]
+            lsd["roofline"]["frac_of_shape_ceiling"] = round(lsd["roofline"]["achieved"] / cb["lsd_shape_gbs"], 4)
     if world == 1:
         with phase(torch, "end_to_end"):
             out["end_to_end_host_frames"] = run_end_to_end(torch, fd, args)

@@ -532,15 +532,28 @@ __global__ __launch_bounds__(256) void k_conv3x3_c64_mfma(const u4 *x, const u4 
 #ifndef FD_C64_PP
 #define FD_C64_PP 1
 #endif
+#ifndef FD_C64_PRIO
+#define FD_C64_PRIO 0
+#endif
 constexpr int kPpRows = 8, kPpCols = 32, kPpInRows = kPpRows + 2, kPpInCols = kPpCols + 2;
 constexpr int kPpInChunks = kPpInRows * kPpInCols * 8;  // 16-byte chunks of a group's input tile
 constexpr int kPpPer = (kPpInChunks + 255) / 256;       // per thread of a group
 
-template <bool POOL>
+// FUSED (fd_nn_conv3x3_c1c64: SuperPoint conv1a + conv1b): the group's input tile is conv1a itself,
+// computed in the housekeeping phase on the matrix cores (D[16 channels][16 pixels] = W1[16][K = the 9 taps
+// padded to 32] x P[K][16]: 4 matrix instructions per 16 pixels of an input row, at most 36 per wave and
+// tile beside the partner's 288) from the one-channel frame: a wave owns input rows q, q + 4, q + 8 of the
+// tile, loads the 3 x 36 frame pixels each needs two phases ahead (two 2-byte loads per lane and row),
+// and builds the patch fragments from a per-wave LDS copy of them; the sum rounded to half, the bias
+// added in half, the ReLU, zero outside the frame (conv1b's padding).
+// x is then the [n][h][w] fp16 frame, w1 [64][9], b1 [64]; the 64-channel activation never goes to HBM.
+template <bool POOL, bool FUSED>
 __global__ __launch_bounds__(512) void k_conv3x3_c64_pp(const u4 *x, const u4 *wpk, const _Float16 *bias, u4 *y,
-                                                        int n, int h, int w, int ystride, int yoff) {
+                                                        int n, int h, int w, int ystride, int yoff,
+                                                        const _Float16 *w1 = nullptr, const _Float16 *b1 = nullptr) {
     __shared__ u4 Wl[9 * 64 * 8];
     __shared__ u4 In[2][kPpInChunks];
+    __shared__ uint16_t Raw[FUSED ? 4 : 1][3 * (kPpInCols + 2)];  // FUSED: a housekeeping wave's frame rows
     const int tid = static_cast<int>(threadIdx.x), lane = tid & 63, wv = tid >> 6;
     const int grp = wv >> 2, cb = wv & 1, rh = (wv >> 1) & 1, gtid = tid & 255;
     for (int i = tid; i < 9 * 64 * 8; i += 512) {
@@ -562,11 +575,47 @@ __global__ __launch_bounds__(512) void k_conv3x3_c64_pp(const u4 *x, const u4 *w
     const int L = G == 256 ? (b & 7) * 32 + (b >> 3) : b;  // (blocks b, b + 8, ... share an XCD)
     const int K = L < total ? (total - L + G - 1) / G : 0;  // this workgroup's tiles: k G + L, k < K
     u4 *const in = In[grp];
-    u4 pre[kPpPer];
+    u4 pre[FUSED ? 1 : kPpPer];
+    // FUSED: conv1a's weights as the lane's A fragments (channels 16 cb + (lane & 15), taps 8 (lane >> 4) ..),
+    // its bias pairs for the lane's D channels 16 cb + 4 (lane >> 4) .., and the lane's patch fragments of
+    // the wave's pixel blocks (blocks q, q + 4, ... of the tile's 10 x 34 input pixels)
+    constexpr int kRawC = kPpInCols + 2, kRawN = 3 * kRawC;  // an input row's frame patch rows: 3 x 36
+    constexpr int kWRows = (kPpInRows + 3) / 4;                // input rows per wave (3)
+    h8 w1a[FUSED ? 4 : 1];
+    uint32_t rawv[FUSED ? kWRows : 1][2];
+    h2v b1p[FUSED ? 4 : 1][2];
+    const int q4 = wv & 3;
+    if constexpr (FUSED) {
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+            const int c = c4 * 16 + px;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w1a[c4][e] = 8 * g4 + e < 9 ? w1[c * 9 + 8 * g4 + e] : static_cast<_Float16>(0.0f);
+            const int cd = c4 * 16 + 4 * g4;
+            b1p[c4][0] = h2v{b1[cd], b1[cd + 1]};
+            b1p[c4][1] = h2v{b1[cd + 2], b1[cd + 3]};
+        }
+    }
     auto fetch = [&](int k) {
         const int tile = k * G + L;
         const int tx = tile % tw, t2 = tile / tw, ty = t2 % th, f = t2 / th;
         const int r0 = ty * kPpRows, c0 = tx * kPpCols;
+        if constexpr (FUSED) {
+            // the frame pixels of the wave's input rows' patches (zero outside the frame)
+            const uint16_t *xf = reinterpret_cast<const uint16_t *>(x) + static_cast<int64_t>(f) * h * w;
+#pragma unroll
+            for (int j = 0; j < kWRows; ++j) {
+                const int pr = q4 + 4 * j;
+#pragma unroll
+                for (int e2 = 0; e2 < 2; ++e2) {
+                    const int e = lane + 64 * e2, dyr = e / kRawC, cc = e - dyr * kRawC;
+                    const int yy = r0 - 2 + pr + dyr, xx = c0 - 2 + cc;
+                    rawv[j][e2] = (pr < kPpInRows && e < kRawN && yy >= 0 && yy < h && xx >= 0 && xx < w)
+                                      ? static_cast<uint32_t>(xf[static_cast<int64_t>(yy) * w + xx]) : 0u;
+                }
+            }
+            return;
+        }
         // a buffer resource over the tile's frame: out-of-frame chunks read past it and get zeros
         const auto rs = make_rsrc(x + static_cast<int64_t>(f) * h * w * 8, static_cast<uint32_t>(h * w * 128));
 #pragma unroll
@@ -579,7 +628,56 @@ __global__ __launch_bounds__(512) void k_conv3x3_c64_pp(const u4 *x, const u4 *w
             pre[k2] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         }
     };
-    auto stage = [&]() {
+    auto stage = [&](int k) {
+        if constexpr (FUSED) {
+            // conv1a of the wave's input rows: the row's patch rows into the wave's LDS copy, then per 16
+            // pixels the lane's patch fragment (taps 8 (lane >> 4) ..), one matrix step per 16 channels, and
+            // the lane's 4 channels of its pixel as 8 bytes into the pixel's (swizzled) 16-byte chunk
+            const int tile = k * G + L;
+            const int tx = tile % tw, t2 = tile / tw, ty = t2 % th;
+            const int r0 = ty * kPpRows, c0 = tx * kPpCols;
+            uint16_t *const raw = Raw[q4];
+#pragma unroll
+            for (int j = 0; j < kWRows; ++j) {
+                const int pr = q4 + 4 * j;
+                if (pr >= kPpInRows) break;  // (wave-uniform)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();  // (the previous row's fragments are read)
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int e2 = 0; e2 < 2; ++e2)
+                    if (lane + 64 * e2 < kRawN) raw[lane + 64 * e2] = static_cast<uint16_t>(rawv[j][e2]);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int gy = r0 - 1 + pr;
+#pragma unroll
+                for (int bk = 0; bk < (kPpInCols + 15) / 16; ++bk) {
+                    const int pc = min(bk * 16 + px, kPpInCols - 1);
+                    uint32_t t[4] = {0u, 0u, 0u, 0u};
+                    if (g4 == 0) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) t[e >> 1] |= static_cast<uint32_t>(raw[(e / 3) * kRawC + pc + e % 3]) << (16 * (e & 1));
+                    } else if (g4 == 1) {
+                        t[0] = raw[2 * kRawC + pc + 2];
+                    }
+                    const h8 pfr = __builtin_bit_cast(h8, u4{t[0], t[1], t[2], t[3]});
+                    const int gx = c0 - 1 + pc;
+                    const bool inframe = gy >= 0 && gy < h && gx >= 0 && gx < w;
+                    const int pi = pr * kPpInCols + pc;
+#pragma unroll
+                    for (int c4 = 0; c4 < 4; ++c4) {
+                        const f4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1a[c4], pfr, f4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+                        const h2v lo = cv_relu2(cv_pair(d[0], d[1], b1p[c4][0])), hi = cv_relu2(cv_pair(d[2], d[3], b1p[c4][1]));
+                        const int ch = c4 * 16 + 4 * g4;  // the lane's first channel: chunk ch / 8, half (ch & 4) / 4
+                        uint2 v = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+                        if (!inframe) v = make_uint2(0u, 0u);
+                        if (bk * 16 + px < kPpInCols) reinterpret_cast<uint2 *>(in)[(pi * 8 + ((ch >> 3) ^ (pc & 7))) * 2 + ((ch >> 2) & 1)] = v;
+                    }
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int k2 = 0; k2 < kPpPer; ++k2) {
             const int i = gtid + k2 * 256;
@@ -701,7 +799,7 @@ __global__ __launch_bounds__(512) void k_conv3x3_c64_pp(const u4 *x, const u4 *w
     if (grp == 0) {
         if (K > 0) {
             fetch(0);
-            stage();
+            stage(0);
         }
         if (K > 2) fetch(2);
     } else if (K > 1) {
@@ -712,10 +810,16 @@ __global__ __launch_bounds__(512) void k_conv3x3_c64_pp(const u4 *x, const u4 *w
     // tile p + 3 (all its own tiles: k = grp mod 2). Every wave runs the K + 1 phases (one barrier each).
     for (int p = 0; p <= K; ++p) {
         if ((p & 1) == grp) {
+#if FD_C64_PRIO
+            __builtin_amdgcn_s_setprio(1);  // the matrix phase wins issue arbitration over the partner's
             if (p < K) kloop();
+            __builtin_amdgcn_s_setprio(0);
+#else
+            if (p < K) kloop();
+#endif
         } else {
             if (p >= 1) epilogue(p - 1);
-            if (p + 1 < K) stage();
+            if (p + 1 < K) stage(p + 1);
             if (p + 3 < K) fetch(p + 3);
         }
         __syncthreads();
@@ -735,13 +839,18 @@ hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, 
                    *b1h = static_cast<const _Float16 *>(b1);
     u4 *yv = static_cast<u4 *>(y);
 #if FD_C64_PP
-    if (!w1) {  // two tiles in flight per CU, a persistent grid of one workgroup per CU
+    {  // two tiles in flight per CU, a persistent grid of one workgroup per CU (w1: conv1a fused)
         const int64_t pt = static_cast<int64_t>(n) * ((h + kPpRows - 1) / kPpRows) * ((w + kPpCols - 1) / kPpCols);
         const unsigned pg = static_cast<unsigned>(std::min<int64_t>(pt, 256));
-        if (pool)
-            hipLaunchKernelGGL(k_conv3x3_c64_pp<true>, dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff);
+        const _Float16 *w1h = static_cast<const _Float16 *>(w1), *b1h = static_cast<const _Float16 *>(b1);
+        if (w1 && pool)
+            hipLaunchKernelGGL((k_conv3x3_c64_pp<true, true>), dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff, w1h, b1h);
+        else if (w1)
+            hipLaunchKernelGGL((k_conv3x3_c64_pp<false, true>), dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff, w1h, b1h);
+        else if (pool)
+            hipLaunchKernelGGL((k_conv3x3_c64_pp<true, false>), dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff, nullptr, nullptr);
         else
-            hipLaunchKernelGGL(k_conv3x3_c64_pp<false>, dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff);
+            hipLaunchKernelGGL((k_conv3x3_c64_pp<false, false>), dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff, nullptr, nullptr);
         return hipGetLastError();
     }
 #endif

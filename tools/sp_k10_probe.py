@@ -18,12 +18,15 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--layer", default="conv1b", choices=sorted(LAYERS))
 ap.add_argument("--calls", type=int, default=5)
 ap.add_argument("--frames", type=int, default=64)
+ap.add_argument("--zero", action="store_true", help="all-zero input (the matrix cores' power draw on zeros vs random)")
 a = ap.parse_args()
 h, w, co, pool = LAYERS[a.layer]
 fd.load()
 g = torch.Generator(device="cuda")
 g.manual_seed(7)
 x = (torch.rand((a.frames, 64, h, w), generator=g, device="cuda") * 2).half().contiguous(memory_format=torch.channels_last)
+if a.zero:
+    x.zero_()
 wt = (torch.randn((co, 64, 3, 3), generator=g, device="cuda") * 0.05).half()
 b = (torch.randn((co,), generator=g, device="cuda") * 0.1).half()
 packed = [sp.pack_conv3x3_weight(wt[k:k + 64]) for k in range(0, co, 64)]
@@ -37,5 +40,5 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / a.calls
 flop = 2.0 * a.frames * h * w * co * 64 * 9
-print(f"{a.layer}: {ms * 1e3:.1f} us per call, {flop / ms / 1e9:.1f} TFLOP/s "
+print(f"{a.layer}{' (zero input)' if a.zero else ''}: {ms * 1e3:.1f} us per call, {flop / ms / 1e9:.1f} TFLOP/s "
       f"(MFMA floor at 2.4 GHz {flop / 2.5e15 * 1e6:.0f} us)", flush=True)
