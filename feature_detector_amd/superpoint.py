@@ -539,8 +539,10 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
             write-bound pass, then conv1b on the matrix cores). The fused pass (conv1ab_bias_relu: conv1a
             recomputed inside conv1b's tiles on the matrix cores, the full-resolution activation never
             written) measured equal to the layered pass -- 4.75-4.78 vs 4.68-4.79 ms per 64-frame forward
-            (profiles/r05_sp_ab.txt: conv1a's write pass saved, conv1b's tile phase longer by as much) --
-            so it runs only under the FD_SP_C1C64 A/B switch."""
+            (profiles/r05_sp_ab.txt: conv1a's write pass saved, conv1b's tile phase longer by as much), and
+            slower again once conv1b kept two tiles in flight per CU (round 6, profiles/r06_sp_fused_ab.txt:
+            4.19-4.38 vs 4.09-4.13 ms; conv1a's matrix work takes the partner's pipe) -- so it runs only
+            under the FD_SP_C1C64 A/B switch."""
             if x.dtype == torch.float16 and x.is_cuda and x.dim() == 4 and x.shape[1] == 1 \
                     and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.shape[3] <= 4096 \
                     and self.conv1a.out_channels == 64 and self.conv1b.in_channels == 64 \
