@@ -113,6 +113,9 @@ struct SelectArgs {
     float *out_xy;
     int out_stride;
     int32_t *out_counts;  // plain feature counts (no flag bits)
+    // host-output calls in the raster tie order: out_xy / out_counts are pinned host memory and the final
+    // status words are mirrored here by finish_frame, so no copy follows the kernel (nullptr: none)
+    uint32_t *status_host;
     // [batch] per-frame status (fd_hip.h FD_FRAME_*: tie in the scanned prefix, guard flags) and
     // [batch] candidate count of the frame (kept for a tie resolution after the list count is reset)
     uint32_t *status;

@@ -659,6 +659,11 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
     const size_t res_head = (sizeof(uint32_t) * 3 * static_cast<size_t>(batch) + 15) & ~size_t(15);
     const size_t res_bytes = res_head + sizeof(float) * 2 * static_cast<size_t>(out_stride) * batch;
     SelectBufs sbl = sb;
+    // In the raster tie order nothing after k_select changes the outputs: the kernel writes the features
+    // and counts straight into the pinned result buffer and mirrors the status words there (no copy after
+    // the kernel: ~6 us per 640x480 host frame). The reference order's pass rewrites them: copied as before.
+    static const bool no_direct = ab_env("FD_HOST_DIRECT") && std::atoi(ab_env("FD_HOST_DIRECT")) == 0;  // (A/B)
+    const bool direct = !outputs_on_device && c->tie_order != FD_TIES_REFERENCE && !no_direct;
     if (!outputs_on_device) {
         if (c->status.n < res_bytes) {  // (grow: the selection's status words move with it)
             FD_HIP_TRY(c, ensure(c, c->status, res_bytes));
@@ -666,9 +671,11 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
             sbl.cand_n = sbl.status + batch;
         }
         FD_HIP_TRY(c, ensure_host(c->h_res, res_bytes));
-        dcnt = reinterpret_cast<int32_t *>(as<uint32_t>(c->status) + 2 * static_cast<size_t>(batch));
-        dxy = reinterpret_cast<float *>(static_cast<uint8_t *>(c->status.p) + res_head);
+        uint8_t *const res = static_cast<uint8_t *>(direct ? c->h_res.p : c->status.p);
+        dcnt = reinterpret_cast<int32_t *>(res + sizeof(uint32_t) * 2 * static_cast<size_t>(batch));
+        dxy = reinterpret_cast<float *>(res + res_head);
     }
+    s.status_host = direct ? static_cast<uint32_t *>(c->h_res.p) : nullptr;
     s.out_xy = dxy;
     s.out_stride = out_stride;
     s.out_counts = dcnt;
@@ -842,7 +849,7 @@ int run_select(fd_ctx *c, const SelectCall &q, const PriorInfo &pi, const Select
         }
     }
     if (!outputs_on_device) {
-        FD_HIP_TRY(c, hipMemcpyAsync(c->h_res.p, c->status.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
+        if (!direct) FD_HIP_TRY(c, hipMemcpyAsync(c->h_res.p, c->status.p, res_bytes, hipMemcpyDeviceToHost, c->stream));
         FD_HIP_TRY(c, hipStreamSynchronize(c->stream));
         const uint32_t *st = static_cast<const uint32_t *>(c->h_res.p);
         std::memcpy(out_counts, st + 2 * static_cast<size_t>(batch), sizeof(int32_t) * batch);

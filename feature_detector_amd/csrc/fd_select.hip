@@ -1257,6 +1257,9 @@ __device__ __forceinline__ void finish_frame(const SelectArgs &a, const int f) {
         if (a.wide_count) __hip_atomic_store(&a.wide_count[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.wide_cut) __hip_atomic_store(&a.wide_cut[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (a.skipped) __hip_atomic_store(&a.skipped[f], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the frame's final status to the host (the stream's synchronisation makes it visible; a redo
+        // pass's finish_frame writes it again)
+        if (a.status_host) a.status_host[f] = __hip_atomic_load(&a.status[f], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
