@@ -197,7 +197,7 @@ __device__ __forceinline__ h2v cv_relu2(h2v v) {
     u &= ~(sgn | (sgn - (sgn >> 15)));
     return __builtin_bit_cast(h2v, u);
 }
-__device__ __forceinline__ _Float16 cv_relu1(_Float16 v) {
+[[maybe_unused]] __device__ __forceinline__ _Float16 cv_relu1(_Float16 v) {  // (the round-5 kernel's pool)
     v = __builtin_elementwise_max(v, static_cast<_Float16>(0.0f));
     const uint16_t u = __builtin_bit_cast(uint16_t, v);
     return __builtin_bit_cast(_Float16, static_cast<uint16_t>((u & 0x8000u) ? 0u : u));
@@ -831,9 +831,6 @@ __global__ __launch_bounds__(512) void k_conv3x3_c64_pp(const u4 *x, const u4 *w
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
                               int y_channels, int y_offset, hipStream_t s, const void *w1, const void *b1) {
     const int ystride = y_channels / 8, yoff = y_offset / 8;
-    const int64_t tiles = static_cast<int64_t>(n) * ((h + kCvRows - 1) / kCvRows) * ((w + kCvCols - 1) / kCvCols);
-    if (tiles == 0) return hipSuccess;
-    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(tiles, 1024));
     const u4 *xv = static_cast<const u4 *>(x), *wv = static_cast<const u4 *>(wpk);
     const _Float16 *bv = static_cast<const _Float16 *>(bias), *w1h = static_cast<const _Float16 *>(w1),
                    *b1h = static_cast<const _Float16 *>(b1);
@@ -841,8 +838,8 @@ hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, 
 #if FD_C64_PP
     {  // two tiles in flight per CU, a persistent grid of one workgroup per CU (w1: conv1a fused)
         const int64_t pt = static_cast<int64_t>(n) * ((h + kPpRows - 1) / kPpRows) * ((w + kPpCols - 1) / kPpCols);
+        if (pt == 0) return hipSuccess;
         const unsigned pg = static_cast<unsigned>(std::min<int64_t>(pt, 256));
-        const _Float16 *w1h = static_cast<const _Float16 *>(w1), *b1h = static_cast<const _Float16 *>(b1);
         if (w1 && pool)
             hipLaunchKernelGGL((k_conv3x3_c64_pp<true, true>), dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff, w1h, b1h);
         else if (w1)
@@ -853,7 +850,11 @@ hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, 
             hipLaunchKernelGGL((k_conv3x3_c64_pp<false, false>), dim3(pg), dim3(512), 0, s, xv, wv, bv, yv, n, h, w, ystride, yoff, nullptr, nullptr);
         return hipGetLastError();
     }
-#endif
+#else
+    // (the round-5 kernel: A/B builds with -DFD_C64_PP=0 only)
+    const int64_t tiles = static_cast<int64_t>(n) * ((h + kCvRows - 1) / kCvRows) * ((w + kCvCols - 1) / kCvCols);
+    if (tiles == 0) return hipSuccess;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(tiles, 1024));
     if (w1) {  // conv1a fused into the staging (fd_nn_conv3x3_c1c64)
         if (pool)
             hipLaunchKernelGGL((k_conv3x3_c64_mfma<true, true>), dim3(grid), dim3(256), 0, s, xv, wv, bv, yv, n, h, w, ystride,
@@ -869,6 +870,7 @@ hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, 
                            yoff, nullptr, nullptr);
     }
     return hipGetLastError();
+#endif
 }
 
 hipError_t launch_conv3x3_c1_bias_relu(const void *x, const void *wt, const void *bias, void *y, int n, int h, int w,
