@@ -11,7 +11,7 @@ CSRC = os.path.join(HERE, "csrc")
 
 FD_OK, FD_ERR_INVALID, FD_ERR_HIP, FD_ERR_CAPACITY = 0, 1, 2, 3
 FD_HARRIS, FD_SHI_TOMASI, FD_FAST = 0, 1, 2
-ABI_VERSION = 5  # include/fd_hip.h FD_ABI_VERSION this binding's signatures follow
+ABI_VERSION = 6  # include/fd_hip.h FD_ABI_VERSION this binding's signatures follow
 
 # Every symbol include/fd_hip.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = (
@@ -20,7 +20,7 @@ EXPORTS = (
     "fd_ctx_synchronize", "fd_ctx_reserve", "fd_ctx_stage", "fd_ctx_set_tie_order", "fd_ctx_frame_status", "fd_points_detect", "fd_points_candidates", "fd_points_response",
     "fd_points_response_append", "fd_points_select",
     "fd_lsd_map", "fd_lsd_map_pitched", "fd_lsd_lines", "fd_lsd_lines_state", "fd_brief_compute", "fd_nn_select", "fd_nn_select_list", "fd_nn_descriptors",
-    "fd_nn_bias_relu", "fd_nn_conv3x3_c1", "fd_nn_conv3x3_c64", "fd_nn_conv3x3_c1c64",
+    "fd_nn_bias_relu", "fd_nn_conv3x3_c1", "fd_nn_conv3x3_c64",
     "fd_nn_heat_softmax", "fd_nn_desc_normalize",
     "fd_build_info", "fd_abi_version", "fd_png_info", "fd_png_decode", "fd_png_frames",
     "fd_ingest_create", "fd_ingest_destroy", "fd_ingest_frames", "fd_ingest_submit", "fd_ingest_wait",
@@ -112,7 +112,6 @@ def load() -> ctypes.CDLL:
         "fd_nn_heat_softmax": (i32, [P, P, P, P, i32, i32, i32]),
         "fd_nn_desc_normalize": (i32, [P, P, P, P, i64, i32]),
         "fd_nn_conv3x3_c64": (i32, [P, P, P, P, P, i32, i32, i32, i32, i32, i32]),
-        "fd_nn_conv3x3_c1c64": (i32, [P, P, P, P, P, P, P, i32, i32, i32, i32]),
         "fd_build_info": (ctypes.c_char_p, []),
         "fd_abi_version": (i32, []),
         "fd_png_info": (i32, [P, ctypes.c_size_t, P, P, P]),

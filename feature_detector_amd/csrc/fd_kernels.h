@@ -354,8 +354,7 @@ hipError_t launch_nn_heat_softmax(const void *semi, const void *bias, float *hea
 hipError_t launch_nn_desc_normalize(const void *x, const void *bias, float *y, int64_t cells, int c, hipStream_t s);
 // (w1, b1 non-null: x is the one-channel frame and conv1a -- 1 -> 64, 3x3, bias, ReLU -- is fused in)
 hipError_t launch_conv3x3_c64(const void *x, const void *wpk, const void *bias, void *y, int n, int h, int w, int pool,
-                              int y_channels, int y_offset, hipStream_t s, const void *w1 = nullptr,
-                              const void *b1 = nullptr);
+                              int y_channels, int y_offset, hipStream_t s);
 hipError_t launch_conv3x3_c1_bias_relu(const void *x, const void *wt, const void *bias, void *y, int n, int h, int w,
                                        int c, hipStream_t s);
 hipError_t launch_bias_relu(const void *x, const void *bias, void *y, int n, int h, int w, int c, int pool,

@@ -2199,24 +2199,6 @@ int fd_nn_conv3x3_c64(fd_ctx *c, const void *x, const void *weight_packed, const
     return FD_OK;
 }
 
-int fd_nn_conv3x3_c1c64(fd_ctx *c, const void *x, const void *weight1, const void *bias1, const void *weight_packed,
-                        const void *bias, void *y, int n, int h, int w, int pool) {
-    if (!c) return FD_ERR_INVALID;
-    if (!x || !weight1 || !bias1 || !weight_packed || !bias || !y) return fail(c, FD_ERR_INVALID, "bad arguments");
-    if (n < 0 || h < 0 || w < 0) return fail(c, FD_ERR_INVALID, "need n, h, w >= 0");
-    if (w > 4096) return fail(c, FD_ERR_INVALID, "w must be <= 4096");
-    if (pool && ((h | w) & 1)) return fail(c, FD_ERR_INVALID, "pooling needs even h and w");
-    if (static_cast<int64_t>(n) * ((h + 1) / 2) * ((w + 63) / 64) >= (int64_t(1) << 31))
-        return fail(c, FD_ERR_INVALID, "too many tiles");
-    if ((reinterpret_cast<uintptr_t>(weight_packed) | reinterpret_cast<uintptr_t>(y)) & 15 ||
-        (reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(weight1) | reinterpret_cast<uintptr_t>(bias1) |
-         reinterpret_cast<uintptr_t>(bias)) & 1)
-        return fail(c, FD_ERR_INVALID, "weight_packed, y must be 16-byte aligned, x / weight1 / biases 2-byte aligned");
-    FD_HIP_TRY(c, hipSetDevice(c->device));
-    FD_HIP_TRY(c, fdk::launch_conv3x3_c64(x, weight_packed, bias, y, n, h, w, pool, 64, 0, c->stream, weight1, bias1));
-    return FD_OK;
-}
-
 int fd_nn_descriptors(fd_ctx *c, const float *map, int map_on_device, int map_layout, int batch, int channels,
                       int map_rows, int map_cols, const float *xy, const int32_t *counts, int32_t stride, float *out,
                       int io_on_device) {

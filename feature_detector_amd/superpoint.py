@@ -343,47 +343,6 @@ def conv64_bias_relu(x, weight, bias, pool: bool = False, out=None, ctx: Context
     return out
 
 
-def conv1ab_bias_relu(x, weight1, bias1, weight, bias, pool: bool = True, out=None, ctx: Context | None = None,
-                      packed=None):
-    """fd_nn_conv3x3_c1c64: the encoder's first two layers in one pass -- conv1a (1 -> 64, 3x3, bias, ReLU)
-    recomputed inside conv1b's tiles (64 -> 64, 3x3, bias, ReLU, and the 2x2 max pool when pool), so the
-    full-resolution 64-channel activation never goes to memory. x [N, 1, H, W] fp16 on the device ->
-    [N, 64, H(/2), W(/2)] fp16 channels-last; equal to conv64_bias_relu(conv1_bias_relu(x)) within fp16
-    rounding (conv1a runs on the matrix cores here, in a different summation order than conv1_bias_relu's
-    FMA chain, so a conv1a value may round to the neighbouring half)."""
-    import torch
-
-    if not (x.is_cuda and x.dtype == torch.float16 and x.dim() == 4 and x.shape[1] == 1
-            and (x.is_contiguous() or x.is_contiguous(memory_format=torch.channels_last))):
-        raise ValueError("conv1ab_bias_relu: x must be a [N, 1, H, W] float16 device tensor")
-    n, _, h, w = x.shape
-    if tuple(weight1.shape) != (64, 1, 3, 3) or bias1.numel() != 64 or tuple(weight.shape) != (64, 64, 3, 3) \
-            or bias.numel() != 64:
-        raise ValueError("conv1ab_bias_relu: weight1 [64, 1, 3, 3], weight [64, 64, 3, 3], 64-value biases")
-    if pool and (h % 2 or w % 2):
-        raise ValueError("conv1ab_bias_relu: pooling needs even H and W")
-    shape = (n, 64, h // 2, w // 2) if pool else (n, 64, h, w)
-    if out is None:
-        out = torch.empty(shape, dtype=torch.float16, device=x.device, memory_format=torch.channels_last)
-    elif not (out.dtype == torch.float16 and tuple(out.shape) == shape and out.device == x.device
-              and out.is_contiguous(memory_format=torch.channels_last)):
-        raise ValueError(f"conv1ab_bias_relu: out must be a channels-last float16 {list(shape)} tensor on {x.device}")
-    if packed is None:
-        packed = pack_conv3x3_weight(weight.to(device=x.device, dtype=torch.float16))
-    w1 = weight1.detach().to(device=x.device, dtype=torch.float16).contiguous()
-    b1 = bias1.detach().to(device=x.device, dtype=torch.float16).contiguous()
-    b = bias.detach().to(device=x.device, dtype=torch.float16).contiguous()
-    xc = x.contiguous()
-    ctx = _resolve_ctx(ctx, x)
-    _bind_stream(ctx, True)
-    rc = _lib.load().fd_nn_conv3x3_c1c64(ctx.ptr, ctypes.c_void_p(xc.data_ptr()), ctypes.c_void_p(w1.data_ptr()),
-                                          ctypes.c_void_p(b1.data_ptr()), ctypes.c_void_p(packed.data_ptr()),
-                                          ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(out.data_ptr()), n, h, w,
-                                          1 if pool else 0)
-    _lib.check(ctx.ptr, rc)
-    return out
-
-
 def nn_descriptors(desc_map, xy, counts=None, out=None, ctx: Context | None = None):
     """fd_nn_descriptors: desc_map [B, C, h, w] float32, xy [B, S, 2] -> descriptors [B, S, C].
 
@@ -536,26 +495,10 @@ def build_net(seed: int = 0, head_gain: float = 100.0, nms: bool = False, top_k:
 
         def first_layers(self, x):
             """conv1a -> ReLU -> conv1b -> ReLU -> MaxPool2d(2, 2), layer by layer through cbr (conv1a's
-            write-bound pass, then conv1b on the matrix cores). The fused pass (conv1ab_bias_relu: conv1a
-            recomputed inside conv1b's tiles on the matrix cores, the full-resolution activation never
-            written) measured equal to the layered pass -- 4.75-4.78 vs 4.68-4.79 ms per 64-frame forward
-            (profiles/r05_sp_ab.txt: conv1a's write pass saved, conv1b's tile phase longer by as much), and
-            slower again once conv1b kept two tiles in flight per CU (round 6, profiles/r06_sp_fused_ab.txt:
-            4.19-4.38 vs 4.09-4.13 ms; conv1a's matrix work takes the partner's pipe) -- so it runs only
-            under the FD_SP_C1C64 A/B switch."""
-            if x.dtype == torch.float16 and x.is_cuda and x.dim() == 4 and x.shape[1] == 1 \
-                    and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0 and x.shape[3] <= 4096 \
-                    and self.conv1a.out_channels == 64 and self.conv1b.in_channels == 64 \
-                    and self.conv1b.out_channels == 64 and not _ab_env("FD_SP_UNFUSED") \
-                    and _ab_env("FD_SP_C1C64"):  # (A/B switches)
-                tag = (self.conv1b.weight.data_ptr(), self.conv1b.weight._version, x.device)
-                cache = self.__dict__.setdefault("_fd_packed", {})
-                hit = cache.get(id(self.conv1b))
-                if hit is None or hit[0] != tag or len(hit[1]) != 1:
-                    hit = (tag, [pack_conv3x3_weight(self.conv1b.weight.to(device=x.device, dtype=torch.float16))])
-                    cache[id(self.conv1b)] = hit
-                return conv1ab_bias_relu(x, self.conv1a.weight, self.conv1a.bias, self.conv1b.weight,
-                                         self.conv1b.bias, pool=True, packed=hit[1][0])
+            write-bound pass, then conv1b on the matrix cores). conv1a recomputed inside conv1b's tiles (the
+            full-resolution activation never written) measured slower in both K10 forms -- 4.75-4.78 vs
+            4.68-4.79 ms per 64-frame forward in round 5, 4.19-4.38 vs 4.09-4.13 ms once conv1b kept two tiles
+            in flight per CU (profiles/r05_sp_ab.txt, r06_sp_fused_ab.txt) -- and was removed."""
             return self.cbr(self.conv1b, self.cbr(self.conv1a, x), pool=True)
 
         def forward(self, x):

@@ -395,18 +395,6 @@ int fd_nn_conv3x3_c64(fd_ctx *ctx, const void *x, const void *weight_packed, con
                       int w, int pool, int y_channels, int y_offset);
 
 /*
- * fd_nn_conv3x3_c1c64 -- SuperPoint's first two layers in one pass: conv1a (1 -> 64 channels, 3x3, bias,
- * ReLU) fused into conv1b (64 -> 64, 3x3, bias, ReLU, with pool = 1 the 2x2 max pool): x [n][h][w] fp16,
- * weight1 [64][1][3][3] fp16, bias1 [64], weight_packed / bias as fd_nn_conv3x3_c64, y [n][h(/2)][w(/2)][64]
- * channels-last fp16, all on the device. Equal to fd_nn_conv3x3_c1 followed by fd_nn_conv3x3_c64 within
- * fp16 rounding: conv1a is recomputed per conv1b tile on the matrix cores, whose summation order differs
- * from fd_nn_conv3x3_c1's FMA chain, so a conv1a value may round to the neighbouring half (its
- * full-resolution 64-channel output never goes to memory). w <= 4096; x 2-byte, y and weight_packed 16-byte aligned; pool needs even h, w.
- */
-int fd_nn_conv3x3_c1c64(fd_ctx *ctx, const void *x, const void *weight1, const void *bias1, const void *weight_packed,
-                        const void *bias, void *y, int n, int h, int w, int pool);
-
-/*
  * fd_nn_heat_softmax -- SuperPoint's detector-head output (the network's last stage after convPb:
  * softmax over a cell's 65 channels, the dustbin channel dropped, pixel_shuffle by 8): semi
  * [n][hc][wc][65] channels-last fp16 logits -> heat [n][8 hc][8 wc] float, heat[8i + r][8j + c] =
@@ -428,11 +416,12 @@ int fd_nn_desc_normalize(fd_ctx *ctx, const void *x, const void *bias, float *y,
 const char *fd_build_info(void);
 
 /*
- * ABI version of this header: bumped whenever an entry point's parameter list changes (5: int64_t
- * bias_len in fd_nn_bias_relu). Bindings compare fd_abi_version() with the FD_ABI_VERSION they were
+ * ABI version of this header: bumped whenever an entry point's parameter list changes or one is removed
+ * (5: int64_t bias_len in fd_nn_bias_relu; 6: fd_nn_conv3x3_c1c64 removed -- the fused first layers
+ * measured slower than fd_nn_conv3x3_c1 + fd_nn_conv3x3_c64). Bindings compare fd_abi_version() with the FD_ABI_VERSION they were
  * written for and refuse a mismatched library, instead of passing misread arguments.
  */
-#define FD_ABI_VERSION 5
+#define FD_ABI_VERSION 6
 int fd_abi_version(void);
 
 /* ---- ingest: pinned, pipelined host frames -> features ------------------------ */

@@ -330,45 +330,6 @@ def test_conv64_bias_relu_matches_torch(sp):
 
 
 @pytest.mark.gpu
-def test_conv1ab_fused_matches_layers(sp):
-    """fd_nn_conv3x3_c1c64 (SuperPoint conv1a fused into conv1b's tile staging, on the matrix cores: the
-    64-channel full-resolution activation never goes to memory) against the two layer kernels in sequence
-    -- conv64_bias_relu(conv1_bias_relu(x)), pooled and not -- and PyTorch's float32
-    relu(conv1b(relu(conv1a(x)))), both within the fp16 roundings (the fused conv1a sums its 9 products
-    on the matrix cores, the layer kernel in an FMA chain: a sum may round to the neighbouring half);
-    ragged tiles (sizes off the tile) and a 640x480 batch."""
-    import torch
-
-    g = torch.Generator(device="cuda")
-    g.manual_seed(21)
-    for n, h, w in ((1, 8, 64), (2, 6, 130), (3, 10, 18), (2, 480, 640), (1, 2, 2)):
-        x = torch.rand((n, 1, h, w), generator=g, device="cuda").half()
-        w1 = (torch.randn((64, 1, 3, 3), generator=g, device="cuda") * 0.5).half()
-        b1 = (torch.randn(64, generator=g, device="cuda") * 0.1).half()
-        w2 = (torch.randn((64, 64, 3, 3), generator=g, device="cuda") * 0.06).half()
-        b2 = (torch.randn(64, generator=g, device="cuda") * 0.2).half()
-        a = sp.conv1_bias_relu(x, w1, b1)
-        conv1 = torch.relu(torch.nn.functional.conv2d(x.float(), w1.float(), b1.float(), 1, 1))
-        conv2 = torch.nn.functional.conv2d(conv1, w2.float(), None, 1, 1)
-        # bound: conv1a's two roundings (2^-10 relative) carried through conv1b's weights, then conv1b's own
-        # two roundings of the sum (2^-10 relative)
-        carried = torch.nn.functional.conv2d(conv1.abs(), w2.float().abs(), None, 1, 1) * 2.0 ** -10
-        tol_full = carried + (conv2.abs() + 1.0) * 2.0 ** -10 + 2.0 ** -14
-        for pool in (True, False):
-            ref = sp.conv64_bias_relu(a, w2, b2, pool=pool)
-            got = sp.conv1ab_bias_relu(x, w1, b1, w2, b2, pool=pool)
-            assert got.is_contiguous(memory_format=torch.channels_last)
-            tol = torch.nn.functional.max_pool2d(tol_full, 2, 2) if pool else tol_full
-            assert bool(((got.float() - ref.float()).abs() <= 2 * tol).all()), (n, h, w, pool)
-        f32 = torch.nn.functional.max_pool2d(torch.relu(conv2 + b2.float().view(1, -1, 1, 1)), 2, 2)
-        tol = torch.nn.functional.max_pool2d(tol_full, 2, 2)
-        err = (sp.conv1ab_bias_relu(x, w1, b1, w2, b2).float() - f32).abs()
-        assert bool((err <= tol).all()), (n, h, w, err.max().item())
-    with pytest.raises(ValueError):
-        sp.conv1ab_bias_relu(torch.zeros((1, 1, 5, 8), device="cuda", dtype=torch.float16), w1, b1, w2, b2)  # odd H
-
-
-@pytest.mark.gpu
 def test_bias_relu_matches_torch(sp):
     """fd_nn_bias_relu (bias + ReLU, and + 2x2 max pool, on channels-last fp16) equals PyTorch's separate
     half-precision ops bit for bit. The fused SuperPoint forward runs the convolutions without their bias,

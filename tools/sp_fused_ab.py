@@ -3,7 +3,7 @@ bias + ReLU (+ pool) kernel (fd_nn_bias_relu) and the one-pass first layer (fd_n
 the fused path with the matrix-core convolution for 64 -> 64 layers only (FD_SP_C64_ONLY64=1: conv3a,
 64 -> 128, on the library), without the matrix-core convolutions (FD_SP_NO_C64=1), without both
 (FD_SP_NO_CONV1=1 FD_SP_NO_C64=1: round-3's path) and PyTorch's separate elementwise passes
-(FD_SP_UNFUSED=1), and the conv1a+conv1b fusion (FD_SP_C1C64=1, off by default: slower), interleaved
+(FD_SP_UNFUSED=1), interleaved
 in one process; prints ms per 64-frame forward. (Sets FD_DEBUG_AB=1: the switches are read only then.)"""
 import os
 import sys
@@ -36,13 +36,11 @@ def timed(reps=10):
     return e0.elapsed_time(e1) / reps
 
 
-MODES = os.environ.get("FD_AB_MODES", "fused,c1c64,c64_only64,no_c64,no_conv1,unfused").split(",")  # (subset: A/B of builds)
+MODES = os.environ.get("FD_AB_MODES", "fused,c64_only64,no_c64,no_conv1,unfused").split(",")  # (subset: A/B of builds)
 for rnd in range(2):
     for mode in MODES:
-        for k in ("FD_SP_UNFUSED", "FD_SP_NO_CONV1", "FD_SP_NO_C64", "FD_SP_C64_ONLY64", "FD_SP_C1C64"):
+        for k in ("FD_SP_UNFUSED", "FD_SP_NO_CONV1", "FD_SP_NO_C64", "FD_SP_C64_ONLY64"):
             os.environ.pop(k, None)
-        if mode == "c1c64":
-            os.environ["FD_SP_C1C64"] = "1"
         if mode == "c64_only64":
             os.environ["FD_SP_C64_ONLY64"] = "1"
         if mode == "unfused":
