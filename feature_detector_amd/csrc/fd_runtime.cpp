@@ -2187,7 +2187,7 @@ int fd_nn_conv3x3_c64(fd_ctx *c, const void *x, const void *weight_packed, const
     if (pool && ((h | w) & 1)) return fail(c, FD_ERR_INVALID, "pooling needs even h and w");
     if (y_channels < 64 || y_channels % 64 || y_offset < 0 || y_offset % 64 || y_offset + 64 > y_channels)
         return fail(c, FD_ERR_INVALID, "y_channels must be a multiple of 64 holding [y_offset, y_offset + 64)");
-    if (static_cast<int64_t>(n) * ((h + 1) / 2) * ((w + 63) / 64) >= (int64_t(1) << 31))
+    if (static_cast<int64_t>(n) * ((h + 7) / 8) * ((w + 31) / 32) >= (int64_t(1) << 31))  // (K10's 8 x 32 tiles)
         return fail(c, FD_ERR_INVALID, "too many tiles");
     if (static_cast<int64_t>(h) * w * 128 >= (int64_t(1) << 31))  // (one frame's input: 32-bit buffer offsets)
         return fail(c, FD_ERR_INVALID, "frame too large (h * w * 64 channels * 2 B must be < 2^31)");
