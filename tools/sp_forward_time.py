@@ -1,4 +1,4 @@
-"""The SuperPoint forward on 64 640x480 frames (BASELINE configs[4] shape), event-timed: prints ms per
+"""The SuperPoint forward on SP_BATCH (default 64) 640x480 frames (BASELINE configs[4] shape), event-timed: prints ms per
 64-frame forward for two rounds of 10 calls (the library from FD_LIB_PATH when set)."""
 import os
 import sys
@@ -14,7 +14,8 @@ det = sp.NNFeaturePointDetector(sp.Options(kMaxImageRows=480, kMaxImageCols=640)
 det.Initialize()
 g = torch.Generator(device="cuda")
 g.manual_seed(1)
-frames = torch.randint(0, 256, (64, 480, 640), generator=g, device="cuda", dtype=torch.int32).to(torch.uint8)
+NB = int(os.environ.get("SP_BATCH", "64"))  # frames per network batch
+frames = torch.randint(0, 256, (NB, 480, 640), generator=g, device="cuda", dtype=torch.int32).to(torch.uint8)
 for _ in range(3):
     det.InferenceSession(frames)
 torch.cuda.synchronize()
@@ -26,4 +27,5 @@ for rnd in range(2):
         det.InferenceSession(frames)
     e1.record()
     torch.cuda.synchronize()
-    print(f"{tag} round {rnd}: {e0.elapsed_time(e1) / 10:.3f} ms per 64-frame forward", flush=True)
+    ms = e0.elapsed_time(e1) / 10
+    print(f"{tag} round {rnd}: {ms:.3f} ms per {NB}-frame forward ({ms * 64 / NB:.3f} ms per 64 frames)", flush=True)
