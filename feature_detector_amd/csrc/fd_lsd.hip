@@ -372,44 +372,38 @@ __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
     else lsd_map_tile<ALIGNED, false>(a, f, strip, chunk, Q);
 }
 
-// Pass 2: per-frame exclusive scan of the counts in column-major order (col outer, chunk inner).
+// Pass 2: per column the total of its chunk counts, and their exclusive scan in column order (the
+// column-major list order) into col_base's chunk-0 row: all the scatter reads, since a column's entries
+// are one contiguous run, chunk after chunk. One workgroup per frame; each thread sums one column's chunk
+// counts (loads coalesced across the threads). (Scanning every (column, chunk) entry in column-major
+// order, gathered across the chunk rows, took 37 us at 1080p x256; this 15 us.)
 __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
-    constexpr int kPer = 4;  // consecutive scan entries per thread and round
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry;
     const int f = blockIdx.x;
     const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
-    const int mc = a.cols - 1;
-    const int64_t n = static_cast<int64_t>(mc) * a.chunks;
+    const int cols = a.cols, mc = cols - 1, chunks = a.chunks;
+    const int64_t n = static_cast<int64_t>(mc) * chunks;
     const int32_t *cnt = a.col_cnt + static_cast<int64_t>(f) * n;
     int32_t *base = a.col_base + static_cast<int64_t>(f) * n;
     if (tid == 0) carry = 0;
     __syncthreads();
     // (a frame's count < 2^29: 32-bit sums)
-    for (int64_t s0 = 0; s0 < n; s0 += kPer * 1024) {
-        uint32_t c[kPer], sum = 0;
-        int64_t at[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int64_t s = s0 + kPer * tid + k;
-            // entries of columns outside [1, cols-3] were never written: treat them as 0
-            const int col = static_cast<int>(s / a.chunks), chunk = static_cast<int>(s - static_cast<int64_t>(col) * a.chunks);
-            at[k] = s < n ? static_cast<int64_t>(chunk) * mc + col : -1;  // (chunk, column) layout
-            c[k] = (s < n && col >= 1 && col <= a.cols - 3) ? static_cast<uint32_t>(cnt[at[k]]) : 0u;
-            sum += c[k];
+    for (int c0 = 0; c0 < mc; c0 += 1024) {
+        const int col = c0 + tid;
+        uint32_t tot = 0;
+        if (col >= 1 && col <= cols - 3) {  // (other columns were never counted)
+#pragma unroll 8
+            for (int k = 0; k < chunks; ++k) tot += static_cast<uint32_t>(cnt[static_cast<int64_t>(k) * mc + col]);
         }
-        const uint32_t incl = wave_incl_add(sum);
+        const uint32_t incl = wave_incl_add(tot);
         if (lane == kWave - 1) wsum[wv] = incl;
         __syncthreads();
-        uint32_t run = carry + incl - sum;
+        uint32_t run = carry + incl - tot;
         for (int q = 0; q < wv; ++q) run += wsum[q];
         __syncthreads();  // everyone has read carry and wsum
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            if (at[k] >= 0) base[at[k]] = static_cast<int32_t>(run);
-            run += c[k];
-        }
-        if (tid == 1023) carry = run;
+        if (col < mc) base[col] = static_cast<int32_t>(run);
+        if (tid == 1023) carry = run + tot;
         __syncthreads();
     }
     if (tid == 0) a.counts[f] = carry;
