@@ -263,6 +263,7 @@ struct LsdArgs {
     uint32_t *rowbits;  // [batch][chunks][words][cols-1]: valid rows of each (column, chunk), bit r - r0
                         // (column fastest: a wave's stores and loads are contiguous)
     int words;          // ceil(chunk_h / 32)
+    int chunk_fastest;  // k_lsd_map wave order: chunk index fastest (else strip fastest)
     int32_t *col_cnt;   // [batch][chunks][cols-1]
     int32_t *col_base;  // same layout, exclusive scan in column-major order (column outer, chunk inner)
     int32_t *idx;

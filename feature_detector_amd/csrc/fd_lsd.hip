@@ -363,10 +363,19 @@ template <bool ALIGNED>
 __global__ __launch_bounds__(256) void k_lsd_map(LsdArgs a) {
     __shared__ LsdQueue Q;
     int w = __builtin_amdgcn_readfirstlane(logical_block() * 4 + (threadIdx.x >> 6));
-    const int strip = w % a.strips4;
-    w /= a.strips4;
-    const int chunk = w % a.chunks;
-    const int f = w / a.chunks;
+    int strip, chunk;
+    if (a.chunk_fastest) {
+        chunk = w % a.chunks;
+        w /= a.chunks;
+        strip = w % a.strips4;
+        w /= a.strips4;
+    } else {
+        strip = w % a.strips4;
+        w /= a.strips4;
+        chunk = w % a.chunks;
+        w /= a.chunks;
+    }
+    const int f = w;
     if (f >= a.batch) return;
     if (strip * 256 >= 1 && strip * 256 + 255 <= a.cols - 3) lsd_map_tile<ALIGNED, true>(a, f, strip, chunk, Q);
     else lsd_map_tile<ALIGNED, false>(a, f, strip, chunk, Q);

@@ -882,11 +882,18 @@ void lsd_geometry(fdk::LsdArgs &a, int batch, int rows, int cols, const uint8_t 
     a.strips4 = (cols - 1 + 255) / 256;
     a.aligned4 = (cols % 4 == 0) && (reinterpret_cast<uintptr_t>(dframes) % 4 == 0);
     a.pitch = cols - 1;  // dense maps: unpitched unless the caller gives a pitch (fd_lsd_map_pitched)
-    int64_t target = 32768;  // waves of the map kernel (with nt map stores: map + scan + scatter 1.56-1.57 -> 1.54 ms vs 16384)
-    if (const char *e = ab_env("FD_LSD_WAVES")) target = std::max<int64_t>(64, std::atoll(e));  // A/B
-    int64_t ch = (static_cast<int64_t>(batch) * a.strips4 * work_rows) / target;
-    ch = std::max<int64_t>(16, std::min<int64_t>(ch, 256));
+    // k_lsd_map chunks of 32 rows (one row-bit word per (column, chunk)), consecutive waves taking consecutive
+    // chunks of a strip: the shortest chunks whose scatter stays on its one-pass path (chunks <= 64 at 1080p);
+    // 1080p x256 map + scan + scatter 1.514 -> 1.469 ms against 67-row chunks strip-fastest
+    // (profiles/r06_lsd_rows.txt). 16 rows when 32 would leave fewer than 4096 waves (small batches).
+    int64_t ch = static_cast<int64_t>(batch) * a.strips4 * ((work_rows + 31) / 32) < 4096 ? 16 : 32;
+    a.chunk_fastest = 1;
+    if (const char *e = ab_env("FD_LSD_WAVES"))  // A/B: rows per chunk from a target wave count
+        ch = std::max<int64_t>(16, std::min<int64_t>(static_cast<int64_t>(batch) * a.strips4 * work_rows /
+                                                         std::max<int64_t>(64, std::atoll(e)), 256));
+    if (const char *e = ab_env("FD_LSD_CH")) ch = std::max(16, std::min(256, std::atoi(e)));  // A/B
     a.chunk_h = static_cast<int>(ch);
+    if (const char *e = ab_env("FD_LSD_ORDER")) a.chunk_fastest = std::atoi(e);  // A/B
     a.chunks = (work_rows + a.chunk_h - 1) / a.chunk_h;
     a.words = (a.chunk_h + 31) / 32;
 }
