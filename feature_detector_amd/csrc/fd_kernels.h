@@ -254,7 +254,7 @@ struct LsdArgs {
     const uint8_t *frames;
     int batch, rows, cols;
     int strips, chunks, chunk_h;
-    int strips4;   // k_lsd_map strips of 256 columns (4 per lane); strips: 64-column strips (scatter)
+    int strips4;   // k_lsd_map strips of 256 columns (4 per lane); strips: 64-column strips
     int aligned4;  // cols % 4 == 0 and 4-byte aligned frames: whole-dword row loads
     float min_norm;
     float *norm, *angle;
@@ -264,6 +264,7 @@ struct LsdArgs {
                         // (column fastest: a wave's stores and loads are contiguous)
     int words;          // ceil(chunk_h / 32)
     int chunk_fastest;  // k_lsd_map wave order: chunk index fastest (else strip fastest)
+    int scatter_cols;   // k_lsd_scatter columns per wave (16, 32 or 64)
     int32_t *col_cnt;   // [batch][chunks][cols-1]
     int32_t *col_base;  // same layout, exclusive scan in column-major order (column outer, chunk inner)
     int32_t *idx;

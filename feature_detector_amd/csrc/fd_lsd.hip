@@ -422,14 +422,16 @@ __global__ __launch_bounds__(1024) void k_lsd_scan(LsdArgs a) {
 // pass 1 (a few words per lane instead of re-reading the valid map row by row).
 // Pass 3: the column-major valid list. The list holds each column's valid rows in order, chunk after
 // chunk, so one column's entries (all chunks) are one contiguous run starting at its chunk-0 base. A wave
-// owns 64 columns and writes them one column at a time: its lanes take the column's (chunk, row word)
+// owns NC columns and writes them one column at a time: its lanes take the column's (chunk, row word)
 // items in row order, a wave prefix of their popcounts places every lane's entries inside the run, so
 // each store instruction covers a few adjacent cache lines (a lane per column, as before, made every
 // store touch 64 lines; the row-bit words of adjacent columns share lines, so the per-column loads hit
 // L1 after the first column of a line).
+template <int NC>
 __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     const int w4 = static_cast<int>(blockIdx.x) * 4 + (static_cast<int>(threadIdx.x) >> 6);
-    const int strip = __builtin_amdgcn_readfirstlane(w4 % a.strips), f = __builtin_amdgcn_readfirstlane(w4 / a.strips);
+    const int nstrips = (a.cols - 1 + NC - 1) / NC;
+    const int strip = __builtin_amdgcn_readfirstlane(w4 % nstrips), f = __builtin_amdgcn_readfirstlane(w4 / nstrips);
     if (f >= a.batch) return;
     const int lane = lane_id();
     const int rows = a.rows, cols = a.cols, mc = cols - 1, words = a.words, chunks = a.chunks;
@@ -439,8 +441,8 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     const uint32_t *fbits = a.rowbits + static_cast<int64_t>(f) * chunks * words * mc;
     int32_t *out = a.frame_base ? a.idx + a.frame_base[f] : a.idx + static_cast<int64_t>(f) * a.idx_cap;
     const int64_t cap = a.frame_base ? INT64_MAX : a.idx_cap;
-    // the 64 columns' run starts (lane = column), read once
-    const int coll = strip * kWave + lane;
+    // the NC columns' run starts (lane = column), read once
+    const int coll = lane < NC ? strip * NC + lane : -1;
     const int64_t basel = coll >= 1 && coll <= cols - 3 ? cbase[coll] : 0;
     auto put = [&](int col, int i, uint32_t m, int64_t &run) {
         const int c = i / words, w = i - c * words;
@@ -465,27 +467,28 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
     if (items <= kWave) {
         // the wave's row-bit words, [item][column], read row by row (lane = column: 256 contiguous bytes per
         // load) into LDS, 16 loads in flight; then one item per lane and column from LDS
-        __shared__ uint32_t sb[4][kWave][kWave + 1];
-        uint32_t(*const wb)[kWave + 1] = sb[threadIdx.x >> 6];
+        __shared__ uint32_t sb[4][kWave][NC + 1];
+        uint32_t(*const wb)[NC + 1] = sb[threadIdx.x >> 6];
         for (int i0 = 0; i0 < items; i0 += 16) {
             uint32_t v[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) v[k] = word(coll, i0 + k);
 #pragma unroll
             for (int k = 0; k < 16; ++k)
-                if (i0 + k < kWave) wb[i0 + k][lane] = v[k];
+                if (i0 + k < kWave && lane < NC) wb[i0 + k][lane] = v[k];
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         constexpr int kG = 8;
-        for (int g = 0; g < kWave; g += kG) {
+        static_assert(NC % kG == 0, "whole column groups");
+        for (int g = 0; g < NC; g += kG) {
             uint32_t mv[kG];
 #pragma unroll
             for (int k = 0; k < kG; ++k) mv[k] = lane < items ? wb[lane][g + k] : 0u;
 #pragma unroll
             for (int k = 0; k < kG; ++k) {
-                const int col = strip * kWave + g + k;
+                const int col = strip * NC + g + k;
                 if (col < 1 || col > cols - 3) continue;  // (wave-uniform)
                 const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(basel), g + k));
                 const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(basel >> 32), g + k));
@@ -495,8 +498,8 @@ __global__ __launch_bounds__(256) void k_lsd_scatter(LsdArgs a) {
         }
         return;
     }
-    for (int cc = 0; cc < kWave; ++cc) {
-        const int col = strip * kWave + cc;
+    for (int cc = 0; cc < NC; ++cc) {
+        const int col = strip * NC + cc;
         if (col < 1 || col > cols - 3) continue;  // (wave-uniform)
         int64_t run = cbase[col];
         for (int i0 = 0; i0 < items; i0 += kWave) put(col, i0 + lane, word(col, i0 + lane), run);
@@ -539,6 +542,21 @@ __global__ __launch_bounds__(64) void k_lsd_frames(const int64_t *counts, int ba
 
 }  // namespace
 
+namespace {
+
+// k_lsd_scatter with a.scatter_cols columns per wave (32; 16 or 64 for A/B)
+hipError_t launch_scatter(const LsdArgs &a, hipStream_t s) {
+    const int nc = a.scatter_cols == 64 ? 64 : a.scatter_cols == 16 ? 16 : 32;
+    const int64_t waves = static_cast<int64_t>(a.batch) * ((a.cols - 1 + nc - 1) / nc);
+    const dim3 grid(static_cast<unsigned>((waves + 3) / 4)), block(256);
+    if (nc == 64) hipLaunchKernelGGL(k_lsd_scatter<64>, grid, block, 0, s, a);
+    else if (nc == 16) hipLaunchKernelGGL(k_lsd_scatter<16>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_lsd_scatter<32>, grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
 hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s) {
     const int64_t mwaves = static_cast<int64_t>(a.batch) * a.chunks * a.strips4;
     const dim3 mgrid(static_cast<unsigned>((mwaves + 3) / 4)), block(256);
@@ -554,9 +572,7 @@ hipError_t launch_lsd_count(const LsdArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_lsd_scatter(const LsdArgs &a, hipStream_t s) {
-    const int64_t waves = static_cast<int64_t>(a.batch) * a.strips;
-    hipLaunchKernelGGL(k_lsd_scatter, dim3(static_cast<unsigned>((waves + 3) / 4)), dim3(256), 0, s, a);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launch_scatter(a, s);
     if (e != hipSuccess || !a.frame_base || a.idx_cap <= 0) return e;
     // compact mode: idx_cap = the batch's total number of entries (frame_base[batch])
     hipLaunchKernelGGL(k_lsd_values, dim3(static_cast<unsigned>((a.idx_cap + 255) / 256)), dim3(256), 0, s, a, a.idx_cap);
@@ -564,10 +580,8 @@ hipError_t launch_lsd_scatter(const LsdArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_lsd(const LsdArgs &a, hipStream_t s) {
-    const int64_t waves = static_cast<int64_t>(a.batch) * a.chunks * a.strips;
-    const dim3 grid(static_cast<unsigned>((waves + 3) / 4)), block(256);
     const int64_t mwaves = static_cast<int64_t>(a.batch) * a.chunks * a.strips4;
-    const dim3 mgrid(static_cast<unsigned>((mwaves + 3) / 4));
+    const dim3 mgrid(static_cast<unsigned>((mwaves + 3) / 4)), block(256);
     if (a.aligned4) hipLaunchKernelGGL(k_lsd_map<true>, mgrid, block, 0, s, a);
     else hipLaunchKernelGGL(k_lsd_map<false>, mgrid, block, 0, s, a);
     hipError_t e = hipGetLastError();
@@ -575,9 +589,7 @@ hipError_t launch_lsd(const LsdArgs &a, hipStream_t s) {
     hipLaunchKernelGGL(k_lsd_scan, dim3(a.batch), dim3(1024), 0, s, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lsd_scatter, dim3(static_cast<unsigned>((static_cast<int64_t>(a.batch) * a.strips + 3) / 4)),
-                       block, 0, s, a);
-    return hipGetLastError();
+    return launch_scatter(a, s);
 }
 
 }  // namespace fdk

@@ -894,6 +894,8 @@ void lsd_geometry(fdk::LsdArgs &a, int batch, int rows, int cols, const uint8_t 
     if (const char *e = ab_env("FD_LSD_CH")) ch = std::max(16, std::min(256, std::atoi(e)));  // A/B
     a.chunk_h = static_cast<int>(ch);
     if (const char *e = ab_env("FD_LSD_ORDER")) a.chunk_fastest = std::atoi(e);  // A/B
+    a.scatter_cols = 32;  // scatter 116 -> 111 us dense, 106 -> 99 us compact vs 64 (16: 130 / 124; r06_lsd_rows.txt)
+    if (const char *e = ab_env("FD_LSD_SC")) a.scatter_cols = std::atoi(e);  // A/B: 16, 32 or 64
     a.chunks = (work_rows + a.chunk_h - 1) / a.chunk_h;
     a.words = (a.chunk_h + 31) / 32;
 }
